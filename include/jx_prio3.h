@@ -1,0 +1,148 @@
+/*
+ * jx_prio3.h — C ABI of the MI355X batched Prio3 helper prepare + aggregate engine.
+ *
+ * Drop-in boundary. In Janus the hot path is reached through the
+ * `prio::vdaf::Aggregator<16, 16>` trait + `PingPongTopology`, called once per
+ * report from the helper's aggregate-init loop:
+ *   /root/reference/aggregator/src/aggregator.rs:1945-1967
+ *     vdaf.helper_initialized(verify_key, agg_param, nonce = report_id,
+ *                             public_share, input_share, leader_msg).evaluate(vdaf)
+ * and the per-report accumulation
+ *   /root/reference/aggregator/src/aggregator/aggregation_job_writer.rs:608-708
+ *   /root/reference/aggregator_core/src/datastore/models.rs:1275-1330 (merged_with)
+ * plus the shard merge of compute_aggregate_share
+ *   /root/reference/aggregator/src/aggregator/aggregate_share.rs:55-96.
+ * This ABI replaces that loop body with one call per batch. HPKE-open, plaintext
+ * decode, replay / collected-batch checks and the datastore stay on the host.
+ *
+ * Conventions:
+ *  - Every function returns int32 status: 0 = OK, < 0 = engine error (JX_E_*).
+ *    Per-report preparation failures are NOT errors: they are verdict bytes.
+ *  - The caller owns every host buffer; it is borrowed for the duration of the call.
+ *  - An engine owns its device memory and one HIP stream on one device. Engines are
+ *    not re-entrant: serialize calls per engine; use one engine per GPU.
+ *  - Byte layouts are the DAP/VDAF encodings (fixed stride per report):
+ *      nonces               n x 16   (report ids; VDAF nonce, aggregator.rs:1951)
+ *      public_shares        n x PS   (Prio3PublicShare: joint-rand parts, 0 or 32 B)
+ *      helper_input_shares  n x HIS  (k_meas || k_proofs || [k_blind])
+ *      leader_prep_shares   n x LPS  (the prep_share inside PingPongMessage::Initialize)
+ *      prep_msgs            n x PM   (prep_msg inside PingPongMessage::Finish; 0 or 16 B)
+ *      output shares        n x OUT x FB, aggregate shares OUT x FB, field elements LE.
+ */
+#ifndef JX_PRIO3_H
+#define JX_PRIO3_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes */
+#define JX_OK 0
+#define JX_E_INVALID (-1)     /* bad argument */
+#define JX_E_UNSUPPORTED (-2) /* parameter set not supported by the engine */
+#define JX_E_HIP (-3)         /* HIP runtime error (see jx_last_error) */
+#define JX_E_NOMEM (-4)       /* device allocation failed */
+#define JX_E_STATE (-5)       /* call out of order (e.g. accumulate without a prepared batch) */
+#define JX_E_NODEVICE (-6)
+
+/* Verdict bytes. Labels match handle_ping_pong_error, aggregator/src/aggregator/error.rs:379-424;
+ * every non-zero verdict goes on the wire as PrepareError::VdafPrepError (messages/src/lib.rs:2344). */
+#define JX_FINISHED 0
+#define JX_PREPARE_INIT_FAILURE 1          /* PingPongError::VdafPrepareInit */
+#define JX_PREP_SHARE_DECODE_FAILURE 2     /* PingPongError::CodecPrepShare (leader share malformed) */
+#define JX_PREPARE_MESSAGE_FAILURE 3       /* PingPongError::VdafPrepareSharesToPrepareMessage */
+#define JX_PREPARE_NEXT_FAILURE 4          /* PingPongError::VdafPrepareNext */
+
+/* Prio3 instance, mirroring janus_core::vdaf::VdafInstance (core/src/vdaf.rs:65-108).
+ * algo_id: 0 Prio3Count, 1 Prio3Sum{bits}, 2 Prio3SumVec{bits,length,chunk_length},
+ *          3 Prio3Histogram{length,chunk_length}  (== Prio3 algorithm ids, messages/src/taskprov.rs:358-363)
+ * num_proofs must be 1 (all TurboSHAKE Prio3 variants Janus dispatches, core/src/vdaf.rs:203-262). */
+typedef struct {
+  uint32_t algo_id;
+  uint32_t bits;
+  uint32_t length;
+  uint32_t chunk_length;
+  uint32_t num_proofs;
+} jx_prio3_params;
+
+typedef struct jx_engine jx_engine;
+
+/* Create an engine for one Prio3 instance and one verify key (VERIFY_KEY_LENGTH = 16,
+ * core/src/vdaf.rs:16) on HIP device `device`. */
+int32_t jx_engine_create(const jx_prio3_params* params, const uint8_t verify_key[16], int32_t device,
+                         jx_engine** out);
+void jx_engine_destroy(jx_engine* e);
+
+/* Encoded sizes (bytes) for this instance. Any pointer may be NULL. */
+int32_t jx_engine_sizes(const jx_engine* e, uint32_t* public_share, uint32_t* helper_input_share,
+                        uint32_t* leader_prep_share, uint32_t* prep_msg, uint32_t* output_len,
+                        uint32_t* field_bytes);
+
+/* Reserve staging for `reports` reports (two-phase API needs n <= capacity; grows on demand). */
+int32_t jx_engine_set_capacity(jx_engine* e, uint64_t reports);
+
+/* Batched helper_initialized + evaluate for n reports (host buffers).
+ * out_verdicts[n] receives JX_FINISHED or a failure code; out_prep_msgs[n x PM] the outbound
+ * Finish{prep_msg} payload (meaningful where verdict == JX_FINISHED); out_output_shares
+ * (nullable) the output shares. Output shares stay resident for jx_accumulate. */
+int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
+                             const uint8_t* helper_input_shares, const uint8_t* leader_prep_shares,
+                             uint8_t* out_prep_msgs, uint8_t* out_verdicts, uint8_t* out_output_shares);
+
+/* Accumulate the output shares of the last jx_helper_prep_batch into batch aggregations:
+ * report i is added iff verdict == FINISHED and accept_mask[i] != 0 (accept_mask nullable = all),
+ * into aggregation `segment[i]` (segment nullable = 0). Adds to the aggregate share, the
+ * report count and the ReportIdChecksum (XOR of SHA-256(report id)). */
+int32_t jx_accumulate(jx_engine* e, uint64_t n, const uint8_t* accept_mask, const uint32_t* segment);
+
+/* Fused prep + accumulate (the metric's unit of work): prepare n reports and add every
+ * finished one into aggregation `segment`. Host buffers; processed in capacity-sized chunks.
+ * out_prep_msgs / out_verdicts nullable. */
+int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
+                                 const uint8_t* helper_input_shares, const uint8_t* leader_prep_shares,
+                                 uint32_t segment, uint8_t* out_prep_msgs, uint8_t* out_verdicts);
+
+/* Same with DEVICE pointers (inputs already resident in HBM, e.g. from a torch tensor).
+ * d_out_prep_msgs / d_out_verdicts are device pointers (nullable). Asynchronous on the
+ * engine stream; call jx_engine_sync before reading results. */
+int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_nonces, const void* d_public_shares,
+                                        const void* d_helper_input_shares, const void* d_leader_prep_shares,
+                                        uint32_t segment, void* d_out_prep_msgs, void* d_out_verdicts);
+
+/* Read aggregation `segment`: encoded aggregate share (OUT x FB, LE), report count, checksum. */
+int32_t jx_aggregate_read(jx_engine* e, uint32_t segment, uint8_t* out_agg, uint64_t* count);
+int32_t jx_aggregate_checksum(jx_engine* e, uint32_t segment, uint8_t out_checksum[32]);
+/* Zero every aggregation. */
+int32_t jx_aggregate_reset(jx_engine* e);
+
+/* Multi-GPU combine (compute_aggregate_share, aggregate_share.rs:87-95): write the encoded
+ * aggregate share of `segment` to device buffer d_dst (OUT x FB bytes), and sum `nparts`
+ * encoded shares laid out back to back at d_parts into d_out (mod p; RCCL's sum is not
+ * field addition). Both asynchronous on the engine stream. */
+int32_t jx_aggregate_export_device(jx_engine* e, uint32_t segment, void* d_dst);
+int32_t jx_aggregate_combine_device(jx_engine* e, const void* d_parts, uint32_t nparts, void* d_out);
+
+/* Wait for all work on the engine stream. */
+int32_t jx_engine_sync(jx_engine* e);
+/* The engine's HIP stream (hipStream_t), for callers that order their own work after it. */
+int32_t jx_engine_stream(jx_engine* e, void** stream);
+
+/* Kernel timing with HIP events recorded on the engine stream around each stage.
+ * enable != 0 starts collecting (and clears the totals). ms[0] = XOF stage (K1),
+ * ms[1] = FLP stage (K3), ms[2] = accumulate (K4), ms[3] = slow-path kernel;
+ * launches[0..3] = launch counts. Reading synchronizes the stream. */
+int32_t jx_engine_timing(jx_engine* e, int32_t enable);
+int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]);
+
+/* Debug knobs (tests only): option 1 = route every report through the slow XOF kernel. */
+int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value);
+
+const char* jx_status_str(int32_t status);
+const char* jx_last_error(const jx_engine* e);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JX_PRIO3_H */

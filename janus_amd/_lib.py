@@ -1,0 +1,83 @@
+"""Loader for the in-tree HIP engine library (libjanus_prio3.so, C ABI in include/jx_prio3.h).
+
+There is no CPU fallback: if the library is missing or no HIP device is present,
+every engine entry point raises. Build with ``python -m janus_amd.build``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libjanus_prio3.so")
+
+# Every symbol include/jx_prio3.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "jx_engine_create", "jx_engine_destroy", "jx_engine_sizes", "jx_engine_set_capacity",
+    "jx_helper_prep_batch", "jx_accumulate", "jx_helper_prep_aggregate", "jx_helper_prep_aggregate_device",
+    "jx_aggregate_read", "jx_aggregate_checksum", "jx_aggregate_reset", "jx_aggregate_export_device",
+    "jx_aggregate_combine_device", "jx_engine_sync", "jx_engine_stream", "jx_engine_timing",
+    "jx_engine_timing_read", "jx_engine_debug", "jx_status_str", "jx_last_error",
+)
+
+_lib = None
+
+
+class JxParams(ctypes.Structure):
+    _fields_ = [("algo_id", ctypes.c_uint32), ("bits", ctypes.c_uint32), ("length", ctypes.c_uint32),
+                ("chunk_length", ctypes.c_uint32), ("num_proofs", ctypes.c_uint32)]
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the shared library and declare exact argument types (fails loudly)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise EngineError(f"{LIB_PATH} is missing: build it with `python -m janus_amd.build` "
+                          "(there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u8p = ctypes.c_void_p, ctypes.c_void_p
+    i32, u32, u64 = ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
+    P = ctypes.POINTER
+    sig = {
+        "jx_engine_create": (i32, [P(JxParams), u8p, i32, P(vp)]),
+        "jx_engine_destroy": (None, [vp]),
+        "jx_engine_sizes": (i32, [vp, P(u32), P(u32), P(u32), P(u32), P(u32), P(u32)]),
+        "jx_engine_set_capacity": (i32, [vp, u64]),
+        "jx_helper_prep_batch": (i32, [vp, u64, u8p, u8p, u8p, u8p, u8p, u8p, u8p]),
+        "jx_accumulate": (i32, [vp, u64, u8p, u8p]),
+        "jx_helper_prep_aggregate": (i32, [vp, u64, u8p, u8p, u8p, u8p, u32, u8p, u8p]),
+        "jx_helper_prep_aggregate_device": (i32, [vp, u64, vp, vp, vp, vp, u32, vp, vp]),
+        "jx_aggregate_read": (i32, [vp, u32, u8p, P(u64)]),
+        "jx_aggregate_checksum": (i32, [vp, u32, u8p]),
+        "jx_aggregate_reset": (i32, [vp]),
+        "jx_aggregate_export_device": (i32, [vp, u32, vp]),
+        "jx_aggregate_combine_device": (i32, [vp, vp, u32, vp]),
+        "jx_engine_sync": (i32, [vp]),
+        "jx_engine_stream": (i32, [vp, P(vp)]),
+        "jx_engine_timing": (i32, [vp, i32]),
+        "jx_engine_timing_read": (i32, [vp, P(ctypes.c_float), P(u64)]),
+        "jx_engine_debug": (i32, [vp, i32, ctypes.c_int64]),
+        "jx_status_str": (ctypes.c_char_p, [i32]),
+        "jx_last_error": (ctypes.c_char_p, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(status: int, engine_ptr=None, what: str = "") -> None:
+    if status == 0:
+        return
+    L = load()
+    msg = L.jx_status_str(status).decode()
+    detail = L.jx_last_error(engine_ptr).decode() if engine_ptr else ""
+    raise EngineError(f"{what}: {msg} ({status}) {detail}".strip())

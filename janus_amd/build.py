@@ -1,0 +1,54 @@
+"""Build the gfx950 engine library in-tree: janus_amd/lib/libjanus_prio3.so.
+
+hipcc cross-compiles for gfx950 without a GPU. Run: ``python -m janus_amd.build``.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+SOURCES = [os.path.join(_HERE, "csrc", f) for f in ("jx_kernels.hip", "jx_engine.cpp")]
+HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("jx_field.h", "jx_keccak.h", "jx_sha256.h", "jx_kernels.h")]
+OUT = os.path.join(_HERE, "lib", "libjanus_prio3.so")
+ARCH = os.environ.get("JX_OFFLOAD_ARCH", "gfx950")
+
+
+def _stale() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = SOURCES + HEADERS + [os.path.join(_HERE, "..", "include", "jx_prio3.h")]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    objs = []
+    # compile the two translation units in parallel
+    procs = []
+    for src in SOURCES:
+        obj = os.path.join(os.path.dirname(OUT), os.path.basename(src) + ".o")
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-x", "hip", "-c", src, "-o", obj]
+        procs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), cmd))
+        objs.append(obj)
+    for p, cmd in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            sys.stderr.write(out.decode())
+            raise RuntimeError(f"hipcc failed: {' '.join(cmd)}")
+        if verbose and out:
+            sys.stderr.write(out.decode())
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs
+    subprocess.run(cmd, check=True)
+    for o in objs:
+        os.remove(o)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,763 @@
+// jx_engine.cpp — host side of the C ABI in include/jx_prio3.h.
+//
+// Owns device staging, constant tables and per-segment batch aggregations; sequences
+// the K1 (XOF) -> K1' (slow path) -> K3 (FLP) -> K4 (accumulate) launches on one HIP
+// stream per engine. There is no CPU compute path: if the device or the kernels are
+// unavailable every entry point fails with an error status.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../../include/jx_prio3.h"
+#include "jx_field.h"
+#include "jx_kernels.h"
+
+using namespace jx;
+
+namespace {
+
+struct Segment {
+  uint4* agg = nullptr;                 // [out_len] canonical
+  uint32_t* checksum = nullptr;         // [8]
+  unsigned long long* count = nullptr;  // [1]
+};
+
+enum { ST_XOF = 0, ST_FLP = 1, ST_ACC = 2, ST_SLOW = 3, NST = 4 };
+
+}  // namespace
+
+struct jx_engine {
+  Cfg cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint64_t cap = 0;  // reports (multiple of 64)
+  uint64_t default_chunk = 0;
+  // inputs (engine-owned copies for host entry points)
+  uint8_t *d_nonces = nullptr, *d_ps = nullptr, *d_his = nullptr, *d_lps = nullptr;
+  // staging
+  uint4 *d_meas = nullptr, *d_proof = nullptr, *d_outs = nullptr, *d_coef = nullptr, *d_consts = nullptr;
+  uint32_t* d_flags = nullptr;
+  uint8_t *d_verdicts = nullptr, *d_msgs = nullptr;
+  // accumulation scratch: partials + selection bytes
+  uint64_t* d_partials = nullptr;
+  uint32_t acc_chunks = 16;
+  uint8_t* d_tmp = nullptr;  // output-share transpose / aggregate encode
+  size_t tmp_bytes = 0;
+  uint8_t* d_mask = nullptr;
+  uint32_t* d_seg = nullptr;
+  std::map<uint32_t, Segment> segs;
+  uint64_t last_n = 0;
+  bool have_batch = false;
+  // the nonces of the resident batch (device pointer; engine copy or caller's)
+  const uint8_t* batch_nonces = nullptr;
+  // timing
+  bool timing = false;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  double ms[NST] = {0, 0, 0, 0};
+  uint64_t launches[NST] = {0, 0, 0, 0};
+  uint32_t force_slow = 0;
+  std::string err;
+};
+
+static int32_t fail(jx_engine* e, int32_t code, const std::string& msg) {
+  if (e) e->err = msg;
+  return code;
+}
+#define HIPCHK(e, call)                                                                                   \
+  do {                                                                                                    \
+    hipError_t _st = (call);                                                                              \
+    if (_st != hipSuccess)                                                                                \
+      return fail((e), _st == hipErrorOutOfMemory ? JX_E_NOMEM : JX_E_HIP,                                \
+                  std::string(#call) + ": " + hipGetErrorString(_st));                                    \
+  } while (0)
+
+// ---------------------------------------------------------------------------- host field helpers
+
+static f128 h_mpow(f128 aR, uint64_t e) {
+  f128 r = make128(R1_128_LO, R1_128_HI);
+  while (e) {
+    if (e & 1) r = mont128(r, aR);
+    aR = mont128(aR, aR);
+    e >>= 1;
+  }
+  return r;
+}
+static f128 h_minv(f128 aR) {
+  // exponent p - 2 = 0xFFFFFFFFFFFFFFE3_FFFFFFFFFFFFFFFF, square-and-multiply from the top bit
+  const uint64_t ehi = 0xFFFFFFFFFFFFFFE3ull, elo = 0xFFFFFFFFFFFFFFFFull;
+  f128 r = make128(R1_128_LO, R1_128_HI);
+  for (int i = 127; i >= 0; i--) {
+    r = mont128(r, r);
+    uint64_t bit = i >= 64 ? (ehi >> (i - 64)) & 1 : (elo >> i) & 1;
+    if (bit) r = mont128(r, aR);
+  }
+  return r;
+}
+static uint4 h_u4(f128 a) {
+  uint4 v;
+  v.x = lo32(a.lo);
+  v.y = hi32(a.lo);
+  v.z = lo32(a.hi);
+  v.w = hi32(a.hi);
+  return v;
+}
+static f128 h_from_u64(uint64_t v) { return make128(v, 0); }
+
+static int next_pow2(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+static int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) l++;
+  return l;
+}
+
+namespace jx {
+int psum_ppw(uint32_t chunk);
+}
+
+// ---------------------------------------------------------------------------- configuration
+
+static int32_t make_cfg(const jx_prio3_params* p, const uint8_t vk[16], Cfg& c, std::string& why) {
+  memset(&c, 0, sizeof c);
+  if (p->num_proofs != 1) {
+    why = "num_proofs must be 1";
+    return JX_E_UNSUPPORTED;
+  }
+  c.algo = p->algo_id;
+  c.bits = p->bits;
+  c.length = p->length;
+  c.chunk = p->chunk_length;
+  uint32_t arity = 0;
+  switch (p->algo_id) {
+    case ALGO_COUNT:
+      c.meas_len = 1;
+      c.out_len = 1;
+      c.jr_len = 0;
+      c.calls = 1;
+      arity = 2;
+      break;
+    case ALGO_SUM:
+      if (p->bits < 1 || p->bits > 32) {
+        why = "Prio3Sum bits must be in [1, 32]";
+        return JX_E_UNSUPPORTED;
+      }
+      c.meas_len = p->bits;
+      c.out_len = 1;
+      c.jr_len = 1;
+      c.calls = p->bits;
+      arity = 1;
+      break;
+    case ALGO_SUMVEC:
+      if (p->bits < 1 || p->bits > 32 || p->length < 1 || p->chunk_length < 1) {
+        why = "Prio3SumVec needs 1 <= bits <= 32, length >= 1, chunk_length >= 1";
+        return JX_E_UNSUPPORTED;
+      }
+      c.meas_len = p->bits * p->length;
+      c.out_len = p->length;
+      c.jr_len = 1;
+      c.calls = (c.meas_len + p->chunk_length - 1) / p->chunk_length;
+      arity = 2 * p->chunk_length;
+      break;
+    case ALGO_HISTOGRAM:
+      if (p->length < 1 || p->chunk_length < 1) {
+        why = "Prio3Histogram needs length >= 1, chunk_length >= 1";
+        return JX_E_UNSUPPORTED;
+      }
+      c.meas_len = p->length;
+      c.out_len = p->length;
+      c.jr_len = 2;
+      c.calls = (p->length + p->chunk_length - 1) / p->chunk_length;
+      arity = 2 * p->chunk_length;
+      c.out_is_meas = 1;
+      break;
+    default:
+      why = "unknown algo_id";
+      return JX_E_INVALID;
+  }
+  if ((c.algo == ALGO_SUMVEC || c.algo == ALGO_HISTOGRAM) && psum_ppw(c.chunk) < 0) {
+    why = "chunk_length too large for the FLP kernel (<= 128 supported)";
+    return JX_E_UNSUPPORTED;
+  }
+  c.P = next_pow2(1 + c.calls);
+  c.logP = ilog2(c.P);
+  c.gpoly_len = 2 * (c.P - 1) + 1;
+  c.proof_len = arity + c.gpoly_len;
+  c.ver_len = arity + 2;
+  const uint32_t fb = c.algo == ALGO_COUNT ? 8 : 16;
+  const bool jr = c.jr_len > 0;
+  c.ps_bytes = jr ? 32 : 0;
+  c.his_bytes = jr ? 48 : 32;
+  c.lps_bytes = c.ver_len * fb + (jr ? 16 : 0);
+  if (c.algo == ALGO_COUNT)
+    c.ncoef = 0;
+  else if (c.algo == ALGO_SUM)
+    c.ncoef = COEF_K + c.calls;
+  else
+    c.ncoef = COEF_K + 2 * c.calls;
+  for (int i = 0; i < 4; i++)
+    c.vk[i] = (uint32_t)vk[4 * i] | ((uint32_t)vk[4 * i + 1] << 8) | ((uint32_t)vk[4 * i + 2] << 16) |
+              ((uint32_t)vk[4 * i + 3] << 24);
+  c.c_omega = 0;
+  c.c_S = c.P;
+  c.c_misc = c.P + c.gpoly_len;
+  return JX_OK;
+}
+
+// constant tables: w^k R (k < P), S_m R = (sum_{k=1..calls} w^{km}) R (m < gpoly_len), misc
+static std::vector<uint4> make_consts(const Cfg& c) {
+  std::vector<uint4> t(c.P + c.gpoly_len + 4);
+  if (c.algo == ALGO_COUNT) return t;
+  // GEN = 7^((p-1)/2^66), order 2^66; w = GEN^(2^(66 - logP))
+  f128 gen = h_mpow(to_mont128(h_from_u64(7)), 4611686018427387897ull);
+  f128 w = gen;
+  for (int i = 0; i < 66 - (int)c.logP; i++) w = mont128(w, w);
+  f128 wk = make128(R1_128_LO, R1_128_HI);
+  std::vector<f128> pw(c.P);
+  for (uint32_t k = 0; k < c.P; k++) {
+    pw[k] = wk;
+    t[c.c_omega + k] = h_u4(wk);
+    wk = mont128(wk, w);
+  }
+  for (uint32_t m = 0; m < c.gpoly_len; m++) {
+    f128 s = make128(0, 0);
+    for (uint32_t k = 1; k <= c.calls; k++) s = add128(s, pw[(uint64_t)(k * m) % c.P]);
+    t[c.c_S + m] = h_u4(s);
+  }
+  f128 invP = h_minv(to_mont128(h_from_u64(c.P)));
+  f128 half_m = h_minv(to_mont128(h_from_u64(2)));
+  t[c.c_misc + 0] = h_u4(invP);                     // (1/P) R
+  t[c.c_misc + 1] = h_u4(from_mont128(half_m));     // 1/2 canonical
+  t[c.c_misc + 2] = h_u4(make128(R1_128_LO, R1_128_HI));
+  t[c.c_misc + 3] = h_u4(half_m);                   // (1/2) R
+  return t;
+}
+
+// ---------------------------------------------------------------------------- buffers
+
+static void free_staging(jx_engine* e) {
+  void* ptrs[] = {e->d_nonces, e->d_ps,       e->d_his,     e->d_lps,  e->d_meas, e->d_proof, e->d_outs,
+                  e->d_coef,   e->d_flags,    e->d_verdicts, e->d_msgs, e->d_partials, e->d_mask, e->d_seg};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  e->d_nonces = e->d_ps = e->d_his = e->d_lps = nullptr;
+  e->d_meas = e->d_proof = e->d_outs = e->d_coef = nullptr;
+  e->d_flags = nullptr;
+  e->d_verdicts = e->d_msgs = nullptr;
+  e->d_partials = nullptr;
+  e->d_mask = nullptr;
+  e->d_seg = nullptr;
+  e->cap = 0;
+  e->have_batch = false;
+}
+
+static uint64_t per_report_bytes(const Cfg& c) {
+  uint64_t b = 16ull * (c.meas_len + c.proof_len + c.ncoef + (c.out_is_meas ? 0 : c.out_len));
+  b += 16 + c.ps_bytes + c.his_bytes + c.lps_bytes + 4 + 1 + 16 + 1 + 4 + 1;
+  return b;
+}
+
+static int32_t ensure_capacity(jx_engine* e, uint64_t n) {
+  if (n <= e->cap) return JX_OK;
+  free_staging(e);
+  const Cfg& c = e->cfg;
+  uint64_t cap = (n + 63) / 64 * 64;
+  auto A = [&](void** p, size_t bytes) -> hipError_t { return hipMalloc(p, bytes ? bytes : 16); };
+  HIPCHK(e, A((void**)&e->d_nonces, cap * 16));
+  HIPCHK(e, A((void**)&e->d_ps, cap * c.ps_bytes));
+  HIPCHK(e, A((void**)&e->d_his, cap * c.his_bytes));
+  HIPCHK(e, A((void**)&e->d_lps, cap * c.lps_bytes));
+  HIPCHK(e, A((void**)&e->d_meas, cap * c.meas_len * 16));
+  HIPCHK(e, A((void**)&e->d_proof, cap * c.proof_len * 16));
+  if (c.algo == ALGO_COUNT || !c.out_is_meas) HIPCHK(e, A((void**)&e->d_outs, cap * c.out_len * 16));
+  HIPCHK(e, A((void**)&e->d_coef, cap * c.ncoef * 16));
+  HIPCHK(e, A((void**)&e->d_flags, cap * 4));
+  HIPCHK(e, A((void**)&e->d_verdicts, cap));
+  HIPCHK(e, A((void**)&e->d_msgs, cap * 16));
+  HIPCHK(e, A((void**)&e->d_mask, cap));
+  HIPCHK(e, A((void**)&e->d_seg, cap * 4));
+  size_t pbytes = (size_t)e->acc_chunks * c.out_len * 3 * sizeof(uint64_t) + cap;
+  HIPCHK(e, A((void**)&e->d_partials, pbytes));
+  HIPCHK(e, hipMemsetAsync(e->d_flags, 0, cap * 4, e->stream));
+  e->cap = cap;
+  return JX_OK;
+}
+
+static int32_t get_segment(jx_engine* e, uint32_t id, Segment** out) {
+  auto it = e->segs.find(id);
+  if (it == e->segs.end()) {
+    Segment s;
+    HIPCHK(e, hipMalloc((void**)&s.agg, (size_t)e->cfg.out_len * 16));
+    HIPCHK(e, hipMalloc((void**)&s.checksum, 32));
+    HIPCHK(e, hipMalloc((void**)&s.count, 8));
+    HIPCHK(e, hipMemsetAsync(s.agg, 0, (size_t)e->cfg.out_len * 16, e->stream));
+    HIPCHK(e, hipMemsetAsync(s.checksum, 0, 32, e->stream));
+    HIPCHK(e, hipMemsetAsync(s.count, 0, 8, e->stream));
+    it = e->segs.emplace(id, s).first;
+  }
+  *out = &it->second;
+  return JX_OK;
+}
+
+static int32_t ensure_tmp(jx_engine* e, size_t bytes) {
+  if (bytes <= e->tmp_bytes) return JX_OK;
+  if (e->d_tmp) (void)hipFree(e->d_tmp);
+  e->d_tmp = nullptr;
+  e->tmp_bytes = 0;
+  HIPCHK(e, hipMalloc((void**)&e->d_tmp, bytes));
+  e->tmp_bytes = bytes;
+  return JX_OK;
+}
+
+// ---------------------------------------------------------------------------- timing
+
+static hipError_t stage_begin(jx_engine* e, hipEvent_t* ev) {
+  if (!e->timing) return hipSuccess;
+  hipError_t st = hipEventCreate(ev);
+  if (st != hipSuccess) return st;
+  return hipEventRecord(*ev, e->stream);
+}
+static hipError_t stage_end(jx_engine* e, int stage, hipEvent_t ev0) {
+  e->launches[stage]++;
+  if (!e->timing) return hipSuccess;
+  hipEvent_t ev1;
+  hipError_t st = hipEventCreate(&ev1);
+  if (st != hipSuccess) return st;
+  st = hipEventRecord(ev1, e->stream);
+  e->pending.push_back({stage, {ev0, ev1}});
+  return st;
+}
+static int32_t drain_timing(jx_engine* e) {
+  if (e->pending.empty()) return JX_OK;
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  for (auto& p : e->pending) {
+    float t = 0;
+    HIPCHK(e, hipEventElapsedTime(&t, p.second.first, p.second.second));
+    e->ms[p.first] += t;
+    (void)hipEventDestroy(p.second.first);
+    (void)hipEventDestroy(p.second.second);
+  }
+  e->pending.clear();
+  return JX_OK;
+}
+
+// ---------------------------------------------------------------------------- core sequencing
+
+// Prepare n <= cap reports whose inputs are at the given device pointers.
+static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* his,
+                         const uint8_t* lps, uint8_t* verdicts, uint8_t* msgs) {
+  const Cfg& c = e->cfg;
+  Bufs b{};
+  b.n = n;
+  b.nonces = nonces;
+  b.ps = ps;
+  b.his = his;
+  b.lps = lps;
+  b.meas = e->d_meas;
+  b.proof = e->d_proof;
+  b.outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? e->d_meas : e->d_outs;
+  b.coef = e->d_coef;
+  b.flags = e->d_flags;
+  b.verdicts = verdicts;
+  b.msgs = msgs;
+  b.consts = e->d_consts;
+  b.force_slow = e->force_slow;
+  hipEvent_t ev = nullptr;
+  if (c.algo == ALGO_COUNT) {
+    HIPCHK(e, stage_begin(e, &ev));
+    HIPCHK(e, launch_count(c, b, e->stream));
+    HIPCHK(e, stage_end(e, ST_XOF, ev));
+  } else {
+    HIPCHK(e, stage_begin(e, &ev));
+    HIPCHK(e, launch_xof(c, b, e->stream));
+    HIPCHK(e, stage_end(e, ST_XOF, ev));
+    HIPCHK(e, stage_begin(e, &ev));
+    HIPCHK(e, launch_xof_slow(c, b, e->stream));
+    HIPCHK(e, stage_end(e, ST_SLOW, ev));
+    HIPCHK(e, stage_begin(e, &ev));
+    HIPCHK(e, launch_flp(c, b, e->stream));
+    HIPCHK(e, stage_end(e, ST_FLP, ev));
+  }
+  e->batch_nonces = nonces;
+  return JX_OK;
+}
+
+static int32_t accumulate_core(jx_engine* e, uint64_t n, const uint8_t* verdicts, const uint8_t* d_mask,
+                               const uint32_t* d_seg, uint32_t seg_id) {
+  const Cfg& c = e->cfg;
+  Segment* s = nullptr;
+  int32_t rc = get_segment(e, seg_id, &s);
+  if (rc) return rc;
+  AccArgs a{};
+  a.n = n;
+  a.outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? e->d_meas : e->d_outs;
+  a.out_len = c.out_len;
+  a.verdicts = verdicts;
+  a.mask = d_mask;
+  a.seg = d_seg;
+  a.seg_id = seg_id;
+  a.partials = e->d_partials;
+  a.nchunks = e->acc_chunks;
+  uint64_t nblk = (n + 63) / 64;
+  a.blocks_per_chunk = (uint32_t)((nblk + a.nchunks - 1) / a.nchunks);
+  if (a.blocks_per_chunk == 0) a.blocks_per_chunk = 1;
+  a.nonces = e->batch_nonces;
+  a.checksum = s->checksum;
+  a.count = s->count;
+  hipEvent_t ev = nullptr;
+  HIPCHK(e, stage_begin(e, &ev));
+  HIPCHK(e, launch_accumulate(c, a, s->agg, e->stream));
+  HIPCHK(e, stage_end(e, ST_ACC, ev));
+  return JX_OK;
+}
+
+// ---------------------------------------------------------------------------- C ABI
+
+extern "C" {
+
+int32_t jx_engine_create(const jx_prio3_params* params, const uint8_t verify_key[16], int32_t device,
+                         jx_engine** out) {
+  if (!params || !verify_key || !out) return JX_E_INVALID;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return JX_E_NODEVICE;
+  if (device < 0 || device >= ndev) return JX_E_INVALID;
+  jx_engine* e = new jx_engine();
+  std::string why;
+  int32_t rc = make_cfg(params, verify_key, e->cfg, why);
+  if (rc) {
+    delete e;
+    return rc;
+  }
+  e->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete e;
+    return JX_E_HIP;
+  }
+  std::vector<uint4> consts = make_consts(e->cfg);
+  if (hipMalloc((void**)&e->d_consts, consts.size() * sizeof(uint4)) != hipSuccess ||
+      hipMemcpy(e->d_consts, consts.data(), consts.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess) {
+    jx_engine_destroy(e);
+    return JX_E_HIP;
+  }
+  // default chunk for the fused path: ~48 GiB of staging (env JX_CHUNK_REPORTS overrides)
+  uint64_t per = per_report_bytes(e->cfg);
+  uint64_t chunk = (48ull << 30) / per;
+  if (chunk > (1ull << 22)) chunk = 1ull << 22;
+  chunk = chunk / 256 * 256;
+  if (chunk < 256) chunk = 256;
+  if (const char* env = getenv("JX_CHUNK_REPORTS")) {
+    uint64_t v = strtoull(env, nullptr, 10);
+    if (v >= 64) chunk = v / 64 * 64;
+  }
+  e->default_chunk = chunk;
+  *out = e;
+  return JX_OK;
+}
+
+void jx_engine_destroy(jx_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (auto& p : e->pending) {
+    (void)hipEventDestroy(p.second.first);
+    (void)hipEventDestroy(p.second.second);
+  }
+  free_staging(e);
+  for (auto& kv : e->segs) {
+    (void)hipFree(kv.second.agg);
+    (void)hipFree(kv.second.checksum);
+    (void)hipFree(kv.second.count);
+  }
+  if (e->d_consts) (void)hipFree(e->d_consts);
+  if (e->d_tmp) (void)hipFree(e->d_tmp);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+int32_t jx_engine_sizes(const jx_engine* e, uint32_t* ps, uint32_t* his, uint32_t* lps, uint32_t* pm,
+                        uint32_t* out_len, uint32_t* fb) {
+  if (!e) return JX_E_INVALID;
+  const Cfg& c = e->cfg;
+  if (ps) *ps = c.ps_bytes;
+  if (his) *his = c.his_bytes;
+  if (lps) *lps = c.lps_bytes;
+  if (pm) *pm = c.jr_len ? 16 : 0;
+  if (out_len) *out_len = c.out_len;
+  if (fb) *fb = c.algo == ALGO_COUNT ? 8 : 16;
+  return JX_OK;
+}
+
+int32_t jx_engine_set_capacity(jx_engine* e, uint64_t reports) {
+  if (!e) return JX_E_INVALID;
+  HIPCHK(e, hipSetDevice(e->device));
+  return ensure_capacity(e, reports);
+}
+
+int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
+                             const uint8_t* helper_input_shares, const uint8_t* leader_prep_shares,
+                             uint8_t* out_prep_msgs, uint8_t* out_verdicts, uint8_t* out_output_shares) {
+  if (!e || !nonces || !helper_input_shares || !leader_prep_shares || !out_verdicts) return JX_E_INVALID;
+  const Cfg& c = e->cfg;
+  if (c.ps_bytes && !public_shares) return JX_E_INVALID;
+  if (n == 0) {
+    e->have_batch = true;
+    e->last_n = 0;
+    return JX_OK;
+  }
+  HIPCHK(e, hipSetDevice(e->device));
+  int32_t rc = ensure_capacity(e, n);
+  if (rc) return rc;
+  HIPCHK(e, hipMemcpyAsync(e->d_nonces, nonces, n * 16, hipMemcpyHostToDevice, e->stream));
+  if (c.ps_bytes) HIPCHK(e, hipMemcpyAsync(e->d_ps, public_shares, n * c.ps_bytes, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipMemcpyAsync(e->d_his, helper_input_shares, n * c.his_bytes, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipMemcpyAsync(e->d_lps, leader_prep_shares, n * c.lps_bytes, hipMemcpyHostToDevice, e->stream));
+  rc = prep_core(e, n, e->d_nonces, e->d_ps, e->d_his, e->d_lps, e->d_verdicts, e->d_msgs);
+  if (rc) return rc;
+  HIPCHK(e, hipMemcpyAsync(out_verdicts, e->d_verdicts, n, hipMemcpyDeviceToHost, e->stream));
+  if (out_prep_msgs && c.jr_len)
+    HIPCHK(e, hipMemcpyAsync(out_prep_msgs, e->d_msgs, n * 16, hipMemcpyDeviceToHost, e->stream));
+  if (out_output_shares) {
+    const uint32_t fb = c.algo == ALGO_COUNT ? 8 : 16;
+    rc = ensure_tmp(e, n * c.out_len * fb);
+    if (rc) return rc;
+    const uint4* outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? e->d_meas : e->d_outs;
+    HIPCHK(e, launch_transpose_out(c, outs, n, e->d_tmp, e->stream));
+    HIPCHK(e, hipMemcpyAsync(out_output_shares, e->d_tmp, n * c.out_len * fb, hipMemcpyDeviceToHost, e->stream));
+  }
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  e->last_n = n;
+  e->have_batch = true;
+  return drain_timing(e);
+}
+
+int32_t jx_accumulate(jx_engine* e, uint64_t n, const uint8_t* accept_mask, const uint32_t* segment) {
+  if (!e) return JX_E_INVALID;
+  if (!e->have_batch || n != e->last_n) return fail(e, JX_E_STATE, "accumulate: no prepared batch of this size");
+  if (n == 0) return JX_OK;
+  HIPCHK(e, hipSetDevice(e->device));
+  const uint8_t* dm = nullptr;
+  const uint32_t* ds = nullptr;
+  if (accept_mask) {
+    HIPCHK(e, hipMemcpyAsync(e->d_mask, accept_mask, n, hipMemcpyHostToDevice, e->stream));
+    dm = e->d_mask;
+  }
+  std::set<uint32_t> ids;
+  if (segment) {
+    HIPCHK(e, hipMemcpyAsync(e->d_seg, segment, n * 4, hipMemcpyHostToDevice, e->stream));
+    ds = e->d_seg;
+    for (uint64_t i = 0; i < n; i++) ids.insert(segment[i]);
+  } else {
+    ids.insert(0);
+  }
+  for (uint32_t id : ids) {
+    int32_t rc = accumulate_core(e, n, e->d_verdicts, dm, ds, id);
+    if (rc) return rc;
+  }
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return drain_timing(e);
+}
+
+int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
+                                 const uint8_t* helper_input_shares, const uint8_t* leader_prep_shares,
+                                 uint32_t segment, uint8_t* out_prep_msgs, uint8_t* out_verdicts) {
+  if (!e || !nonces || !helper_input_shares || !leader_prep_shares) return JX_E_INVALID;
+  const Cfg& c = e->cfg;
+  if (c.ps_bytes && !public_shares) return JX_E_INVALID;
+  HIPCHK(e, hipSetDevice(e->device));
+  const uint64_t chunk = n < e->default_chunk ? n : e->default_chunk;
+  int32_t rc = ensure_capacity(e, chunk);
+  if (rc) return rc;
+  for (uint64_t off = 0; off < n; off += chunk) {
+    const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
+    HIPCHK(e, hipMemcpyAsync(e->d_nonces, nonces + off * 16, m * 16, hipMemcpyHostToDevice, e->stream));
+    if (c.ps_bytes)
+      HIPCHK(e, hipMemcpyAsync(e->d_ps, public_shares + off * c.ps_bytes, m * c.ps_bytes, hipMemcpyHostToDevice,
+                               e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->d_his, helper_input_shares + off * c.his_bytes, m * c.his_bytes,
+                             hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->d_lps, leader_prep_shares + off * c.lps_bytes, m * c.lps_bytes,
+                             hipMemcpyHostToDevice, e->stream));
+    rc = prep_core(e, m, e->d_nonces, e->d_ps, e->d_his, e->d_lps, e->d_verdicts, e->d_msgs);
+    if (rc) return rc;
+    rc = accumulate_core(e, m, e->d_verdicts, nullptr, nullptr, segment);
+    if (rc) return rc;
+    if (out_verdicts)
+      HIPCHK(e, hipMemcpyAsync(out_verdicts + off, e->d_verdicts, m, hipMemcpyDeviceToHost, e->stream));
+    if (out_prep_msgs && c.jr_len)
+      HIPCHK(e, hipMemcpyAsync(out_prep_msgs + off * 16, e->d_msgs, m * 16, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
+  e->have_batch = false;  // staging no longer holds one whole batch
+  return drain_timing(e);
+}
+
+int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_nonces, const void* d_ps,
+                                        const void* d_his, const void* d_lps, uint32_t segment,
+                                        void* d_out_prep_msgs, void* d_out_verdicts) {
+  if (!e || !d_nonces || !d_his || !d_lps) return JX_E_INVALID;
+  const Cfg& c = e->cfg;
+  if (c.ps_bytes && !d_ps) return JX_E_INVALID;
+  HIPCHK(e, hipSetDevice(e->device));
+  const uint64_t chunk = n < e->default_chunk ? n : e->default_chunk;
+  int32_t rc = ensure_capacity(e, chunk);
+  if (rc) return rc;
+  const uint8_t *N = (const uint8_t*)d_nonces, *PS = (const uint8_t*)d_ps, *H = (const uint8_t*)d_his,
+                *L = (const uint8_t*)d_lps;
+  for (uint64_t off = 0; off < n; off += chunk) {
+    const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
+    uint8_t* vout = d_out_verdicts ? (uint8_t*)d_out_verdicts + off : e->d_verdicts;
+    uint8_t* mout = (d_out_prep_msgs && c.jr_len) ? (uint8_t*)d_out_prep_msgs + off * 16 : e->d_msgs;
+    rc = prep_core(e, m, N + off * 16, PS ? PS + off * c.ps_bytes : nullptr, H + off * c.his_bytes,
+                   L + off * c.lps_bytes, vout, mout);
+    if (rc) return rc;
+    rc = accumulate_core(e, m, vout, nullptr, nullptr, segment);
+    if (rc) return rc;
+  }
+  e->have_batch = false;
+  return JX_OK;
+}
+
+int32_t jx_aggregate_read(jx_engine* e, uint32_t segment, uint8_t* out_agg, uint64_t* count) {
+  if (!e) return JX_E_INVALID;
+  HIPCHK(e, hipSetDevice(e->device));
+  const Cfg& c = e->cfg;
+  const uint32_t fb = c.algo == ALGO_COUNT ? 8 : 16;
+  Segment* s = nullptr;
+  int32_t rc = get_segment(e, segment, &s);
+  if (rc) return rc;
+  rc = ensure_tmp(e, (size_t)c.out_len * fb);
+  if (rc) return rc;
+  HIPCHK(e, launch_agg_encode(c, s->agg, e->d_tmp, e->stream));
+  if (out_agg) HIPCHK(e, hipMemcpyAsync(out_agg, e->d_tmp, (size_t)c.out_len * fb, hipMemcpyDeviceToHost, e->stream));
+  unsigned long long cnt = 0;
+  HIPCHK(e, hipMemcpyAsync(&cnt, s->count, 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (count) *count = cnt;
+  return drain_timing(e);
+}
+
+int32_t jx_aggregate_checksum(jx_engine* e, uint32_t segment, uint8_t out_checksum[32]) {
+  if (!e || !out_checksum) return JX_E_INVALID;
+  HIPCHK(e, hipSetDevice(e->device));
+  Segment* s = nullptr;
+  int32_t rc = get_segment(e, segment, &s);
+  if (rc) return rc;
+  HIPCHK(e, hipMemcpyAsync(out_checksum, s->checksum, 32, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return JX_OK;
+}
+
+int32_t jx_aggregate_reset(jx_engine* e) {
+  if (!e) return JX_E_INVALID;
+  HIPCHK(e, hipSetDevice(e->device));
+  for (auto& kv : e->segs) {
+    HIPCHK(e, hipMemsetAsync(kv.second.agg, 0, (size_t)e->cfg.out_len * 16, e->stream));
+    HIPCHK(e, hipMemsetAsync(kv.second.checksum, 0, 32, e->stream));
+    HIPCHK(e, hipMemsetAsync(kv.second.count, 0, 8, e->stream));
+  }
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return JX_OK;
+}
+
+int32_t jx_aggregate_export_device(jx_engine* e, uint32_t segment, void* d_dst) {
+  if (!e || !d_dst) return JX_E_INVALID;
+  HIPCHK(e, hipSetDevice(e->device));
+  Segment* s = nullptr;
+  int32_t rc = get_segment(e, segment, &s);
+  if (rc) return rc;
+  HIPCHK(e, launch_agg_encode(e->cfg, s->agg, (uint8_t*)d_dst, e->stream));
+  return JX_OK;
+}
+
+int32_t jx_aggregate_combine_device(jx_engine* e, const void* d_parts, uint32_t nparts, void* d_out) {
+  if (!e || !d_parts || !d_out || nparts == 0) return JX_E_INVALID;
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, launch_combine(e->cfg, (const uint8_t*)d_parts, nparts, (uint8_t*)d_out, e->stream));
+  return JX_OK;
+}
+
+int32_t jx_engine_sync(jx_engine* e) {
+  if (!e) return JX_E_INVALID;
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return JX_OK;
+}
+
+int32_t jx_engine_stream(jx_engine* e, void** stream) {
+  if (!e || !stream) return JX_E_INVALID;
+  *stream = (void*)e->stream;
+  return JX_OK;
+}
+
+int32_t jx_engine_timing(jx_engine* e, int32_t enable) {
+  if (!e) return JX_E_INVALID;
+  int32_t rc = drain_timing(e);
+  if (rc) return rc;
+  e->timing = enable != 0;
+  for (int i = 0; i < NST; i++) {
+    e->ms[i] = 0;
+    e->launches[i] = 0;
+  }
+  return JX_OK;
+}
+
+int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]) {
+  if (!e) return JX_E_INVALID;
+  int32_t rc = drain_timing(e);
+  if (rc) return rc;
+  for (int i = 0; i < NST; i++) {
+    if (ms) ms[i] = (float)e->ms[i];
+    if (launches) launches[i] = e->launches[i];
+  }
+  return JX_OK;
+}
+
+int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
+  if (!e) return JX_E_INVALID;
+  if (option == 1) {
+    e->force_slow = value != 0;
+    return JX_OK;
+  }
+  if (option == 2) {  // accumulate chunking (tests)
+    if (value < 1 || value > 4096) return JX_E_INVALID;
+    free_staging(e);
+    e->acc_chunks = (uint32_t)value;
+    return JX_OK;
+  }
+  return JX_E_INVALID;
+}
+
+const char* jx_status_str(int32_t s) {
+  switch (s) {
+    case JX_OK:
+      return "ok";
+    case JX_E_INVALID:
+      return "invalid argument";
+    case JX_E_UNSUPPORTED:
+      return "unsupported Prio3 parameters";
+    case JX_E_HIP:
+      return "HIP runtime error";
+    case JX_E_NOMEM:
+      return "device out of memory";
+    case JX_E_STATE:
+      return "call out of order";
+    case JX_E_NODEVICE:
+      return "no HIP device";
+    default:
+      return "unknown status";
+  }
+}
+
+const char* jx_last_error(const jx_engine* e) { return e ? e->err.c_str() : ""; }
+
+}  // extern "C"

@@ -1,0 +1,271 @@
+// jx_field.h — Field64 / Field128 arithmetic for the gfx950 Prio3 engine.
+//
+// Fields are those of VDAF-08 §6.1.2 as used by prio 0.16.1 (Janus pins prio at
+// /root/reference/Cargo.toml:50): Field64 p = 2^64 - 2^32 + 1 (Prio3Count),
+// Field128 p = 2^128 - 28*2^64 + 1 (Prio3Sum/SumVec/Histogram, core/src/vdaf.rs:203-262).
+//
+// Field128 representation: four 32-bit limbs (the native VALU width) in a
+// struct of two uint64 halves. Products use Montgomery multiplication with
+// R = 2^128: since p == 1 (mod 2^64), -p^-1 mod 2^64 = -1 and m*p needs only a
+// multiply by 28, so each of the two 64-bit REDC steps is a handful of adds.
+// Values that stream through HBM (measurement shares, output shares, verifier
+// shares) stay canonical; per-report coefficients are stored in Montgomery form
+// so that mont(x_canonical, c*R) = x*c comes out canonical with ONE reduction.
+//
+// Everything here is __host__ __device__ so the exact same code is unit-tested
+// on the CPU (tests/csrc/hosttest.cpp) before it runs on the GPU.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define JX_HD __host__ __device__ __forceinline__
+#else
+#define JX_HD static inline
+#endif
+
+namespace jx {
+
+// ----------------------------------------------------------------------------
+// 128-bit helpers
+
+struct f128 {
+  uint64_t lo, hi;
+};
+
+JX_HD uint32_t lo32(uint64_t v) { return (uint32_t)v; }
+JX_HD uint32_t hi32(uint64_t v) { return (uint32_t)(v >> 32); }
+
+// add with carry-out
+JX_HD uint64_t addc64(uint64_t a, uint64_t b, uint32_t& carry) {
+  uint64_t s = a + b;
+  uint32_t c1 = s < a;
+  uint64_t s2 = s + carry;
+  uint32_t c2 = s2 < s;
+  carry = c1 | c2;
+  return s2;
+}
+JX_HD uint64_t subb64(uint64_t a, uint64_t b, uint32_t& borrow) {
+  uint64_t d = a - b;
+  uint32_t b1 = a < b;
+  uint64_t d2 = d - borrow;
+  uint32_t b2 = d < (uint64_t)borrow;
+  borrow = b1 | b2;
+  return d2;
+}
+
+// Field128 modulus p = 2^128 - 28*2^64 + 1
+constexpr uint64_t P128_LO = 1ull;
+constexpr uint64_t P128_HI = 0xFFFFFFFFFFFFFFE4ull;
+
+JX_HD f128 make128(uint64_t lo, uint64_t hi) {
+  f128 r;
+  r.lo = lo;
+  r.hi = hi;
+  return r;
+}
+JX_HD bool eq128(f128 a, f128 b) { return a.lo == b.lo && a.hi == b.hi; }
+JX_HD bool is_zero128(f128 a) { return (a.lo | a.hi) == 0; }
+JX_HD bool ge_p128(f128 a) { return a.hi > P128_HI || (a.hi == P128_HI && a.lo >= P128_LO); }
+
+// canonical modular add / sub
+JX_HD f128 add128(f128 a, f128 b) {
+  uint32_t c = 0;
+  uint64_t lo = addc64(a.lo, b.lo, c);
+  uint64_t hi = addc64(a.hi, b.hi, c);
+  // s - p
+  uint32_t br = 0;
+  uint64_t dlo = subb64(lo, P128_LO, br);
+  uint64_t dhi = subb64(hi, P128_HI, br);
+  bool take = c || !br;  // sum >= p
+  return make128(take ? dlo : lo, take ? dhi : hi);
+}
+JX_HD f128 sub128(f128 a, f128 b) {
+  uint32_t br = 0;
+  uint64_t lo = subb64(a.lo, b.lo, br);
+  uint64_t hi = subb64(a.hi, b.hi, br);
+  if (br) {  // add p back
+    uint32_t c = 0;
+    lo = addc64(lo, P128_LO, c);
+    hi = addc64(hi, P128_HI, c);
+  }
+  return make128(lo, hi);
+}
+JX_HD f128 neg128(f128 a) { return sub128(make128(0, 0), a); }
+
+// full 128x128 -> 256 product, 32-bit limb schoolbook (16 v_mad_u64_u32 on gfx950)
+JX_HD void mul128_full(f128 a, f128 b, uint64_t z[4]) {
+  const uint32_t A[4] = {lo32(a.lo), hi32(a.lo), lo32(a.hi), hi32(a.hi)};
+  const uint32_t B[4] = {lo32(b.lo), hi32(b.lo), lo32(b.hi), hi32(b.hi)};
+  uint32_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) r[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      uint64_t t = (uint64_t)A[i] * B[j] + ((uint64_t)r[i + j] + carry);
+      r[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    r[i + 4] = (uint32_t)carry;
+  }
+  z[0] = (uint64_t)r[0] | ((uint64_t)r[1] << 32);
+  z[1] = (uint64_t)r[2] | ((uint64_t)r[3] << 32);
+  z[2] = (uint64_t)r[4] | ((uint64_t)r[5] << 32);
+  z[3] = (uint64_t)r[6] | ((uint64_t)r[7] << 32);
+}
+
+JX_HD uint64_t umulhi64_28(uint64_t m) {
+  // floor(28*m / 2^64): 28m = 32m - 4m
+  // computed exactly with 32-bit pieces
+  uint64_t lo = (uint64_t)lo32(m) * 28u;
+  uint64_t hi = (uint64_t)hi32(m) * 28u + (lo >> 32);
+  return hi >> 32;
+}
+
+// One 64-bit Montgomery REDC step for p = 2^128 - 28*2^64 + 1 (p' = -1 mod 2^64):
+// T' = (T + m*p) / 2^64 with m = -T0 mod 2^64.  m*p = m*2^128 - 28m*2^64 + m, so
+// T' = T[1..] + carry(T0 != 0) + m*(2^64 - 28).
+JX_HD void redc_step(uint64_t& t0, uint64_t& t1, uint64_t& t2, uint64_t& t3) {
+  uint64_t m = 0 - t0;
+  uint32_t c = t0 != 0;
+  uint64_t v = m * 28u;          // low 64 bits of 28m
+  uint64_t u = umulhi64_28(m);   // high bits of 28m
+  uint64_t q_lo = 0 - v;         // m*(2^64-28) = (m - u - (v!=0)) * 2^64 + (2^64 - v)
+  uint64_t q_hi = m - u - (uint64_t)(v != 0);
+  // (t1, t2, t3) + (q_lo, q_hi, 0) + c
+  uint64_t n0 = addc64(t1, q_lo, c);
+  uint64_t n1 = addc64(t2, q_hi, c);
+  uint64_t n2 = t3 + c;
+  t0 = n0;
+  t1 = n1;
+  t2 = n2;
+  t3 = 0;
+}
+
+// Montgomery product a*b*2^-128 mod p, canonical output (inputs < p).
+JX_HD f128 mont128(f128 a, f128 b) {
+  uint64_t z[4];
+  mul128_full(a, b, z);
+  uint64_t t0 = z[0], t1 = z[1], t2 = z[2], t3 = z[3];
+  redc_step(t0, t1, t2, t3);  // now (t0,t1,t2) < p*2^64 + p  (193 bits)
+  redc_step(t0, t1, t2, t3);  // now (t0,t1) + t2*2^128 < 2p
+  // conditional subtract
+  uint32_t br = 0;
+  uint64_t dlo = subb64(t0, P128_LO, br);
+  uint64_t dhi = subb64(t1, P128_HI, br);
+  bool take = (t2 != 0) || !br;
+  return make128(take ? dlo : t0, take ? dhi : t1);
+}
+
+// Montgomery product without the final subtraction: result < 2p, returned as
+// (lo, hi, top) with top in {0,1}. For lazy accumulation.
+JX_HD void mont128_lazy(f128 a, f128 b, uint64_t& lo, uint64_t& hi, uint32_t& top) {
+  uint64_t z[4];
+  mul128_full(a, b, z);
+  uint64_t t0 = z[0], t1 = z[1], t2 = z[2], t3 = z[3];
+  redc_step(t0, t1, t2, t3);
+  redc_step(t0, t1, t2, t3);
+  lo = t0;
+  hi = t1;
+  top = (uint32_t)t2;
+}
+
+// R^2 mod p (R = 2^128), for to_mont
+constexpr uint64_t R2_128_LO = 0xfffffffffffffcf1ull;  // 2^256 mod p (checked in tests)
+constexpr uint64_t R2_128_HI = 0x0000000000005587ull;
+// R mod p = 2^128 - p = 28*2^64 - 1 : Montgomery form of 1
+constexpr uint64_t R1_128_LO = 0xffffffffffffffffull;
+constexpr uint64_t R1_128_HI = 0x000000000000001bull;
+
+JX_HD f128 to_mont128(f128 a) { return mont128(a, make128(R2_128_LO, R2_128_HI)); }
+
+JX_HD f128 from_mont128(f128 a) { return mont128(a, make128(1, 0)); }
+
+// Modular reduction of a value < 2^192 (three 64-bit words) to canonical.
+// 2^128 == 28*2^64 - 1 (mod p).
+JX_HD f128 reduce192(uint64_t w0, uint64_t w1, uint64_t w2) {
+  // v = w0 + w1*2^64 + w2*2^128 == w0 + w1*2^64 + w2*(28*2^64 - 1)
+  //   = (w0 - w2) + 2^64*(w1 + 28*w2)
+  // w2 < 2^64: 28*w2 < 2^69.  Iterate until the top word is zero.
+#pragma unroll 1
+  for (int it = 0; it < 4 && w2 != 0; it++) {
+    uint64_t m_lo = w2 * 28u;
+    uint64_t m_hi = umulhi64_28(w2);  // 28*w2 = m_hi*2^64 + m_lo
+    uint32_t br = 0;
+    uint64_t a0 = subb64(w0, w2, br);  // w0 - w2, borrow into the 2^64 column
+    uint32_t c = 0;
+    uint64_t a1 = addc64(w1, m_lo, c);
+    uint64_t a2 = m_hi + c;
+    // subtract borrow from (a1, a2)
+    uint32_t br2 = br;
+    a1 = subb64(a1, 0, br2);
+    a2 = a2 - br2;
+    w0 = a0;
+    w1 = a1;
+    w2 = a2;
+  }
+  f128 v = make128(w0, w1);
+  // v < 2^128 now; at most two subtractions of p
+  if (ge_p128(v)) {
+    uint32_t br = 0;
+    v.lo = subb64(v.lo, P128_LO, br);
+    v.hi = subb64(v.hi, P128_HI, br);
+  }
+  if (ge_p128(v)) {
+    uint32_t br = 0;
+    v.lo = subb64(v.lo, P128_LO, br);
+    v.hi = subb64(v.hi, P128_HI, br);
+  }
+  return v;
+}
+
+// 192-bit lazy accumulator (sums of < 2^129 values; safe for < 2^63 terms)
+struct acc192 {
+  uint64_t w0, w1, w2;
+};
+JX_HD void acc_zero(acc192& a) { a.w0 = a.w1 = a.w2 = 0; }
+JX_HD void acc_add(acc192& a, uint64_t lo, uint64_t hi, uint32_t top) {
+  uint32_t c = 0;
+  a.w0 = addc64(a.w0, lo, c);
+  a.w1 = addc64(a.w1, hi, c);
+  a.w2 += (uint64_t)top + c;
+}
+JX_HD void acc_add128(acc192& a, f128 v) { acc_add(a, v.lo, v.hi, 0); }
+JX_HD f128 acc_reduce(const acc192& a) { return reduce192(a.w0, a.w1, a.w2); }
+
+// ----------------------------------------------------------------------------
+// Field64 (Goldilocks) p = 2^64 - 2^32 + 1, canonical representation
+
+constexpr uint64_t P64 = 0xFFFFFFFF00000001ull;
+
+JX_HD uint64_t add64(uint64_t a, uint64_t b) {
+  uint64_t s = a + b;
+  bool c = s < a;
+  // if carry: s + 2^64 - p = s + 2^32 - 1
+  if (c) s += 0xFFFFFFFFull;  // cannot overflow again since s < p - 2^32... handled by final check
+  if (s >= P64) s -= P64;
+  return s;
+}
+JX_HD uint64_t sub64(uint64_t a, uint64_t b) { return a >= b ? a - b : a + (P64 - b); }
+JX_HD uint64_t mul64(uint64_t a, uint64_t b) {
+  // 128-bit product
+  uint64_t a0 = lo32(a), a1 = hi32(a), b0 = lo32(b), b1 = hi32(b);
+  uint64_t p00 = a0 * b0, p01 = a0 * b1, p10 = a1 * b0, p11 = a1 * b1;
+  uint64_t mid = (p00 >> 32) + (uint32_t)p01 + (uint32_t)p10;
+  uint64_t lo = (uint32_t)p00 | (mid << 32);
+  uint64_t hi = p11 + (p01 >> 32) + (p10 >> 32) + (mid >> 32);
+  // x = lo + hi*2^64; 2^64 == 2^32 - 1; 2^96 == -1
+  uint64_t hh = hi >> 32, hl = hi & 0xFFFFFFFFull;
+  uint64_t t = lo - hh;
+  if (lo < hh) t += P64;  // borrow: add p (t = lo - hh + p, fits since lo - hh + p < p)
+  uint64_t u = hl * 0xFFFFFFFFull;  // < 2^64
+  uint64_t r = t + u;
+  if (r < t) r += 0xFFFFFFFFull;  // carry: 2^64 == 2^32 - 1
+  if (r >= P64) r -= P64;
+  return r;
+}
+
+}  // namespace jx

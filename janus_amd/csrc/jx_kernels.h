@@ -1,0 +1,87 @@
+// jx_kernels.h — kernel argument structs and launchers shared by jx_kernels.hip and
+// jx_engine.cpp.  See DESIGN.md for the HBM layout.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace jx {
+
+enum Algo : uint32_t { ALGO_COUNT = 0, ALGO_SUM = 1, ALGO_SUMVEC = 2, ALGO_HISTOGRAM = 3 };
+
+// per-report flag bits written by the XOF stage, consumed by the FLP stage
+enum : uint32_t {
+  FLAG_INIT_FAIL = 1u,  // query randomness t is a P-th root of unity -> prepare_init_failure
+  FLAG_NEXT_FAIL = 2u,  // leader's joint-rand part disagrees with the public share -> prepare_next_failure
+  FLAG_SLOW = 4u,       // a rejected XOF sample shifted a stream: the slow kernel redoes this report
+};
+
+// Interleaved staging: element e of report r lives at [(r/64)][e][r%64] (16 bytes each),
+// so a wave (64 reports, one per lane) touching element e moves one coalesced 1 KiB.
+constexpr int IL = 64;
+
+struct Cfg {
+  uint32_t algo, bits, length, chunk;
+  uint32_t meas_len, out_len, jr_len, proof_len, ver_len, calls, P, logP, gpoly_len;
+  uint32_t ps_bytes, his_bytes, lps_bytes;
+  uint32_t ncoef;        // coefficient slots per report
+  uint32_t out_is_meas;  // truncate == identity (Histogram): output share aliases the meas staging
+  uint32_t vk[4];
+  // constant table offsets (uint4 units) in Bufs::consts
+  uint32_t c_omega, c_S, c_misc;
+};
+
+// coefficient slots (Montgomery form unless noted) for the ParallelSum / Sum FLP
+enum : uint32_t {
+  COEF_L = 0,        // (t^P - 1)/P
+  COEF_C0 = 1,       // c_0 = 1/(t - 1)
+  COEF_HALFSUM = 2,  // (1/2) * sum_{k>=1} c_k   [canonical]
+  COEF_T = 3,        // t
+  COEF_R = 4,        // joint_rand[0]
+  COEF_R2 = 5,       // joint_rand[1] (Histogram)
+  COEF_K = 6,        // first per-call slot
+};
+
+struct Bufs {
+  uint64_t n;  // reports in this launch
+  const uint8_t* nonces;
+  const uint8_t* ps;
+  const uint8_t* his;
+  const uint8_t* lps;
+  uint4* meas;
+  uint4* proof;
+  uint4* outs;
+  uint4* coef;
+  uint32_t* flags;
+  uint8_t* verdicts;
+  uint8_t* msgs;
+  const uint4* consts;
+  uint32_t force_slow;  // debug: route every report through the slow XOF kernel
+};
+
+struct AccArgs {
+  uint64_t n;
+  const uint4* outs;
+  uint32_t out_len;
+  const uint8_t* verdicts;
+  const uint8_t* mask;     // nullable
+  const uint32_t* seg;     // nullable
+  uint32_t seg_id;
+  uint64_t* partials;      // [nchunks][out_len][3]
+  uint32_t blocks_per_chunk;
+  uint32_t nchunks;
+  const uint8_t* nonces;
+  uint32_t* checksum;      // [8] (XOR)
+  unsigned long long* count;
+};
+
+// launchers (jx_kernels.hip)
+hipError_t launch_count(const Cfg& c, const Bufs& b, hipStream_t s);
+hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s);
+hipError_t launch_xof_slow(const Cfg& c, const Bufs& b, hipStream_t s);
+hipError_t launch_flp(const Cfg& c, const Bufs& b, hipStream_t s);
+hipError_t launch_accumulate(const Cfg& c, const AccArgs& a, uint4* agg, hipStream_t s);
+hipError_t launch_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, hipStream_t s);
+hipError_t launch_transpose_out(const Cfg& c, const uint4* outs, uint64_t n, uint8_t* dst, hipStream_t s);
+hipError_t launch_agg_encode(const Cfg& c, const uint4* agg, uint8_t* dst, hipStream_t s);
+
+}  // namespace jx

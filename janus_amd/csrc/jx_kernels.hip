@@ -1,0 +1,1119 @@
+// jx_kernels.hip — gfx950 kernels for batched Prio3 helper preparation + aggregation.
+//
+// The per-report work Janus does at aggregator/src/aggregator.rs:1945-1967
+// (prio 0.16.1 ping-pong helper_initialized + evaluate) is split into three
+// launches over a batch of reports:
+//
+//   K1 xof_kernel      one report per lane. TurboSHAKE128 expansion of the helper
+//                      measurement share (fused with the joint_rand_part absorb of the
+//                      same bytes) and proof share; joint_rand_seed, joint_rands,
+//                      query_rands, the prepare-message seed; per-report FLP
+//                      coefficients (barycentric weights, batch-inverted).
+//   K3 flp_*_kernel    FLP query on the helper share + add the leader's verifier
+//                      share + decide + prepare_next check -> verdict byte.
+//   K4 accumulate      masked/segmented field sum of output shares (+count, +checksum),
+//                      i.e. BatchAggregation::merged_with (models.rs:1275-1330).
+//
+// Prio3Count (Field64, 3 permutations) runs as one lane-per-report kernel.
+// Algorithm: draft-irtf-cfrg-vdaf-08 as implemented by prio 0.16.1; see DESIGN.md.
+#include "jx_field.h"
+#include "jx_kernels.h"
+#include "jx_keccak.h"
+#include "jx_sha256.h"
+
+namespace jx {
+
+// ---------------------------------------------------------------------------- helpers
+
+__device__ __forceinline__ f128 u4_to_f(uint4 v) {
+  return make128((uint64_t)v.x | ((uint64_t)v.y << 32), (uint64_t)v.z | ((uint64_t)v.w << 32));
+}
+__device__ __forceinline__ uint4 f_to_u4(f128 a) { return make_uint4(lo32(a.lo), hi32(a.lo), lo32(a.hi), hi32(a.hi)); }
+__device__ __forceinline__ f128 w4_to_f(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return make128((uint64_t)a | ((uint64_t)b << 32), (uint64_t)c | ((uint64_t)d << 32));
+}
+// interleaved staging address
+__device__ __forceinline__ uint64_t il_idx(uint64_t blk, uint32_t len, uint32_t e, uint32_t lane) {
+  return (blk * len + e) * IL + lane;
+}
+__device__ __forceinline__ f128 ld_il(const uint4* base, uint64_t blk, uint32_t len, uint32_t e, uint32_t lane) {
+  return u4_to_f(base[il_idx(blk, len, e, lane)]);
+}
+__device__ __forceinline__ void st_il(uint4* base, uint64_t blk, uint32_t len, uint32_t e, uint32_t lane, f128 v) {
+  base[il_idx(blk, len, e, lane)] = f_to_u4(v);
+}
+__device__ __forceinline__ void load16(const uint8_t* p, uint32_t w[4]) {
+  uint4 v = *reinterpret_cast<const uint4*>(p);
+  w[0] = v.x;
+  w[1] = v.y;
+  w[2] = v.z;
+  w[3] = v.w;
+}
+
+// Montgomery exponentiation, uniform exponent
+__device__ f128 mpow(f128 aR, uint32_t e) {
+  f128 r = make128(R1_128_LO, R1_128_HI);
+  while (e) {
+    if (e & 1) r = mont128(r, aR);
+    aR = mont128(aR, aR);
+    e >>= 1;
+  }
+  return r;
+}
+__device__ __forceinline__ f128 msqr_n(f128 a, int n) {
+  for (int i = 0; i < n; i++) a = mont128(a, a);
+  return a;
+}
+// Montgomery inverse: (aR)^(p-2) via an addition chain for p-2 = (2^64-29)*2^64 + (2^64-1)
+__device__ f128 minv(f128 a) {
+  f128 x2 = mont128(mont128(a, a), a);    // 2^2-1
+  f128 x4 = mont128(msqr_n(x2, 2), x2);   // 2^4-1
+  f128 x8 = mont128(msqr_n(x4, 4), x4);   // 2^8-1
+  f128 x16 = mont128(msqr_n(x8, 8), x8);  // 2^16-1
+  f128 x32 = mont128(msqr_n(x16, 16), x16);
+  f128 x64 = mont128(msqr_n(x32, 32), x32);
+  f128 x48 = mont128(msqr_n(x32, 16), x16);
+  f128 y = mont128(msqr_n(x48, 8), x8);  // 2^56-1
+  // append the 8 low bits of 0xE3 = 1110 0011
+  const uint32_t tail = 0xE3u;
+  for (int i = 7; i >= 0; i--) {
+    y = mont128(y, y);
+    if ((tail >> i) & 1) y = mont128(y, a);
+  }
+  // y = a^(2^64 - 29); result = y^(2^64) * a^(2^64-1)
+  y = msqr_n(y, 64);
+  return mont128(y, x64);
+}
+
+// ---------------------------------------------------------------------------- Field64 helpers (Count)
+
+__device__ uint64_t pow64(uint64_t a, uint64_t e) {
+  uint64_t r = 1;
+  while (e) {
+    if (e & 1) r = mul64(r, a);
+    a = mul64(a, a);
+    e >>= 1;
+  }
+  return r;
+}
+
+// first N accepted Field64 samples from a stream whose first block is in S
+template <int N>
+__device__ void sample64(uint32_t* S, uint64_t out[N]) {
+  int cnt = 0;
+#pragma unroll 1
+  for (int guard = 0; guard < 64; guard++) {
+#pragma unroll
+    for (int ci = 0; ci < 21; ci++) {
+      uint64_t x = (uint64_t)S[2 * ci] | ((uint64_t)S[2 * ci + 1] << 32);
+      bool acc = x < P64;
+#pragma unroll
+      for (int i = 0; i < N; i++)
+        if (acc && cnt == i) out[i] = x;
+      cnt += acc ? 1 : 0;
+    }
+    if (cnt >= N) break;
+    keccak_p12(S);
+  }
+}
+
+// ---------------------------------------------------------------------------- K0: Prio3Count
+
+__global__ __launch_bounds__(256) void count_kernel(Cfg c, Bufs b) {
+  const uint64_t r0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nblk = (b.n + 63) / 64;
+  if (r0 >= nblk * 64) return;
+  const uint64_t r = r0 < b.n ? r0 : b.n - 1;
+  const uint64_t blk = r0 / 64;
+  const uint32_t lane = r0 % 64;
+  uint32_t nonce[4], kmeas[4], kproof[4], S[50];
+  load16(b.nonces + 16 * r, nonce);
+  load16(b.his + (uint64_t)c.his_bytes * r, kmeas);
+  load16(b.his + (uint64_t)c.his_bytes * r + 16, kproof);
+  uint64_t x[1], proof[5], t[1];
+  {  // helper_meas_share: XOF(k_meas, DST(usage 1), [agg_id=1])
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, ALGO_COUNT, 1, kmeas);
+    blk_put_byte(m, pos, 1);
+    blk_pad(m, pos + 1);
+    sponge_oneblock(S, m);
+    sample64<1>(S, x);
+  }
+  {  // helper_proofs_share: XOF(k_proofs, DST(usage 2), [PROOFS=1, agg_id=1])
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, ALGO_COUNT, 2, kproof);
+    blk_put_byte(m, pos, 1);
+    blk_put_byte(m, pos + 1, 1);
+    blk_pad(m, pos + 2);
+    sponge_oneblock(S, m);
+    sample64<5>(S, proof);
+  }
+  {  // query_rands: XOF(verify_key, DST(usage 5), [PROOFS=1] || nonce)
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, ALGO_COUNT, 5, c.vk);
+    blk_put_byte(m, pos, 1);
+#pragma unroll
+    for (int i = 0; i < 4; i++) blk_put_word(m, pos + 1 + 4 * i, nonce[i]);
+    blk_pad(m, pos + 17);
+    sponge_oneblock(S, m);
+    sample64<1>(S, t);
+  }
+  // FLP query, gadget Mul (arity 2), 1 call, P = 2, alpha = -1
+  const uint64_t one = 1, minus1 = P64 - 1;
+  uint64_t tt = t[0];
+  uint64_t t2 = mul64(tt, tt);
+  uint32_t verdict = 0;
+  if (t2 == one) verdict = 1;  // prepare_init_failure
+  uint64_t dm = sub64(tt, one), dp = add64(tt, one);
+  uint64_t inv = pow64(mul64(dm, dp), P64 - 2);
+  uint64_t c0 = mul64(inv, dp);                  // 1/(t-1)
+  uint64_t c1 = mul64(minus1, mul64(inv, dm));   // -1/(t+1) = alpha^1/(t - alpha^1)
+  uint64_t inv2 = (P64 + 1) / 2;
+  uint64_t L = mul64(sub64(t2, one), inv2);
+  uint64_t xm = x[0];
+  uint64_t W0 = mul64(L, add64(mul64(c0, proof[0]), mul64(c1, xm)));
+  uint64_t W1 = mul64(L, add64(mul64(c0, proof[1]), mul64(c1, xm)));
+  // circuit: Mul(x,x) - x with the gadget replaced by gadget_poly(alpha^1) = g0 - g1 + g2
+  uint64_t v = sub64(add64(sub64(proof[2], proof[3]), proof[4]), xm);
+  uint64_t G = add64(proof[2], mul64(tt, add64(proof[3], mul64(tt, proof[4]))));
+  // leader verifier share: [v, W0, W1, G] as 4 x 8-byte LE
+  const uint8_t* lp = b.lps + (uint64_t)c.lps_bytes * r;
+  uint64_t lv[4];
+  bool dfail = false;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint2 q = *reinterpret_cast<const uint2*>(lp + 8 * i);
+    lv[i] = (uint64_t)q.x | ((uint64_t)q.y << 32);
+    dfail |= lv[i] >= P64;
+  }
+  if (verdict == 0 && dfail) verdict = 2;
+  if (verdict == 0) {
+    uint64_t V0 = add64(v, lv[0]), V1 = add64(W0, lv[1]), V2 = add64(W1, lv[2]), VG = add64(G, lv[3]);
+    if (V0 != 0 || mul64(V1, V2) != VG) verdict = 3;
+  }
+  if (r0 < b.n) b.verdicts[r0] = (uint8_t)verdict;
+  b.outs[il_idx(blk, 1, 0, lane)] = make_uint4(lo32(xm), hi32(xm), 0, 0);
+}
+
+// ---------------------------------------------------------------------------- K1: XOF stage (Field128)
+
+struct Trunc {
+  acc192 a;
+  uint32_t j, i;
+};
+
+// 192-bit add of x << sh (sh < 64) into the accumulator
+__device__ __forceinline__ void trunc_add(acc192& a, f128 x, uint32_t sh) {
+  uint64_t w0 = x.lo << sh;
+  uint64_t w1 = sh ? ((x.hi << sh) | (x.lo >> (64 - sh))) : x.hi;
+  uint64_t w2 = sh ? (x.hi >> (64 - sh)) : 0;
+  uint32_t cc = 0;
+  a.w0 = addc64(a.w0, w0, cc);
+  a.w1 = addc64(a.w1, w1, cc);
+  a.w2 = a.w2 + w2 + cc;
+}
+
+// one measurement element at static stream position e (fast path: no rejections)
+__device__ __forceinline__ void emit_meas(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t lane, uint32_t e,
+                                          f128 x, uint32_t& flags, Trunc& tr) {
+  if (e >= c.meas_len) return;
+  if (ge_p128(x)) flags |= FLAG_SLOW;
+  st_il(b.meas, blk, c.meas_len, e, lane, x);
+  if (!c.out_is_meas) {
+    trunc_add(tr.a, x, tr.j);
+    tr.j++;
+    if (tr.j == c.bits) {
+      st_il(b.outs, blk, c.out_len, tr.i, lane, acc_reduce(tr.a));
+      acc_zero(tr.a);
+      tr.j = 0;
+      tr.i++;
+    }
+  }
+}
+__device__ __forceinline__ void emit_proof(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t lane, uint32_t e,
+                                           f128 x, uint32_t& flags) {
+  if (e >= c.proof_len) return;
+  if (ge_p128(x)) flags |= FLAG_SLOW;
+  st_il(b.proof, blk, c.proof_len, e, lane, x);
+}
+
+// slot of c_k (k = 0..calls) in the coefficient table
+__device__ __forceinline__ uint32_t slot_c(const Cfg& c, uint32_t k) {
+  if (k == 0) return COEF_C0;
+  return c.algo == ALGO_SUM ? COEF_K + (k - 1) : COEF_K + 2 * (k - 1);
+}
+
+// Tail of the XOF stage shared by the fast and slow kernels: joint randomness,
+// prepare-message seed, query randomness, FLP coefficients.
+// part_h: the helper's joint_rand_part. Writes msgs / flags / coef.
+// Returns flags (with FLAG_SLOW set if a rejected sample was hit and slow == false).
+__device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t lane, uint64_t r, bool write_msg,
+                             const uint32_t nonce[4], const uint32_t part_l[4], const uint32_t lead_part[4],
+                             const uint32_t part_h[4], uint32_t flags, bool slow) {
+  uint32_t S[50];
+  const uint32_t zero[4] = {0, 0, 0, 0};
+  // corrected joint-rand seed = XOF(0^16, DST(6), part_L || part_H)[0:16]
+  uint32_t corr[4];
+  {
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.algo, 6, zero);
+#pragma unroll
+    for (int i = 0; i < 4; i++) blk_put_word(m, pos + 4 * i, part_l[i]);
+#pragma unroll
+    for (int i = 0; i < 4; i++) blk_put_word(m, pos + 16 + 4 * i, part_h[i]);
+    blk_pad(m, pos + 32);
+    sponge_oneblock(S, m);
+#pragma unroll
+    for (int i = 0; i < 4; i++) corr[i] = S[i];
+  }
+  // joint_rands = expand(corrected, DST(3), [PROOFS=1], JR_LEN)
+  f128 jr[2];
+  {
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.algo, 3, corr);
+    blk_put_byte(m, pos, 1);
+    blk_pad(m, pos + 1);
+    sponge_oneblock(S, m);
+    if (!slow) {
+      jr[0] = w4_to_f(S[0], S[1], S[2], S[3]);
+      jr[1] = w4_to_f(S[4], S[5], S[6], S[7]);
+      if (ge_p128(jr[0]) || (c.jr_len > 1 && ge_p128(jr[1]))) flags |= FLAG_SLOW;
+    } else {
+      // general rejection sampling (stays within the first block with overwhelming probability;
+      // beyond it we permute and continue)
+      int cnt = 0;
+      for (int guard = 0; guard < 64 && cnt < 2; guard++) {
+        for (int ci = 0; ci < 10 && cnt < 2; ci++) {
+          f128 v = w4_to_f(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]);
+          if (!ge_p128(v)) jr[cnt++] = v;
+        }
+        // chunks beyond the tenth straddle blocks; only reachable after 10 rejections (p ~ 2^-600)
+        if (cnt < 2) keccak_p12(S);
+      }
+    }
+  }
+  // prepare message = XOF(0^16, DST(6), leader's part || part_H); equals corr when the
+  // leader's part matches the public share.
+  bool same = part_l[0] == lead_part[0] && part_l[1] == lead_part[1] && part_l[2] == lead_part[2] &&
+              part_l[3] == lead_part[3];
+  uint32_t msg[4] = {corr[0], corr[1], corr[2], corr[3]};
+  if (!same) {
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.algo, 6, zero);
+#pragma unroll
+    for (int i = 0; i < 4; i++) blk_put_word(m, pos + 4 * i, lead_part[i]);
+#pragma unroll
+    for (int i = 0; i < 4; i++) blk_put_word(m, pos + 16 + 4 * i, part_h[i]);
+    blk_pad(m, pos + 32);
+    sponge_oneblock(S, m);
+#pragma unroll
+    for (int i = 0; i < 4; i++) msg[i] = S[i];
+    if (msg[0] != corr[0] || msg[1] != corr[1] || msg[2] != corr[2] || msg[3] != corr[3]) flags |= FLAG_NEXT_FAIL;
+  }
+  if (write_msg) *reinterpret_cast<uint4*>(b.msgs + 16 * r) = make_uint4(msg[0], msg[1], msg[2], msg[3]);
+  // query_rands = expand(verify_key, DST(5), [PROOFS=1] || nonce, 1)
+  f128 t;
+  {
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.algo, 5, c.vk);
+    blk_put_byte(m, pos, 1);
+#pragma unroll
+    for (int i = 0; i < 4; i++) blk_put_word(m, pos + 1 + 4 * i, nonce[i]);
+    blk_pad(m, pos + 17);
+    sponge_oneblock(S, m);
+    t = w4_to_f(S[0], S[1], S[2], S[3]);
+    if (ge_p128(t)) {
+      if (!slow) {
+        flags |= FLAG_SLOW;
+      } else {
+        bool found = false;
+        for (int guard = 0; guard < 64 && !found; guard++) {
+          for (int ci = 0; ci < 10 && !found; ci++) {
+            f128 v = w4_to_f(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]);
+            if (!ge_p128(v)) {
+              t = v;
+              found = true;
+            }
+          }
+          if (!found) keccak_p12(S);
+        }
+      }
+    }
+  }
+  // ---- FLP coefficients (Montgomery form). Barycentric weights on the P-th roots:
+  //   wire_j(t) = L * sum_k c_k * wire_j[k],  c_k = w^k / (t - w^k),  L = (t^P - 1)/P
+  const uint4* omega = b.consts + c.c_omega;
+  const uint4* misc = b.consts + c.c_misc;
+  const f128 R1 = make128(R1_128_LO, R1_128_HI);
+  f128 tR = to_mont128(t);
+  f128 tp = tR;
+  for (uint32_t i = 0; i < c.logP; i++) tp = mont128(tp, tp);
+  if (eq128(tp, R1)) flags |= FLAG_INIT_FAIL;
+  f128 LR = mont128(sub128(tp, R1), u4_to_f(misc[0]));
+  uint4* coef = b.coef;
+  const uint32_t NC = c.ncoef;
+  st_il(coef, blk, NC, COEF_L, lane, LR);
+  st_il(coef, blk, NC, COEF_T, lane, tR);
+  f128 rR = to_mont128(jr[0]);
+  st_il(coef, blk, NC, COEF_R, lane, rR);
+  st_il(coef, blk, NC, COEF_R2, lane, to_mont128(jr[1]));
+  // batch inversion of den_k = t - w^k, k = 0..calls (prefix products parked in the c_k slots)
+  const uint32_t C = c.calls;
+  f128 acc = sub128(tR, u4_to_f(omega[0]));
+  st_il(coef, blk, NC, slot_c(c, 0), lane, acc);
+  for (uint32_t k = 1; k <= C; k++) {
+    acc = mont128(acc, sub128(tR, u4_to_f(omega[k])));
+    st_il(coef, blk, NC, slot_c(c, k), lane, acc);
+  }
+  f128 inv = minv(acc);
+  f128 sumc = make128(0, 0);
+  for (uint32_t k = C; k >= 1; k--) {
+    f128 pre = ld_il(coef, blk, NC, slot_c(c, k - 1), lane);
+    f128 w = u4_to_f(omega[k]);
+    f128 invden = mont128(inv, pre);
+    inv = mont128(inv, sub128(tR, w));
+    f128 ck = mont128(w, invden);
+    st_il(coef, blk, NC, slot_c(c, k), lane, ck);
+    sumc = add128(sumc, ck);
+  }
+  st_il(coef, blk, NC, COEF_C0, lane, inv);  // c_0 = 1/(t - 1)
+  // (1/2) * sum c_k, canonical: mont(sumc*R, 1/2) = sumc/2
+  st_il(coef, blk, NC, COEF_HALFSUM, lane, mont128(sumc, u4_to_f(misc[1])));
+  if (c.algo != ALGO_SUM) {
+    // d_k = c_k * r^{(k-1)*chunk}
+    f128 rc = mpow(rR, c.chunk);
+    f128 rp = R1;
+    for (uint32_t k = 1; k <= C; k++) {
+      f128 ck = ld_il(coef, blk, NC, slot_c(c, k), lane);
+      st_il(coef, blk, NC, slot_c(c, k) + 1, lane, mont128(ck, rp));
+      rp = mont128(rp, rc);
+    }
+  }
+  return flags;
+}
+
+__global__ __launch_bounds__(256) void xof_kernel(Cfg c, Bufs b) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t blk = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t nblk = (b.n + 63) / 64;
+  if (blk >= nblk) return;
+  const uint64_t r0 = blk * 64 + lane;
+  const uint64_t r = r0 < b.n ? r0 : b.n - 1;
+
+  uint32_t nonce[4], kmeas[4], kproof[4], kblind[4];
+  load16(b.nonces + 16 * r, nonce);
+  const uint8_t* hs = b.his + (uint64_t)c.his_bytes * r;
+  load16(hs, kmeas);
+  load16(hs + 16, kproof);
+  load16(hs + 32, kblind);
+  uint32_t flags = 0;
+
+  // ---- measurement share fused with the joint_rand_part absorb --------------------
+  // S: XOF(k_meas, DST(1), [1])            (squeezing, 168 bytes per block)
+  // J: XOF(k_blind, DST(7), [1] || nonce || enc(meas_share))   (absorbing those bytes)
+  uint32_t S[50], J[50];
+  {
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.algo, 1, kmeas);
+    blk_put_byte(m, pos, 1);
+    blk_pad(m, pos + 1);
+    sponge_oneblock(S, m);
+  }
+  uint32_t hdr[11];
+  {
+    Block h;
+    blk_zero(h);
+    int pos = blk_xof_prefix(h, c.algo, 7, kblind);
+    blk_put_byte(h, pos, 1);
+#pragma unroll
+    for (int i = 0; i < 4; i++) blk_put_word(h, pos + 1 + 4 * i, nonce[i]);
+#pragma unroll
+    for (int w = 0; w < 11; w++) hdr[w] = h.w[w];  // 42 header bytes
+  }
+#pragma unroll
+  for (int w = 0; w < 50; w++) J[w] = 0;
+  const uint32_t MB = c.meas_len * 16;
+  const uint32_t ML = 42 + MB;
+  const uint32_t NM = (MB + 167) / 168;
+  const uint32_t b_last = ML / 168;
+  uint32_t prev[11];
+#pragma unroll
+  for (int w = 0; w < 11; w++) prev[w] = 0;
+  uint32_t carry0 = 0, carry1 = 0;
+  Trunc tr;
+  acc_zero(tr.a);
+  tr.j = 0;
+  tr.i = 0;
+  for (uint32_t m = 0; m <= b_last; m++) {
+    const bool have = m < NM;
+    if (have) {
+      if (m > 0) keccak_p12(S);
+      const uint32_t e0 = 21 * (m >> 1);
+      if ((m & 1) == 0) {
+#pragma unroll
+        for (int ci = 0; ci < 10; ci++)
+          emit_meas(c, b, blk, lane, e0 + ci, w4_to_f(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]), flags,
+                    tr);
+        carry0 = S[40];
+        carry1 = S[41];
+      } else {
+        emit_meas(c, b, blk, lane, e0 + 10, w4_to_f(carry0, carry1, S[0], S[1]), flags, tr);
+#pragma unroll
+        for (int ci = 0; ci < 10; ci++)
+          emit_meas(c, b, blk, lane, e0 + 11 + ci,
+                    w4_to_f(S[2 + 4 * ci], S[3 + 4 * ci], S[4 + 4 * ci], S[5 + 4 * ci]), flags, tr);
+      }
+    }
+    // J block m: message bytes [168m, 168m + 168) = meas bytes [168m - 42, 168m + 126)
+    uint32_t jw[42];
+    const uint32_t s0 = have ? S[0] : 0u;
+    if (m == 0) {
+#pragma unroll
+      for (int w = 0; w < 10; w++) jw[w] = hdr[w];
+      jw[10] = (hdr[10] & 0xffffu) | (s0 << 16);
+    } else {
+#pragma unroll
+      for (int w = 0; w < 10; w++) jw[w] = alignbit(prev[w + 1], prev[w], 16);
+      jw[10] = alignbit(s0, prev[10], 16);
+    }
+#pragma unroll
+    for (int w = 11; w < 42; w++) jw[w] = have ? alignbit(S[w - 10], S[w - 11], 16) : 0u;
+    if (m == b_last) {
+      const uint32_t nb = ML - 168 * m;  // message bytes in this block (< 168)
+#pragma unroll
+      for (int w = 0; w < 42; w++) {
+        const uint32_t lo_b = 4 * w;
+        if (lo_b >= nb)
+          jw[w] = 0;
+        else if (lo_b + 4 > nb)
+          jw[w] &= (1u << (8 * (nb - lo_b))) - 1u;
+        if ((uint32_t)w == (nb >> 2)) jw[w] ^= 1u << (8 * (nb & 3));  // TurboSHAKE D = 0x01
+      }
+      jw[41] ^= 0x80000000u;
+    }
+#pragma unroll
+    for (int w = 0; w < 42; w++) J[w] ^= jw[w];
+    keccak_p12(J);
+    if (have) {
+#pragma unroll
+      for (int w = 0; w < 11; w++) prev[w] = S[31 + w];
+    }
+  }
+  uint32_t part_h[4] = {J[0], J[1], J[2], J[3]};
+
+  // ---- proof share: XOF(k_proofs, DST(2), [PROOFS=1, agg_id=1]) -------------------
+  {
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.algo, 2, kproof);
+    blk_put_byte(m, pos, 1);
+    blk_put_byte(m, pos + 1, 1);
+    blk_pad(m, pos + 2);
+    sponge_oneblock(S, m);
+  }
+  const uint32_t NP = (c.proof_len * 16 + 167) / 168;
+  for (uint32_t m = 0; m < NP; m++) {
+    if (m > 0) keccak_p12(S);
+    const uint32_t e0 = 21 * (m >> 1);
+    if ((m & 1) == 0) {
+#pragma unroll
+      for (int ci = 0; ci < 10; ci++)
+        emit_proof(c, b, blk, lane, e0 + ci, w4_to_f(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]), flags);
+      carry0 = S[40];
+      carry1 = S[41];
+    } else {
+      emit_proof(c, b, blk, lane, e0 + 10, w4_to_f(carry0, carry1, S[0], S[1]), flags);
+#pragma unroll
+      for (int ci = 0; ci < 10; ci++)
+        emit_proof(c, b, blk, lane, e0 + 11 + ci,
+                   w4_to_f(S[2 + 4 * ci], S[3 + 4 * ci], S[4 + 4 * ci], S[5 + 4 * ci]), flags);
+    }
+  }
+
+  uint32_t part_l[4], lead_part[4];
+  load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
+  load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
+  flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, part_l, lead_part, part_h, flags, false);
+  if (b.force_slow) flags |= FLAG_SLOW;
+  if (r0 < b.n) b.flags[r0] = flags;
+}
+
+// ---------------------------------------------------------------------------- K1': slow XOF path
+// General byte-stream implementation with rejection sampling at any position. Runs only
+// for reports flagged FLAG_SLOW (a sampled chunk was >= p; ~1e-14 per SumVec report).
+
+struct ByteXof {
+  uint32_t s[50];
+  uint32_t pos;
+};
+__device__ uint32_t bx_byte(ByteXof& x) {
+  if (x.pos == 168) {
+    keccak_p12(x.s);
+    x.pos = 0;
+  }
+  uint32_t v = (x.s[x.pos >> 2] >> (8 * (x.pos & 3))) & 0xffu;
+  x.pos++;
+  return v;
+}
+__device__ f128 bx_elem128(ByteXof& x) {
+  uint32_t w[4];
+  for (int i = 0; i < 4; i++) {
+    uint32_t v = 0;
+    for (int k = 0; k < 4; k++) v |= bx_byte(x) << (8 * k);
+    w[i] = v;
+  }
+  return w4_to_f(w[0], w[1], w[2], w[3]);
+}
+__device__ f128 bx_sample128(ByteXof& x) {
+  for (;;) {
+    f128 v = bx_elem128(x);
+    if (!ge_p128(v)) return v;
+  }
+}
+struct ByteAbs {
+  uint32_t s[50];
+  uint32_t pos;
+};
+__device__ void ba_byte(ByteAbs& a, uint32_t v) {
+  a.s[a.pos >> 2] ^= (v & 0xffu) << (8 * (a.pos & 3));
+  a.pos++;
+  if (a.pos == 168) {
+    keccak_p12(a.s);
+    a.pos = 0;
+  }
+}
+__device__ void ba_word(ByteAbs& a, uint32_t v) {
+  for (int k = 0; k < 4; k++) ba_byte(a, v >> (8 * k));
+}
+
+__global__ __launch_bounds__(64) void xof_slow_kernel(Cfg c, Bufs b) {
+  const uint64_t r0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r0 >= b.n) return;
+  if (!(b.flags[r0] & FLAG_SLOW)) return;
+  const uint64_t r = r0, blk = r0 / 64;
+  const uint32_t lane = r0 % 64;
+  uint32_t nonce[4], kmeas[4], kproof[4], kblind[4];
+  load16(b.nonces + 16 * r, nonce);
+  const uint8_t* hs = b.his + (uint64_t)c.his_bytes * r;
+  load16(hs, kmeas);
+  load16(hs + 16, kproof);
+  load16(hs + 32, kblind);
+  uint32_t flags = 0;
+  ByteXof X;
+  ByteAbs A;
+  {
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.algo, 1, kmeas);
+    blk_put_byte(m, pos, 1);
+    blk_pad(m, pos + 1);
+    sponge_oneblock(X.s, m);
+    X.pos = 0;
+  }
+  for (int w = 0; w < 50; w++) A.s[w] = 0;
+  A.pos = 0;
+  {
+    Block h;
+    blk_zero(h);
+    int pos = blk_xof_prefix(h, c.algo, 7, kblind);
+    blk_put_byte(h, pos, 1);
+    for (int i = 0; i < 4; i++) blk_put_word(h, pos + 1 + 4 * i, nonce[i]);
+    for (int i = 0; i < 42; i++) ba_byte(A, h.w[i >> 2] >> (8 * (i & 3)));
+  }
+  Trunc tr;
+  acc_zero(tr.a);
+  tr.j = 0;
+  tr.i = 0;
+  for (uint32_t e = 0; e < c.meas_len; e++) {
+    f128 x = bx_sample128(X);
+    st_il(b.meas, blk, c.meas_len, e, lane, x);
+    ba_word(A, lo32(x.lo));
+    ba_word(A, hi32(x.lo));
+    ba_word(A, lo32(x.hi));
+    ba_word(A, hi32(x.hi));
+    if (!c.out_is_meas) {
+      trunc_add(tr.a, x, tr.j);
+      if (++tr.j == c.bits) {
+        st_il(b.outs, blk, c.out_len, tr.i, lane, acc_reduce(tr.a));
+        acc_zero(tr.a);
+        tr.j = 0;
+        tr.i++;
+      }
+    }
+  }
+  A.s[A.pos >> 2] ^= 1u << (8 * (A.pos & 3));
+  A.s[41] ^= 0x80000000u;
+  keccak_p12(A.s);
+  uint32_t part_h[4] = {A.s[0], A.s[1], A.s[2], A.s[3]};
+  {
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.algo, 2, kproof);
+    blk_put_byte(m, pos, 1);
+    blk_put_byte(m, pos + 1, 1);
+    blk_pad(m, pos + 2);
+    sponge_oneblock(X.s, m);
+    X.pos = 0;
+  }
+  for (uint32_t e = 0; e < c.proof_len; e++) st_il(b.proof, blk, c.proof_len, e, lane, bx_sample128(X));
+  uint32_t part_l[4], lead_part[4];
+  load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
+  load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
+  flags = xof_tail(c, b, blk, lane, r, true, nonce, part_l, lead_part, part_h, flags, true);
+  b.flags[r0] = flags & ~FLAG_SLOW;
+}
+
+// ---------------------------------------------------------------------------- K3: FLP query + decide
+
+__device__ __forceinline__ f128 ld_lead(const Bufs& b, const Cfg& c, uint64_t r, uint32_t idx, bool& dfail) {
+  uint4 v = *reinterpret_cast<const uint4*>(b.lps + (uint64_t)c.lps_bytes * r + 16u * idx);
+  f128 x = u4_to_f(v);
+  dfail |= ge_p128(x);
+  return x;
+}
+
+// Prio3Sum: gadget PolyEval(x^2 - x), arity 1, `bits` calls; one report per lane.
+__global__ __launch_bounds__(256) void flp_sum_kernel(Cfg c, Bufs b) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t blk = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t nblk = (b.n + 63) / 64;
+  if (blk >= nblk) return;
+  const uint64_t r0 = blk * 64 + lane;
+  const uint64_t r = r0 < b.n ? r0 : b.n - 1;
+  const uint32_t NC = c.ncoef, C = c.calls;
+  const uint4* omega = b.consts + c.c_omega;
+  f128 LR = ld_il(b.coef, blk, NC, COEF_L, lane), c0R = ld_il(b.coef, blk, NC, COEF_C0, lane);
+  f128 tR = ld_il(b.coef, blk, NC, COEF_T, lane), rR = ld_il(b.coef, blk, NC, COEF_R, lane);
+  acc192 ao;
+  acc_zero(ao);
+  for (uint32_t k = 1; k <= C; k++) {
+    f128 x = ld_il(b.meas, blk, c.meas_len, k - 1, lane);
+    uint64_t lo, hi;
+    uint32_t top;
+    mont128_lazy(x, ld_il(b.coef, blk, NC, COEF_K + k - 1, lane), lo, hi, top);
+    acc_add(ao, lo, hi, top);
+  }
+  f128 s0 = ld_il(b.proof, blk, c.proof_len, 0, lane);
+  f128 W0 = mont128(add128(mont128(s0, c0R), acc_reduce(ao)), LR);
+  // v = sum_k r^k * gadget_poly(alpha^k);   G(t) by Horner
+  const uint32_t GL = c.gpoly_len;
+  f128 v = make128(0, 0), rk = rR;
+  for (uint32_t k = 1; k <= C; k++) {
+    f128 wk = u4_to_f(omega[k]);
+    f128 h = make128(0, 0);
+    for (uint32_t m = GL; m-- > 0;) h = add128(mont128(h, wk), ld_il(b.proof, blk, c.proof_len, 1 + m, lane));
+    v = add128(v, mont128(h, rk));
+    rk = mont128(rk, rR);
+  }
+  f128 G = make128(0, 0);
+  for (uint32_t m = GL; m-- > 0;) G = add128(mont128(G, tR), ld_il(b.proof, blk, c.proof_len, 1 + m, lane));
+  bool dfail = false;
+  f128 lv = ld_lead(b, c, r, 0, dfail), lw = ld_lead(b, c, r, 1, dfail), lg = ld_lead(b, c, r, 2, dfail);
+  const uint32_t flags = b.flags[r];
+  uint32_t verdict = 0;
+  if (flags & FLAG_INIT_FAIL)
+    verdict = 1;
+  else if (dfail)
+    verdict = 2;
+  else {
+    f128 V0 = add128(v, lv), V1 = add128(W0, lw), VG = add128(G, lg);
+    // (V1^2 - V1) == VG, compared in the R^-1 scaled domain
+    f128 lhs = sub128(mont128(V1, V1), mont128(V1, make128(1, 0)));
+    if (!is_zero128(V0) || !eq128(lhs, mont128(VG, make128(1, 0))))
+      verdict = 3;
+    else if (flags & FLAG_NEXT_FAIL)
+      verdict = 4;
+  }
+  if (r0 < b.n) b.verdicts[r0] = (uint8_t)verdict;
+}
+
+// Prio3SumVec / Prio3Histogram: gadget ParallelSum(Mul, chunk), arity 2*chunk.
+// One 64-report block per workgroup; wave w owns chunk positions [w*PPW, (w+1)*PPW).
+template <int PPW, bool HIST, int MAXT>
+__global__ __launch_bounds__(MAXT) void flp_psum_kernel(Cfg c, Bufs b) {
+  extern __shared__ uint4 sh[];
+  const uint32_t NW = blockDim.x >> 6;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t blk = blockIdx.x;
+  const uint64_t r0 = blk * 64 + lane;
+  const uint64_t r = r0 < b.n ? r0 : b.n - 1;
+  const uint32_t NC = c.ncoef, C = c.calls, chunk = c.chunk, M = c.meas_len, A = 2 * chunk;
+  const uint32_t j0 = w * PPW;
+
+  acc192 ae[PPW], ao[PPW], sx;
+#pragma unroll
+  for (int i = 0; i < PPW; i++) {
+    acc_zero(ae[i]);
+    acc_zero(ao[i]);
+  }
+  acc_zero(sx);
+  const uint4* coefb = b.coef + il_idx(blk, NC, 0, lane);
+  const uint4* measb = b.meas + il_idx(blk, M, 0, lane);
+  for (uint32_t k = 1; k <= C; k++) {
+    const f128 ck = u4_to_f(coefb[(COEF_K + 2 * (k - 1)) * IL]);
+    const f128 dk = u4_to_f(coefb[(COEF_K + 2 * (k - 1) + 1) * IL]);
+    const uint32_t nb = (k - 1) * chunk + j0;
+    if (k < C && j0 + PPW <= chunk) {
+      // steady state: all PPW positions valid
+      f128 x[PPW];
+#pragma unroll
+      for (int i = 0; i < PPW; i++) x[i] = u4_to_f(measb[(uint64_t)(nb + i) * IL]);
+#pragma unroll
+      for (int i = 0; i < PPW; i++) {
+        uint64_t lo, hi;
+        uint32_t top;
+        mont128_lazy(x[i], dk, lo, hi, top);
+        acc_add(ae[i], lo, hi, top);
+        mont128_lazy(x[i], ck, lo, hi, top);
+        acc_add(ao[i], lo, hi, top);
+        if (HIST) acc_add128(sx, x[i]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < PPW; i++) {
+        if (j0 + i < chunk && nb + i < M) {
+          f128 x = u4_to_f(measb[(uint64_t)(nb + i) * IL]);
+          uint64_t lo, hi;
+          uint32_t top;
+          mont128_lazy(x, dk, lo, hi, top);
+          acc_add(ae[i], lo, hi, top);
+          mont128_lazy(x, ck, lo, hi, top);
+          acc_add(ao[i], lo, hi, top);
+          if (HIST) acc_add128(sx, x);
+        }
+      }
+    }
+  }
+  // ---- wires at t, add the leader's verifier share, partial decide sum
+  const f128 LR = u4_to_f(coefb[COEF_L * IL]), c0R = u4_to_f(coefb[COEF_C0 * IL]);
+  const f128 hs = u4_to_f(coefb[COEF_HALFSUM * IL]), tR = u4_to_f(coefb[COEF_T * IL]);
+  const f128 rR = u4_to_f(coefb[COEF_R * IL]);
+  bool dfail = false;
+  f128 prod = make128(0, 0);
+  f128 rpow = mpow(rR, j0 + 1);
+#pragma unroll
+  for (int i = 0; i < PPW; i++) {
+    const uint32_t j = j0 + i;
+    if (j < chunk) {
+      f128 se = ld_il(b.proof, blk, c.proof_len, 2 * j, lane);
+      f128 so = ld_il(b.proof, blk, c.proof_len, 2 * j + 1, lane);
+      f128 E = acc_reduce(ae[i]), O = acc_reduce(ao[i]);
+      f128 We = mont128(add128(mont128(se, c0R), mont128(E, rpow)), LR);
+      f128 Wo = mont128(sub128(add128(mont128(so, c0R), O), hs), LR);
+      rpow = mont128(rpow, rR);
+      f128 Ve = add128(We, ld_lead(b, c, r, 1 + 2 * j, dfail));
+      f128 Vo = add128(Wo, ld_lead(b, c, r, 2 + 2 * j, dfail));
+      prod = add128(prod, mont128(Ve, Vo));
+    }
+  }
+  // ---- gadget polynomial: v-part = sum_m g_m * S_m, G(t) part, over this wave's m-range
+  const uint32_t GL = c.gpoly_len;
+  const uint32_t per = (GL + NW - 1) / NW;
+  const uint32_t m0 = w * per, m1 = min(GL, m0 + per);
+  const uint4* Sm = b.consts + c.c_S;
+  f128 vpart = make128(0, 0), gpart = make128(0, 0);
+  if (m0 < m1) {
+    for (uint32_t m = m1; m-- > m0;) {
+      f128 g = ld_il(b.proof, blk, c.proof_len, A + m, lane);
+      vpart = add128(vpart, mont128(g, u4_to_f(Sm[m])));
+      gpart = add128(mont128(gpart, tR), g);
+    }
+    gpart = mont128(gpart, mpow(tR, m0));
+  }
+  // ---- cross-wave reduction in LDS
+  uint4* shp = sh + (w * 64 + lane) * 4;
+  shp[0] = f_to_u4(prod);
+  shp[1] = f_to_u4(vpart);
+  shp[2] = f_to_u4(gpart);
+  shp[3] = HIST ? f_to_u4(acc_reduce(sx)) : make_uint4(0, 0, 0, 0);
+  __shared__ uint32_t dfs[16 * 64];
+  dfs[w * 64 + lane] = dfail;
+  __syncthreads();
+  if (w != 0) return;
+  f128 P = make128(0, 0), V = make128(0, 0), G = make128(0, 0), SX = make128(0, 0);
+  bool df = false;
+  for (uint32_t q = 0; q < NW; q++) {
+    const uint4* s = sh + (q * 64 + lane) * 4;
+    P = add128(P, u4_to_f(s[0]));
+    V = add128(V, u4_to_f(s[1]));
+    G = add128(G, u4_to_f(s[2]));
+    if (HIST) SX = add128(SX, u4_to_f(s[3]));
+    df |= dfs[q * 64 + lane] != 0;
+  }
+  f128 vh = V;
+  if (HIST) {
+    // v = jr1 * range_check + jr1^2 * (sum(x) - 1/2)
+    const f128 r2R = u4_to_f(coefb[COEF_R2 * IL]);
+    const f128 half = u4_to_f(b.consts[c.c_misc + 1]);
+    f128 sc = sub128(SX, half);
+    vh = add128(mont128(V, r2R), mont128(sc, mont128(r2R, r2R)));
+  }
+  f128 lv = ld_lead(b, c, r, 0, df), lg = ld_lead(b, c, r, A + 1, df);
+  const uint32_t flags = b.flags[r];
+  uint32_t verdict = 0;
+  if (flags & FLAG_INIT_FAIL)
+    verdict = 1;
+  else if (df)
+    verdict = 2;
+  else {
+    f128 V0 = add128(vh, lv), VG = add128(G, lg);
+    if (!is_zero128(V0) || !eq128(P, mont128(VG, make128(1, 0))))
+      verdict = 3;
+    else if (flags & FLAG_NEXT_FAIL)
+      verdict = 4;
+  }
+  if (r0 < b.n) b.verdicts[r0] = (uint8_t)verdict;
+}
+
+// ---------------------------------------------------------------------------- K4: accumulate
+
+// selection + count + checksum (one report per thread)
+__global__ __launch_bounds__(256) void select_kernel(AccArgs a, uint8_t* sel) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool s = false;
+  if (r < a.n)
+    s = a.verdicts[r] == 0 && (!a.mask || a.mask[r]) && (!a.seg || a.seg[r] == a.seg_id);
+  if (r < ((a.n + 63) / 64) * 64) sel[r] = s;
+  uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (s) {
+    uint32_t id[4];
+    load16(a.nonces + 16 * r, id);
+    sha256_16(id, d);
+  }
+  // wave XOR-reduce then one atomic per word per wave
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    uint32_t v = d[k];
+    for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off);
+    d[k] = v;
+  }
+  unsigned long long cnt = __popcll(__ballot(s));
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      if (d[k]) atomicXor(&a.checksum[k], d[k]);
+    if (cnt) atomicAdd(a.count, cnt);
+  }
+}
+
+__global__ __launch_bounds__(256) void accumulate_kernel(AccArgs a, const uint8_t* sel) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= a.out_len) return;
+  const uint64_t nblk = (a.n + 63) / 64;
+  const uint64_t b0 = (uint64_t)blockIdx.y * a.blocks_per_chunk;
+  const uint64_t b1 = (b0 + a.blocks_per_chunk < nblk) ? b0 + a.blocks_per_chunk : nblk;
+  acc192 acc;
+  acc_zero(acc);
+  for (uint64_t bk = b0; bk < b1; bk++) {
+    if (sel[bk * 64 + lane]) acc_add128(acc, u4_to_f(a.outs[il_idx(bk, a.out_len, i, lane)]));
+  }
+  // wave reduction of the 192-bit accumulators
+  for (int off = 32; off > 0; off >>= 1) {
+    uint64_t o0 = ((uint64_t)__shfl_xor((uint32_t)(acc.w0 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w0, off);
+    uint64_t o1 = ((uint64_t)__shfl_xor((uint32_t)(acc.w1 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w1, off);
+    uint64_t o2 = ((uint64_t)__shfl_xor((uint32_t)(acc.w2 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w2, off);
+    uint32_t cc = 0;
+    acc.w0 = addc64(acc.w0, o0, cc);
+    acc.w1 = addc64(acc.w1, o1, cc);
+    acc.w2 = acc.w2 + o2 + cc;
+  }
+  if (lane == 0) {
+    uint64_t* p = a.partials + ((uint64_t)blockIdx.y * a.out_len + i) * 3;
+    p[0] = acc.w0;
+    p[1] = acc.w1;
+    p[2] = acc.w2;
+  }
+}
+
+__device__ uint64_t reduce192_p64(uint64_t w0, uint64_t w1, uint64_t w2) {
+  const uint64_t c64 = 0xFFFFFFFFull;  // 2^64 mod p
+  const uint64_t c128 = mul64(c64, c64);
+  uint64_t a = w0 >= P64 ? w0 - P64 : w0;
+  uint64_t b = w1 >= P64 ? w1 - P64 : w1;
+  uint64_t d = w2 >= P64 ? w2 - P64 : w2;
+  return add64(add64(a, mul64(b, c64)), mul64(d, c128));
+}
+
+__global__ void reduce_partials_kernel(Cfg c, const uint64_t* partials, uint32_t nchunks, uint4* agg) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c.out_len) return;
+  acc192 acc;
+  acc_zero(acc);
+  for (uint32_t q = 0; q < nchunks; q++) {
+    const uint64_t* p = partials + ((uint64_t)q * c.out_len + i) * 3;
+    uint32_t cc = 0;
+    acc.w0 = addc64(acc.w0, p[0], cc);
+    acc.w1 = addc64(acc.w1, p[1], cc);
+    acc.w2 = acc.w2 + p[2] + cc;
+  }
+  acc_add128(acc, u4_to_f(agg[i]));
+  if (c.algo == ALGO_COUNT) {
+    uint64_t v = reduce192_p64(acc.w0, acc.w1, acc.w2);
+    agg[i] = make_uint4(lo32(v), hi32(v), 0, 0);
+  } else {
+    agg[i] = f_to_u4(acc_reduce(acc));
+  }
+}
+
+// multi-GPU combine: sum nparts encoded aggregate shares (LE bytes) mod p
+__global__ void combine_kernel(Cfg c, const uint8_t* parts, uint32_t nparts, uint8_t* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c.out_len) return;
+  const uint32_t fb = c.algo == ALGO_COUNT ? 8 : 16;
+  const uint64_t stride = (uint64_t)c.out_len * fb;
+  if (fb == 8) {
+    uint64_t s = 0;
+    for (uint32_t q = 0; q < nparts; q++) {
+      const uint8_t* p = parts + q * stride + (uint64_t)i * 8;
+      uint64_t v = 0;
+      for (int k = 7; k >= 0; k--) v = (v << 8) | p[k];
+      s = add64(s, v >= P64 ? v - P64 : v);
+    }
+    for (int k = 0; k < 8; k++) out[(uint64_t)i * 8 + k] = (uint8_t)(s >> (8 * k));
+  } else {
+    f128 s = make128(0, 0);
+    for (uint32_t q = 0; q < nparts; q++) {
+      const uint8_t* p = parts + q * stride + (uint64_t)i * 16;
+      uint64_t lo = 0, hi = 0;
+      for (int k = 7; k >= 0; k--) lo = (lo << 8) | p[k];
+      for (int k = 15; k >= 8; k--) hi = (hi << 8) | p[k];
+      s = add128(s, make128(lo, hi));
+    }
+    for (int k = 0; k < 8; k++) out[(uint64_t)i * 16 + k] = (uint8_t)(s.lo >> (8 * k));
+    for (int k = 0; k < 8; k++) out[(uint64_t)i * 16 + 8 + k] = (uint8_t)(s.hi >> (8 * k));
+  }
+}
+
+// interleaved output shares -> [r][i] LE bytes
+__global__ void transpose_out_kernel(Cfg c, const uint4* outs, uint64_t n, uint8_t* dst) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t r = t / c.out_len;
+  const uint32_t i = t % c.out_len;
+  if (r >= n) return;
+  uint4 v = outs[il_idx(r / 64, c.out_len, i, r % 64)];
+  if (c.algo == ALGO_COUNT) {
+    *reinterpret_cast<uint2*>(dst + t * 8) = make_uint2(v.x, v.y);
+  } else {
+    *reinterpret_cast<uint4*>(dst + t * 16) = v;
+  }
+}
+
+__global__ void agg_encode_kernel(Cfg c, const uint4* agg, uint8_t* dst) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c.out_len) return;
+  uint4 v = agg[i];
+  if (c.algo == ALGO_COUNT)
+    *reinterpret_cast<uint2*>(dst + (uint64_t)i * 8) = make_uint2(v.x, v.y);
+  else
+    *reinterpret_cast<uint4*>(dst + (uint64_t)i * 16) = v;
+}
+
+// ---------------------------------------------------------------------------- launchers
+
+static inline uint32_t nblk_of(uint64_t n) { return (uint32_t)((n + 63) / 64); }
+
+hipError_t launch_count(const Cfg& c, const Bufs& b, hipStream_t s) {
+  uint32_t nb = nblk_of(b.n);
+  hipLaunchKernelGGL(count_kernel, dim3((nb * 64 + 255) / 256), dim3(256), 0, s, c, b);
+  return hipGetLastError();
+}
+hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
+  uint32_t nb = nblk_of(b.n);
+  hipLaunchKernelGGL(xof_kernel, dim3((nb + 3) / 4), dim3(256), 0, s, c, b);
+  return hipGetLastError();
+}
+hipError_t launch_xof_slow(const Cfg& c, const Bufs& b, hipStream_t s) {
+  hipLaunchKernelGGL(xof_slow_kernel, dim3((uint32_t)((b.n + 63) / 64)), dim3(64), 0, s, c, b);
+  return hipGetLastError();
+}
+
+int psum_ppw(uint32_t chunk) {
+  // positions per wave: minimise padded positions. Register-heavy widths (>= 8 positions,
+  // 2*PPW lazy accumulators) are limited to 8 waves (512 threads, 256 VGPRs); narrow ones to 16.
+  const int cands[] = {16, 11, 8, 4, 2, 1};
+  int best = -1, best_waste = 1 << 30;
+  for (int p : cands) {
+    int nw = (chunk + p - 1) / p;
+    if (nw > (p >= 8 ? 8 : 16)) continue;
+    int waste = nw * p - (int)chunk;
+    if (waste < best_waste) {
+      best = p;
+      best_waste = waste;
+    }
+  }
+  return best;
+}
+
+template <int PPW>
+static hipError_t launch_psum_t(const Cfg& c, const Bufs& b, hipStream_t s) {
+  uint32_t nb = nblk_of(b.n);
+  uint32_t nw = (c.chunk + PPW - 1) / PPW;
+  size_t shmem = (size_t)nw * 64 * 4 * sizeof(uint4);
+  constexpr int MAXT = PPW >= 8 ? 512 : 1024;
+  if (c.algo == ALGO_HISTOGRAM)
+    hipLaunchKernelGGL((flp_psum_kernel<PPW, true, MAXT>), dim3(nb), dim3(nw * 64), shmem, s, c, b);
+  else
+    hipLaunchKernelGGL((flp_psum_kernel<PPW, false, MAXT>), dim3(nb), dim3(nw * 64), shmem, s, c, b);
+  return hipGetLastError();
+}
+
+hipError_t launch_flp(const Cfg& c, const Bufs& b, hipStream_t s) {
+  if (c.algo == ALGO_SUM) {
+    uint32_t nb = nblk_of(b.n);
+    hipLaunchKernelGGL(flp_sum_kernel, dim3((nb + 3) / 4), dim3(256), 0, s, c, b);
+    return hipGetLastError();
+  }
+  switch (psum_ppw(c.chunk)) {
+    case 16:
+      return launch_psum_t<16>(c, b, s);
+    case 11:
+      return launch_psum_t<11>(c, b, s);
+    case 8:
+      return launch_psum_t<8>(c, b, s);
+    case 4:
+      return launch_psum_t<4>(c, b, s);
+    case 2:
+      return launch_psum_t<2>(c, b, s);
+    case 1:
+      return launch_psum_t<1>(c, b, s);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_accumulate(const Cfg& c, const AccArgs& a, uint4* agg, hipStream_t s) {
+  // sel lives at the tail of the partials allocation (see engine)
+  uint8_t* sel = reinterpret_cast<uint8_t*>(a.partials + (size_t)a.nchunks * c.out_len * 3);
+  uint64_t nthreads = ((a.n + 63) / 64) * 64;
+  hipLaunchKernelGGL(select_kernel, dim3((uint32_t)((nthreads + 255) / 256)), dim3(256), 0, s, a, sel);
+  hipLaunchKernelGGL(accumulate_kernel, dim3((c.out_len + 3) / 4, a.nchunks), dim3(256), 0, s, a,
+                     (const uint8_t*)sel);
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((c.out_len + 255) / 256), dim3(256), 0, s, c,
+                     (const uint64_t*)a.partials, a.nchunks, agg);
+  return hipGetLastError();
+}
+
+hipError_t launch_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(combine_kernel, dim3((c.out_len + 255) / 256), dim3(256), 0, s, c, parts, nparts, out);
+  return hipGetLastError();
+}
+hipError_t launch_transpose_out(const Cfg& c, const uint4* outs, uint64_t n, uint8_t* dst, hipStream_t s) {
+  uint64_t t = n * c.out_len;
+  hipLaunchKernelGGL(transpose_out_kernel, dim3((uint32_t)((t + 255) / 256)), dim3(256), 0, s, c, outs, n, dst);
+  return hipGetLastError();
+}
+hipError_t launch_agg_encode(const Cfg& c, const uint4* agg, uint8_t* dst, hipStream_t s) {
+  hipLaunchKernelGGL(agg_encode_kernel, dim3((c.out_len + 255) / 256), dim3(256), 0, s, c, agg, dst);
+  return hipGetLastError();
+}
+
+}  // namespace jx

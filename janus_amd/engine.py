@@ -1,0 +1,216 @@
+"""Batched Prio3 helper preparation + aggregation on one MI355X (wrapper of include/jx_prio3.h).
+
+This is the host-side mirror of the prio `vdaf::Aggregator` + ping-pong surface that
+Janus calls per report at /root/reference/aggregator/src/aggregator.rs:1945-1967:
+
+    vdaf.helper_initialized(verify_key, agg_param, nonce, public_share, input_share,
+                            leader_message).and_then(|t| t.evaluate(&vdaf))
+
+`HelperEngine.helper_initialized_batch` does that for a whole batch and returns, per
+report, either the outbound `PingPongMessage::Finish{prep_msg}` or a verdict naming the
+`PingPongError` variant (labels of aggregator/src/aggregator/error.rs:379-424).
+`accumulate` is `BatchAggregation::merged_with` (aggregator_core/src/datastore/models.rs:
+1275-1330) for the finished reports, with an accept mask and per-report batch segment so
+the host can drop replayed / collected reports first (aggregation_job_writer.rs:557-704).
+
+All compute runs in the HIP kernels of libjanus_prio3.so; nothing here falls back to the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import EngineError, JxParams, check
+from .vdaf import Prio3
+
+FINISHED = 0
+PREPARE_INIT_FAILURE = 1
+PREP_SHARE_DECODE_FAILURE = 2
+PREPARE_MESSAGE_FAILURE = 3
+PREPARE_NEXT_FAILURE = 4
+VERDICT_LABELS = {
+    FINISHED: "finished",
+    PREPARE_INIT_FAILURE: "prepare_init_failure",
+    PREP_SHARE_DECODE_FAILURE: "leader_prep_share_decode_failure",
+    PREPARE_MESSAGE_FAILURE: "prepare_message_failure",
+    PREPARE_NEXT_FAILURE: "prepare_next_failure",
+}
+
+
+def _ptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    if not a.flags["C_CONTIGUOUS"]:
+        raise ValueError("array must be C-contiguous")
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _u8(a, n: int, width: int, what: str) -> np.ndarray:
+    arr = np.ascontiguousarray(np.frombuffer(a, np.uint8) if isinstance(a, (bytes, bytearray)) else a,
+                               dtype=np.uint8)
+    if width == 0:
+        return np.zeros((max(n, 1), 1), np.uint8)
+    arr = arr.reshape(n, width) if arr.size == n * width else None
+    if arr is None:
+        raise ValueError(f"{what}: expected {n} x {width} bytes")
+    return arr
+
+
+@dataclass
+class BatchResult:
+    verdicts: np.ndarray       # uint8[n]
+    prep_msgs: np.ndarray      # uint8[n, PM]
+    out_shares: np.ndarray | None  # uint8[n, OUT*FB]
+
+    def finished(self) -> np.ndarray:
+        return self.verdicts == FINISHED
+
+
+class HelperEngine:
+    """One engine per (Prio3 instance, verify key, GPU)."""
+
+    def __init__(self, vdaf: Prio3, verify_key: bytes, device: int = 0):
+        if len(verify_key) != 16:
+            raise ValueError("verify key must be 16 bytes (VERIFY_KEY_LENGTH)")
+        self.vdaf = vdaf
+        self.device = device
+        L = _lib.load()
+        self._L = L
+        p = JxParams(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length, vdaf.num_proofs)
+        h = ctypes.c_void_p()
+        vk = (ctypes.c_uint8 * 16).from_buffer_copy(verify_key)
+        st = L.jx_engine_create(ctypes.byref(p), ctypes.cast(vk, ctypes.c_void_p), device, ctypes.byref(h))
+        check(st, None, f"jx_engine_create({vdaf.name()})")
+        self._h = h
+        sizes = [ctypes.c_uint32() for _ in range(6)]
+        check(L.jx_engine_sizes(h, *[ctypes.byref(s) for s in sizes]), h, "jx_engine_sizes")
+        self.public_share_len, self.helper_input_share_len, self.prep_share_len, self.prep_msg_len, \
+            self.output_len, self.field_bytes = (s.value for s in sizes)
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.jx_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ------------------------------------------------------------------ prepare
+    def helper_initialized_batch(self, nonces, public_shares, helper_input_shares, leader_prep_shares,
+                                 want_out_shares: bool = False) -> BatchResult:
+        """prio ping-pong helper_initialized + evaluate for n reports (host buffers).
+
+        leader_prep_shares are the prep_share payloads of the leaders'
+        PingPongMessage::Initialize (fixed length; the aggregator layer rejects other
+        lengths as leader_prep_share_decode_failure before calling this)."""
+        n = len(nonces) // 16 if isinstance(nonces, (bytes, bytearray)) else int(np.asarray(nonces).shape[0])
+        nn = _u8(nonces, n, 16, "nonces")
+        ps = _u8(public_shares, n, self.public_share_len, "public_shares")
+        his = _u8(helper_input_shares, n, self.helper_input_share_len, "helper_input_shares")
+        lps = _u8(leader_prep_shares, n, self.prep_share_len, "leader_prep_shares")
+        verdicts = np.zeros(max(n, 1), np.uint8)
+        msgs = np.zeros((max(n, 1), max(self.prep_msg_len, 1)), np.uint8)
+        outs = np.zeros((max(n, 1), self.output_len * self.field_bytes), np.uint8) if want_out_shares else None
+        st = self._L.jx_helper_prep_batch(self._h, n, _ptr(nn), _ptr(ps) if self.public_share_len else None,
+                                          _ptr(his), _ptr(lps), _ptr(msgs) if self.prep_msg_len else None,
+                                          _ptr(verdicts), _ptr(outs))
+        check(st, self._h, "jx_helper_prep_batch")
+        return BatchResult(verdicts[:n], msgs[:n, : self.prep_msg_len], outs[:n] if outs is not None else None)
+
+    def accumulate(self, n: int, accept_mask: np.ndarray | None = None, segments: np.ndarray | None = None):
+        """Merge the finished output shares of the last batch into batch aggregations."""
+        m = None if accept_mask is None else np.ascontiguousarray(accept_mask, dtype=np.uint8)
+        s = None if segments is None else np.ascontiguousarray(segments, dtype=np.uint32)
+        check(self._L.jx_accumulate(self._h, n, _ptr(m), _ptr(s)), self._h, "jx_accumulate")
+
+    def prep_and_aggregate(self, nonces, public_shares, helper_input_shares, leader_prep_shares,
+                           segment: int = 0, want_results: bool = True):
+        """Fused prep_init + aggregate of n reports (the benchmark's unit of work), host buffers."""
+        n = int(np.asarray(nonces).reshape(-1, 16).shape[0])
+        nn = _u8(nonces, n, 16, "nonces")
+        ps = _u8(public_shares, n, self.public_share_len, "public_shares")
+        his = _u8(helper_input_shares, n, self.helper_input_share_len, "helper_input_shares")
+        lps = _u8(leader_prep_shares, n, self.prep_share_len, "leader_prep_shares")
+        verdicts = np.zeros(max(n, 1), np.uint8) if want_results else None
+        msgs = np.zeros((max(n, 1), 16), np.uint8) if (want_results and self.prep_msg_len) else None
+        st = self._L.jx_helper_prep_aggregate(self._h, n, _ptr(nn), _ptr(ps) if self.public_share_len else None,
+                                              _ptr(his), _ptr(lps), segment, _ptr(msgs), _ptr(verdicts))
+        check(st, self._h, "jx_helper_prep_aggregate")
+        if want_results:
+            return verdicts[:n], (msgs[:n] if msgs is not None else np.zeros((n, 0), np.uint8))
+        return None
+
+    def prep_and_aggregate_device(self, d_nonces: int, d_public_shares: int | None, d_helper_input_shares: int,
+                                  d_leader_prep_shares: int, n: int, segment: int = 0,
+                                  d_out_prep_msgs: int | None = None, d_out_verdicts: int | None = None):
+        """Same, with inputs already resident in HBM (device pointers, e.g. tensor.data_ptr()).
+        Asynchronous: call sync() before reading outputs."""
+        st = self._L.jx_helper_prep_aggregate_device(self._h, n, d_nonces, d_public_shares, d_helper_input_shares,
+                                                     d_leader_prep_shares, segment, d_out_prep_msgs, d_out_verdicts)
+        check(st, self._h, "jx_helper_prep_aggregate_device")
+
+    # ------------------------------------------------------------------ aggregation state
+    def aggregate_share(self, segment: int = 0) -> tuple[bytes, int, bytes]:
+        """(encoded aggregate share, report count, checksum) of one batch aggregation."""
+        out = np.zeros(self.output_len * self.field_bytes, np.uint8)
+        cnt = ctypes.c_uint64()
+        check(self._L.jx_aggregate_read(self._h, segment, _ptr(out), ctypes.byref(cnt)), self._h,
+              "jx_aggregate_read")
+        cs = np.zeros(32, np.uint8)
+        check(self._L.jx_aggregate_checksum(self._h, segment, _ptr(cs)), self._h, "jx_aggregate_checksum")
+        return out.tobytes(), cnt.value, cs.tobytes()
+
+    def reset_aggregates(self):
+        check(self._L.jx_aggregate_reset(self._h), self._h, "jx_aggregate_reset")
+
+    def export_aggregate_device(self, segment: int, d_dst: int):
+        check(self._L.jx_aggregate_export_device(self._h, segment, d_dst), self._h, "jx_aggregate_export_device")
+
+    def combine_device(self, d_parts: int, nparts: int, d_out: int):
+        check(self._L.jx_aggregate_combine_device(self._h, d_parts, nparts, d_out), self._h,
+              "jx_aggregate_combine_device")
+
+    def set_capacity(self, reports: int):
+        check(self._L.jx_engine_set_capacity(self._h, reports), self._h, "jx_engine_set_capacity")
+
+    def sync(self):
+        check(self._L.jx_engine_sync(self._h), self._h, "jx_engine_sync")
+
+    def stream(self) -> int:
+        s = ctypes.c_void_p()
+        check(self._L.jx_engine_stream(self._h, ctypes.byref(s)), self._h, "jx_engine_stream")
+        return s.value or 0
+
+    # ------------------------------------------------------------------ instrumentation
+    def timing(self, enable: bool):
+        check(self._L.jx_engine_timing(self._h, int(enable)), self._h, "jx_engine_timing")
+
+    def timing_read(self) -> dict:
+        ms = (ctypes.c_float * 4)()
+        ln = (ctypes.c_uint64 * 4)()
+        check(self._L.jx_engine_timing_read(self._h, ms, ln), self._h, "jx_engine_timing_read")
+        names = ("xof", "flp", "accumulate", "slow")
+        return {k: {"ms": float(ms[i]), "launches": int(ln[i])} for i, k in enumerate(names)}
+
+    def debug(self, option: int, value: int):
+        check(self._L.jx_engine_debug(self._h, option, value), self._h, "jx_engine_debug")
+
+
+__all__ = ["HelperEngine", "BatchResult", "EngineError", "VERDICT_LABELS", "FINISHED"]

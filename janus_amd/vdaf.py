@@ -1,0 +1,114 @@
+"""VDAF instances handled by the engine — mirror of janus_core::vdaf::VdafInstance.
+
+Reference: /root/reference/core/src/vdaf.rs:65-108 (enum) and :203-262 (the prio
+constructors `Prio3::new_count(2)`, `new_sum(2, bits)`, `new_sum_vec_multithreaded(2,
+bits, length, chunk_length)`, `new_histogram(2, length, chunk_length)`). Sizes follow
+VDAF-08 / prio 0.16.1.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+VERIFY_KEY_LENGTH = 16  # core/src/vdaf.rs:16
+
+# Prio3 algorithm ids (== taskprov VDAF type codes, messages/src/taskprov.rs:358-363)
+PRIO3_COUNT, PRIO3_SUM, PRIO3_SUMVEC, PRIO3_HISTOGRAM = 0, 1, 2, 3
+
+
+def _next_pow2(v: int) -> int:
+    p = 1
+    while p < v:
+        p <<= 1
+    return p
+
+
+@dataclass(frozen=True)
+class Prio3:
+    """One Prio3 instance (2 aggregators, 1 proof, XofTurboShake128)."""
+
+    algo_id: int
+    bits: int = 0
+    length: int = 0
+    chunk_length: int = 0
+    num_proofs: int = 1
+
+    # -- constructors named like VdafInstance variants
+    @staticmethod
+    def count() -> "Prio3":
+        return Prio3(PRIO3_COUNT)
+
+    @staticmethod
+    def sum(bits: int) -> "Prio3":
+        return Prio3(PRIO3_SUM, bits=bits)
+
+    @staticmethod
+    def sum_vec(bits: int, length: int, chunk_length: int) -> "Prio3":
+        return Prio3(PRIO3_SUMVEC, bits=bits, length=length, chunk_length=chunk_length)
+
+    @staticmethod
+    def histogram(length: int, chunk_length: int) -> "Prio3":
+        return Prio3(PRIO3_HISTOGRAM, length=length, chunk_length=chunk_length)
+
+    # -- derived sizes
+    @property
+    def field_bytes(self) -> int:
+        return 8 if self.algo_id == PRIO3_COUNT else 16
+
+    @property
+    def meas_len(self) -> int:
+        return {PRIO3_COUNT: 1, PRIO3_SUM: self.bits, PRIO3_SUMVEC: self.bits * self.length,
+                PRIO3_HISTOGRAM: self.length}[self.algo_id]
+
+    @property
+    def output_len(self) -> int:
+        return 1 if self.algo_id in (PRIO3_COUNT, PRIO3_SUM) else self.length
+
+    @property
+    def joint_rand_len(self) -> int:
+        return {PRIO3_COUNT: 0, PRIO3_SUM: 1, PRIO3_SUMVEC: 1, PRIO3_HISTOGRAM: 2}[self.algo_id]
+
+    @property
+    def arity(self) -> int:
+        return {PRIO3_COUNT: 2, PRIO3_SUM: 1}.get(self.algo_id, 2 * self.chunk_length)
+
+    @property
+    def calls(self) -> int:
+        if self.algo_id == PRIO3_COUNT:
+            return 1
+        if self.algo_id == PRIO3_SUM:
+            return self.bits
+        return -(-self.meas_len // self.chunk_length)
+
+    @property
+    def P(self) -> int:
+        return _next_pow2(1 + self.calls)
+
+    @property
+    def proof_len(self) -> int:
+        return self.arity + 2 * (self.P - 1) + 1
+
+    @property
+    def verifier_len(self) -> int:
+        return self.arity + 2
+
+    @property
+    def public_share_len(self) -> int:
+        return 32 if self.joint_rand_len else 0
+
+    @property
+    def helper_input_share_len(self) -> int:
+        return 48 if self.joint_rand_len else 32
+
+    @property
+    def prep_share_len(self) -> int:
+        return self.verifier_len * self.field_bytes + (16 if self.joint_rand_len else 0)
+
+    @property
+    def prep_msg_len(self) -> int:
+        return 16 if self.joint_rand_len else 0
+
+    def name(self) -> str:
+        return {PRIO3_COUNT: "Prio3Count", PRIO3_SUM: f"Prio3Sum{{bits={self.bits}}}",
+                PRIO3_SUMVEC: f"Prio3SumVec{{bits={self.bits},length={self.length},chunk_length={self.chunk_length}}}",
+                PRIO3_HISTOGRAM: f"Prio3Histogram{{length={self.length},chunk_length={self.chunk_length}}}",
+                }[self.algo_id]

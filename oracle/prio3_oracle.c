@@ -1,0 +1,1140 @@
+/*
+ * prio3_oracle.c — TEST INFRASTRUCTURE ONLY (see prio3_oracle.h for who may use it).
+ *
+ * A deliberately literal CPU restatement of Prio3 as specified in
+ * draft-irtf-cfrg-vdaf-08 and implemented by the external `prio` crate v0.16.1
+ * (Cargo.lock:3435-3438; not vendored in /root/reference). Section numbers
+ * refer to the VDAF-08 text; Janus call sites are cited as file:line under
+ * /root/reference. The FLP is computed the way the spec writes it (record wire
+ * values, interpolate by inverse DFT, evaluate by Horner) — NOT the way the GPU
+ * kernels do it — so that agreement between the two is meaningful.
+ *
+ * Parity: UNPINNED against prio 0.16.1 (no Prio3 vectors exist in the
+ * reference tree). TurboSHAKE128 is pinned by published KATs.
+ */
+#include "prio3_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef unsigned __int128 u128;
+typedef u128 fe; /* a field element (Field64 values live in the low 64 bits) */
+
+/* ------------------------------------------------------------------------- */
+/* Keccak-p[1600, n_r] and TurboSHAKE128 (RFC 9861; VDAF-08 §6.2.1 XofTurboShake128,
+ * implemented in prio via sha3 0.10.8 / keccak 0.1.4, Cargo.lock:4252,2537).   */
+
+static const uint64_t KECCAK_RC[24] = {
+    0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808AULL, 0x8000000080008000ULL,
+    0x000000000000808BULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+    0x000000000000008AULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000AULL,
+    0x000000008000808BULL, 0x800000000000008BULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+    0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800AULL, 0x800000008000000AULL,
+    0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+
+/* rotation offsets r[x + 5y] */
+static const int KECCAK_ROT[25] = {0,  1,  62, 28, 27, 36, 44, 6,  55, 20, 3,  10, 43,
+                                   25, 39, 41, 45, 15, 21, 8,  18, 2,  61, 56, 14};
+
+static inline uint64_t rotl64(uint64_t v, int n) { return n ? (v << n) | (v >> (64 - n)) : v; }
+
+void jo_keccak_p1600(uint64_t A[25], int rounds) {
+  for (int ir = 24 - rounds; ir < 24; ir++) {
+    uint64_t C[5], D[5], B[25];
+    for (int x = 0; x < 5; x++) C[x] = A[x] ^ A[x + 5] ^ A[x + 10] ^ A[x + 15] ^ A[x + 20];
+    for (int x = 0; x < 5; x++) D[x] = C[(x + 4) % 5] ^ rotl64(C[(x + 1) % 5], 1);
+    for (int i = 0; i < 25; i++) A[i] ^= D[i % 5];
+    /* rho + pi: B[y, 2x+3y] = rot(A[x,y], r[x,y]) */
+    for (int x = 0; x < 5; x++)
+      for (int y = 0; y < 5; y++) B[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64(A[x + 5 * y], KECCAK_ROT[x + 5 * y]);
+    /* chi */
+    for (int y = 0; y < 5; y++)
+      for (int x = 0; x < 5; x++)
+        A[x + 5 * y] = B[x + 5 * y] ^ (~B[(x + 1) % 5 + 5 * y] & B[(x + 2) % 5 + 5 * y]);
+    A[0] ^= KECCAK_RC[ir];
+  }
+}
+
+#define TS_RATE 168
+typedef struct {
+  uint64_t s[25];
+  unsigned pos;
+  int squeezing;
+  uint8_t D;
+} ts_t;
+
+static void ts_init(ts_t *t, uint8_t D) {
+  memset(t, 0, sizeof *t);
+  t->D = D;
+}
+static inline void ts_xor_byte(ts_t *t, unsigned i, uint8_t b) { t->s[i / 8] ^= (uint64_t)b << (8 * (i % 8)); }
+static inline uint8_t ts_get_byte(const ts_t *t, unsigned i) { return (uint8_t)(t->s[i / 8] >> (8 * (i % 8))); }
+
+static void ts_absorb(ts_t *t, const uint8_t *m, size_t len) {
+  for (size_t i = 0; i < len; i++) {
+    ts_xor_byte(t, t->pos++, m[i]);
+    if (t->pos == TS_RATE) {
+      jo_keccak_p1600(t->s, 12);
+      t->pos = 0;
+    }
+  }
+}
+static void ts_squeeze(ts_t *t, uint8_t *out, size_t len) {
+  if (!t->squeezing) {
+    ts_xor_byte(t, t->pos, t->D);
+    ts_xor_byte(t, TS_RATE - 1, 0x80);
+    jo_keccak_p1600(t->s, 12);
+    t->pos = 0;
+    t->squeezing = 1;
+  }
+  for (size_t i = 0; i < len; i++) {
+    if (t->pos == TS_RATE) {
+      jo_keccak_p1600(t->s, 12);
+      t->pos = 0;
+    }
+    out[i] = ts_get_byte(t, t->pos++);
+  }
+}
+
+void jo_turboshake128(const uint8_t *msg, size_t len, uint8_t D, uint8_t *out, size_t outlen) {
+  ts_t t;
+  ts_init(&t, D);
+  ts_absorb(&t, msg, len);
+  ts_squeeze(&t, out, outlen);
+}
+
+/* XofTurboShake128 (VDAF-08 §6.2.1): M = byte(len(dst)) || dst || seed || binder, D = 1. */
+static void xof_init(ts_t *x, const uint8_t seed[16], const uint8_t *dst, size_t dst_len) {
+  uint8_t l = (uint8_t)dst_len;
+  ts_init(x, 1);
+  ts_absorb(x, &l, 1);
+  ts_absorb(x, dst, dst_len);
+  ts_absorb(x, seed, 16);
+}
+
+void jo_xof_expand(const uint8_t seed[16], const uint8_t *dst, size_t dst_len, const uint8_t *binder,
+                   size_t binder_len, uint8_t *out, size_t outlen) {
+  ts_t x;
+  xof_init(&x, seed, dst, dst_len);
+  ts_absorb(&x, binder, binder_len);
+  ts_squeeze(&x, out, outlen);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Fields (VDAF-08 §6.1.2): Field64 p = 2^64-2^32+1, Field128 p = 2^128-28*2^64+1.
+ * GEN = 7^((p-1)/2^GEN_LOG2). LE encoding; decode rejects values >= p.       */
+
+typedef struct {
+  int is64;
+  int enc;
+  fe p;
+  fe gen;
+  int gen_log2;
+} field_t;
+
+static const u128 P128 = (((u128)0xFFFFFFFFFFFFFFE4ULL) << 64) | 1u;
+static const u128 P64 = 0xFFFFFFFF00000001ULL;
+
+static field_t F64, F128;
+static pthread_once_t fields_once = PTHREAD_ONCE_INIT;
+
+static inline fe f_add(const field_t *F, fe a, fe b) {
+  if (F->is64) {
+    u128 s = a + b;
+    return s >= F->p ? s - F->p : s;
+  }
+  u128 s = a + b;
+  int carry = s < a;
+  if (carry || s >= F->p) s -= F->p; /* wraps mod 2^128 correctly when carry */
+  return s;
+}
+static inline fe f_sub(const field_t *F, fe a, fe b) { return a >= b ? a - b : a + (F->p - b); }
+static inline fe f_neg(const field_t *F, fe a) { return a ? F->p - a : 0; }
+
+static void mul_128x128(u128 a, u128 b, uint64_t z[4]) {
+  uint64_t a0 = (uint64_t)a, a1 = (uint64_t)(a >> 64), b0 = (uint64_t)b, b1 = (uint64_t)(b >> 64);
+  u128 p00 = (u128)a0 * b0, p01 = (u128)a0 * b1, p10 = (u128)a1 * b0, p11 = (u128)a1 * b1;
+  u128 mid = (p00 >> 64) + (uint64_t)p01 + (uint64_t)p10;
+  u128 hi = p11 + (p01 >> 64) + (p10 >> 64) + (mid >> 64);
+  z[0] = (uint64_t)p00;
+  z[1] = (uint64_t)mid;
+  z[2] = (uint64_t)hi;
+  z[3] = (uint64_t)(hi >> 64);
+}
+
+/* reduce a 256-bit value mod p128 by folding 2^128 == 28*2^64 - 1 (mod p) */
+static fe reduce256_p128(uint64_t z[4]) {
+  const u128 c = (((u128)28) << 64) - 1;
+  while (z[2] | z[3]) {
+    u128 H = ((u128)z[3] << 64) | z[2];
+    u128 L = ((u128)z[1] << 64) | z[0];
+    uint64_t t[4];
+    mul_128x128(H, c, t);
+    u128 lo = ((u128)t[1] << 64) | t[0];
+    u128 s = lo + L;
+    u128 carry = s < lo;
+    u128 hi = (((u128)t[3] << 64) | t[2]) + carry;
+    z[0] = (uint64_t)s;
+    z[1] = (uint64_t)(s >> 64);
+    z[2] = (uint64_t)hi;
+    z[3] = (uint64_t)(hi >> 64);
+  }
+  u128 v = ((u128)z[1] << 64) | z[0];
+  while (v >= P128) v -= P128;
+  return v;
+}
+
+static inline fe f_mul(const field_t *F, fe a, fe b) {
+  if (F->is64) return (a * b) % F->p;
+  uint64_t z[4];
+  mul_128x128(a, b, z);
+  return reduce256_p128(z);
+}
+
+static fe f_pow(const field_t *F, fe a, u128 e) {
+  fe r = 1;
+  while (e) {
+    if (e & 1) r = f_mul(F, r, a);
+    a = f_mul(F, a, a);
+    e >>= 1;
+  }
+  return r;
+}
+static fe f_inv(const field_t *F, fe a) { return f_pow(F, a, F->p - 2); }
+static fe f_from_u64(const field_t *F, uint64_t v) { return (fe)v % F->p; }
+
+/* root of unity of order 2^l */
+static fe f_root(const field_t *F, int l) {
+  fe r = F->gen;
+  for (int i = l; i < F->gen_log2; i++) r = f_mul(F, r, r);
+  return r;
+}
+
+static void init_fields(void) {
+  F64.is64 = 1;
+  F64.enc = 8;
+  F64.p = P64;
+  F64.gen_log2 = 32;
+  F64.gen = f_pow(&F64, 7, (P64 - 1) >> 32);
+  F128.is64 = 0;
+  F128.enc = 16;
+  F128.p = P128;
+  F128.gen_log2 = 66;
+  F128.gen = f_pow(&F128, 7, (P128 - 1) >> 66);
+}
+
+static void f_encode(const field_t *F, fe v, uint8_t *out) {
+  for (int i = 0; i < F->enc; i++) out[i] = (uint8_t)(v >> (8 * i));
+}
+/* returns 0 on success, -1 if the encoding is >= p */
+static int f_decode(const field_t *F, const uint8_t *in, fe *v) {
+  fe x = 0;
+  for (int i = F->enc - 1; i >= 0; i--) x = (x << 8) | in[i];
+  if (x >= F->p) return -1;
+  *v = x;
+  return 0;
+}
+
+/* XOF.next_vec (VDAF-08 §6.2): read ENC bytes LE, mask to next_pow2(p)-1 (a no-op
+ * for both fields), reject if >= p, continue the stream. */
+static void xof_next_vec(const field_t *F, ts_t *x, fe *out, size_t n) {
+  uint8_t buf[16];
+  size_t i = 0;
+  while (i < n) {
+    ts_squeeze(x, buf, F->enc);
+    fe v;
+    if (f_decode(F, buf, &v) == 0) out[i++] = v;
+  }
+}
+
+/* ------------------------------------------------------------------------- */
+/* Prio3 configuration (VDAF-08 §7; Janus VdafInstance core/src/vdaf.rs:65-108,
+ * constructors core/src/vdaf.rs:203-262).                                     */
+
+enum { G_MUL = 0, G_RANGE2 = 1, G_PSUM_MUL = 2 };
+enum {
+  USAGE_MEAS_SHARE = 1,
+  USAGE_PROOF_SHARE = 2,
+  USAGE_JOINT_RANDOMNESS = 3,
+  USAGE_PROVE_RANDOMNESS = 4,
+  USAGE_QUERY_RANDOMNESS = 5,
+  USAGE_JOINT_RAND_SEED = 6,
+  USAGE_JOINT_RAND_PART = 7,
+};
+
+typedef struct {
+  int algo, bits, length, chunk, proofs;
+  const field_t *F;
+  int meas_len, out_len, jr_len, qr_len;
+  int gadget, arity, degree, calls, P;
+  int gpoly_len, proof_len, verifier_len, prove_rand_len;
+} cfg_t;
+
+static int next_pow2(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+static int cfg_make(cfg_t *c, int algo, int bits, int length, int chunk, int proofs) {
+  pthread_once(&fields_once, init_fields);
+  memset(c, 0, sizeof *c);
+  c->algo = algo;
+  c->bits = bits;
+  c->length = length;
+  c->chunk = chunk;
+  c->proofs = proofs;
+  if (proofs < 1 || proofs > 255) return -1;
+  c->qr_len = 1;
+  c->degree = 2;
+  switch (algo) {
+    case JO_COUNT:
+      c->F = &F64;
+      c->meas_len = 1;
+      c->out_len = 1;
+      c->jr_len = 0;
+      c->gadget = G_MUL;
+      c->arity = 2;
+      c->calls = 1;
+      break;
+    case JO_SUM:
+      if (bits < 1 || bits > 64) return -1;
+      c->F = &F128;
+      c->meas_len = bits;
+      c->out_len = 1;
+      c->jr_len = 1;
+      c->gadget = G_RANGE2;
+      c->arity = 1;
+      c->calls = bits;
+      break;
+    case JO_SUMVEC:
+      if (bits < 1 || bits > 64 || length < 1 || chunk < 1) return -1;
+      c->F = &F128;
+      c->meas_len = bits * length;
+      c->out_len = length;
+      c->jr_len = 1;
+      c->gadget = G_PSUM_MUL;
+      c->arity = 2 * chunk;
+      c->calls = (c->meas_len + chunk - 1) / chunk;
+      break;
+    case JO_HISTOGRAM:
+      if (length < 1 || chunk < 1) return -1;
+      c->F = &F128;
+      c->meas_len = length;
+      c->out_len = length;
+      c->jr_len = 2;
+      c->gadget = G_PSUM_MUL;
+      c->arity = 2 * chunk;
+      c->calls = (length + chunk - 1) / chunk;
+      break;
+    default:
+      return -1;
+  }
+  c->P = next_pow2(1 + c->calls);
+  c->gpoly_len = c->degree * (c->P - 1) + 1;
+  c->proof_len = c->arity + c->gpoly_len;
+  c->verifier_len = 1 + c->arity + 1;
+  c->prove_rand_len = c->arity;
+  return 0;
+}
+
+int jo_sizes(int algo, int bits, int length, int chunk, int proofs, uint32_t out[JO_NSIZES]) {
+  cfg_t c;
+  if (cfg_make(&c, algo, bits, length, chunk, proofs)) return -1;
+  int E = c.F->enc, jr = c.jr_len > 0;
+  out[0] = c.meas_len;
+  out[1] = c.out_len;
+  out[2] = c.jr_len;
+  out[3] = c.proof_len;
+  out[4] = c.verifier_len;
+  out[5] = jr ? 32 : 0;
+  out[6] = (c.meas_len + c.proof_len * proofs) * E + (jr ? 16 : 0);
+  out[7] = 32 + (jr ? 16 : 0);
+  out[8] = c.verifier_len * proofs * E + (jr ? 16 : 0);
+  out[9] = jr ? 16 : 0;
+  out[10] = E;
+  out[11] = 16 * (3 + (jr ? 2 : 0));
+  out[12] = c.arity;
+  out[13] = c.calls;
+  out[14] = c.P;
+  return 0;
+}
+
+static void dst_make(const cfg_t *c, int usage, uint8_t dst[8]) {
+  /* VDAF-08 §7.2.x domain_separation_tag = format_dst(0, ID, usage): VERSION=8 */
+  uint32_t id = (uint32_t)c->algo;
+  dst[0] = 8;
+  dst[1] = 0;
+  dst[2] = (uint8_t)(id >> 24);
+  dst[3] = (uint8_t)(id >> 16);
+  dst[4] = (uint8_t)(id >> 8);
+  dst[5] = (uint8_t)id;
+  dst[6] = (uint8_t)(usage >> 8);
+  dst[7] = (uint8_t)usage;
+}
+
+static void expand_into_vec(const cfg_t *c, const uint8_t seed[16], int usage, const uint8_t *binder,
+                            size_t blen, fe *out, size_t n) {
+  uint8_t dst[8];
+  ts_t x;
+  dst_make(c, usage, dst);
+  xof_init(&x, seed, dst, 8);
+  ts_absorb(&x, binder, blen);
+  xof_next_vec(c->F, &x, out, n);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Polynomials (VDAF-08 §6.1.3 poly_eval / poly_interp via the DFT over alpha). */
+
+static fe poly_eval(const field_t *F, const fe *p, int len, fe x) {
+  fe r = 0;
+  for (int i = len - 1; i >= 0; i--) r = f_add(F, f_mul(F, r, x), p[i]);
+  return r;
+}
+
+/* in-place DFT: X_i = sum_j x_j w^{ij}, n a power of two */
+static void dft(const field_t *F, fe *a, int n, fe w) {
+  for (int i = 1, j = 0; i < n; i++) {
+    int bit = n >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j ^= bit;
+    if (i < j) {
+      fe t = a[i];
+      a[i] = a[j];
+      a[j] = t;
+    }
+  }
+  for (int len = 2; len <= n; len <<= 1) {
+    fe wl = f_pow(F, w, (u128)(n / len));
+    for (int i = 0; i < n; i += len) {
+      fe ww = 1;
+      for (int k = 0; k < len / 2; k++) {
+        fe u = a[i + k], v = f_mul(F, a[i + k + len / 2], ww);
+        a[i + k] = f_add(F, u, v);
+        a[i + k + len / 2] = f_sub(F, u, v);
+        ww = f_mul(F, ww, wl);
+      }
+    }
+  }
+}
+
+/* coefficients of the unique poly of degree < n with p(w^i) = vals[i] */
+static void poly_interp_roots(const field_t *F, const fe *vals, fe *coef, int n, fe w) {
+  memcpy(coef, vals, sizeof(fe) * n);
+  dft(F, coef, n, f_inv(F, w));
+  fe ninv = f_inv(F, f_from_u64(F, (uint64_t)n));
+  for (int i = 0; i < n; i++) coef[i] = f_mul(F, coef[i], ninv);
+}
+
+/* ------------------------------------------------------------------------- */
+/* FLP (VDAF-08 §7.3 FlpGeneric) with gadgets Mul, PolyEval(x^2-x), ParallelSum(Mul). */
+
+static fe gadget_eval(const cfg_t *c, const fe *x) {
+  const field_t *F = c->F;
+  switch (c->gadget) {
+    case G_MUL:
+      return f_mul(F, x[0], x[1]);
+    case G_RANGE2: /* PolyEval([0,-1,1]) : x^2 - x */
+      return f_sub(F, f_mul(F, x[0], x[0]), x[0]);
+    default: {
+      fe s = 0;
+      for (int j = 0; j < c->chunk; j++) s = f_add(F, s, f_mul(F, x[2 * j], x[2 * j + 1]));
+      return s;
+    }
+  }
+}
+
+typedef struct {
+  fe *wire; /* arity x P, row-major */
+  int k;
+  int query;
+  const fe *gpoly;
+  fe alpha;
+} grec_t;
+
+static fe gadget_call(const cfg_t *c, grec_t *g, const fe *inp) {
+  g->k++;
+  for (int j = 0; j < c->arity; j++) g->wire[j * c->P + g->k] = inp[j];
+  if (!g->query) return gadget_eval(c, inp); /* ProveGadget */
+  /* QueryGadget: gadget_poly(alpha^k) */
+  return poly_eval(c->F, g->gpoly, c->gpoly_len, f_pow(c->F, g->alpha, (u128)g->k));
+}
+
+/* ParallelSum range checks as in prio's parallel_sum_range_checks (padding with
+ * (0, -1/num_shares) and no r_power update for padded slots). */
+static fe psum_range_checks(const cfg_t *c, grec_t *g, const fe *meas, fe r, int num_shares, fe *buf) {
+  const field_t *F = c->F;
+  fe shares_inv = f_inv(F, f_from_u64(F, (uint64_t)num_shares));
+  fe out = 0, r_power = r;
+  for (int call = 0; call < c->calls; call++) {
+    for (int j = 0; j < c->chunk; j++) {
+      int idx = call * c->chunk + j;
+      if (idx < c->meas_len) {
+        buf[2 * j] = f_mul(F, r_power, meas[idx]);
+        buf[2 * j + 1] = f_sub(F, meas[idx], shares_inv);
+        r_power = f_mul(F, r_power, r);
+      } else {
+        buf[2 * j] = 0;
+        buf[2 * j + 1] = f_neg(F, shares_inv);
+      }
+    }
+    out = f_add(F, out, gadget_call(c, g, buf));
+  }
+  return out;
+}
+
+static fe valid_eval(const cfg_t *c, grec_t *g, const fe *meas, const fe *jr, int num_shares) {
+  const field_t *F = c->F;
+  switch (c->algo) {
+    case JO_COUNT: { /* Mul(x, x) - x */
+      fe in[2] = {meas[0], meas[0]};
+      return f_sub(F, gadget_call(c, g, in), meas[0]);
+    }
+    case JO_SUM: { /* sum_i r^(i+1) * Range2(bit_i) */
+      fe out = 0, r = jr[0];
+      for (int i = 0; i < c->meas_len; i++) {
+        out = f_add(F, out, f_mul(F, r, gadget_call(c, g, &meas[i])));
+        r = f_mul(F, r, jr[0]);
+      }
+      return out;
+    }
+    case JO_SUMVEC: {
+      fe *buf = calloc((size_t)c->arity, sizeof(fe));
+      fe out = psum_range_checks(c, g, meas, jr[0], num_shares, buf);
+      free(buf);
+      return out;
+    }
+    default: { /* Histogram */
+      fe *buf = calloc((size_t)c->arity, sizeof(fe));
+      fe rc = psum_range_checks(c, g, meas, jr[0], num_shares, buf);
+      free(buf);
+      fe sc = f_neg(F, f_inv(F, f_from_u64(F, (uint64_t)num_shares)));
+      for (int i = 0; i < c->meas_len; i++) sc = f_add(F, sc, meas[i]);
+      return f_add(F, f_mul(F, jr[1], rc), f_mul(F, f_mul(F, jr[1], jr[1]), sc));
+    }
+  }
+}
+
+static void flp_encode(const cfg_t *c, uint64_t m, const uint64_t *vec, fe *meas) {
+  const field_t *F = c->F;
+  switch (c->algo) {
+    case JO_COUNT:
+      meas[0] = f_from_u64(F, m);
+      break;
+    case JO_SUM:
+      for (int i = 0; i < c->bits; i++) meas[i] = (m >> i) & 1;
+      break;
+    case JO_SUMVEC:
+      for (int i = 0; i < c->length; i++)
+        for (int j = 0; j < c->bits; j++) meas[i * c->bits + j] = (vec[i] >> j) & 1;
+      break;
+    default:
+      for (int i = 0; i < c->length; i++) meas[i] = (i == (int)m);
+  }
+}
+
+static void flp_truncate(const cfg_t *c, const fe *meas, fe *out) {
+  const field_t *F = c->F;
+  switch (c->algo) {
+    case JO_COUNT:
+    case JO_HISTOGRAM:
+      memcpy(out, meas, sizeof(fe) * c->out_len);
+      break;
+    default: {
+      int b = c->bits;
+      for (int i = 0; i < c->out_len; i++) {
+        fe acc = 0, pw = 1;
+        for (int j = 0; j < b; j++) {
+          acc = f_add(F, acc, f_mul(F, pw, meas[i * b + j]));
+          pw = f_add(F, pw, pw);
+        }
+        out[i] = acc;
+      }
+    }
+  }
+}
+
+/* FlpGeneric.prove (VDAF-08 §7.3.3): run the circuit with num_shares = 1, then
+ * gadget_poly = G(wire polys), computed through a size-2P DFT. */
+static void flp_prove(const cfg_t *c, const fe *meas, const fe *prove_rand, const fe *jr, fe *proof) {
+  const field_t *F = c->F;
+  int P = c->P, A = c->arity, N = 2 * P;
+  fe *wire = calloc((size_t)A * P, sizeof(fe));
+  for (int j = 0; j < A; j++) wire[j * P] = prove_rand[j];
+  grec_t g = {wire, 0, 0, NULL, 0};
+  (void)valid_eval(c, &g, meas, jr, 1);
+  fe aP = f_root(F, __builtin_ctz((unsigned)P));
+  fe aN = f_root(F, __builtin_ctz((unsigned)N));
+  fe *acc = calloc((size_t)N, sizeof(fe));
+  fe *e0 = calloc((size_t)N, sizeof(fe)), *e1 = calloc((size_t)N, sizeof(fe));
+  fe *coef = calloc((size_t)P, sizeof(fe));
+  for (int j = 0; j < (c->gadget == G_RANGE2 ? 1 : A / 2); j++) {
+    /* evaluations of wire polys at the N-th roots of unity */
+    for (int w = 0; w < (c->gadget == G_RANGE2 ? 1 : 2); w++) {
+      fe *e = w ? e1 : e0;
+      int idx = (c->gadget == G_RANGE2) ? 0 : 2 * j + w;
+      poly_interp_roots(F, &wire[idx * P], coef, P, aP);
+      memset(e, 0, sizeof(fe) * N);
+      memcpy(e, coef, sizeof(fe) * P);
+      dft(F, e, N, aN);
+    }
+    for (int i = 0; i < N; i++) {
+      fe v = (c->gadget == G_RANGE2) ? f_sub(F, f_mul(F, e0[i], e0[i]), e0[i]) : f_mul(F, e0[i], e1[i]);
+      acc[i] = f_add(F, acc[i], v);
+    }
+  }
+  dft(F, acc, N, f_inv(F, aN));
+  fe ninv = f_inv(F, f_from_u64(F, (uint64_t)N));
+  for (int j = 0; j < A; j++) proof[j] = prove_rand[j];
+  for (int i = 0; i < c->gpoly_len; i++) proof[A + i] = f_mul(F, acc[i], ninv);
+  /* degree check: coefficient 2P-1 must vanish */
+  if (f_mul(F, acc[N - 1], ninv) != 0) abort();
+  free(wire);
+  free(acc);
+  free(e0);
+  free(e1);
+  free(coef);
+}
+
+/* FlpGeneric.query (VDAF-08 §7.3.3). Returns 0, or -1 if t is a P-th root of unity. */
+static int flp_query(const cfg_t *c, const fe *meas, const fe *proof, const fe *qr, const fe *jr, int num_shares,
+                     fe *verifier) {
+  const field_t *F = c->F;
+  int P = c->P, A = c->arity;
+  fe *wire = calloc((size_t)A * P, sizeof(fe));
+  for (int j = 0; j < A; j++) wire[j * P] = proof[j];
+  fe aP = f_root(F, __builtin_ctz((unsigned)P));
+  grec_t g = {wire, 0, 1, proof + A, aP};
+  verifier[0] = valid_eval(c, &g, meas, jr, num_shares);
+  fe t = qr[0];
+  if (f_pow(F, t, (u128)P) == 1) {
+    free(wire);
+    return -1;
+  }
+  fe *coef = calloc((size_t)P, sizeof(fe));
+  for (int j = 0; j < A; j++) {
+    poly_interp_roots(F, &wire[j * P], coef, P, aP);
+    verifier[1 + j] = poly_eval(F, coef, P, t);
+  }
+  verifier[1 + A] = poly_eval(F, proof + A, c->gpoly_len, t);
+  free(coef);
+  free(wire);
+  return 0;
+}
+
+static int flp_decide(const cfg_t *c, const fe *verifier) {
+  if (verifier[0] != 0) return 0;
+  return gadget_eval(c, verifier + 1) == verifier[1 + c->arity];
+}
+
+/* ------------------------------------------------------------------------- */
+/* Prio3 (VDAF-08 §7.2).                                                       */
+
+static void derive_seed(const cfg_t *c, const uint8_t seed[16], int usage, const uint8_t *binder, size_t blen,
+                        uint8_t out[16]) {
+  uint8_t dst[8];
+  ts_t x;
+  dst_make(c, usage, dst);
+  xof_init(&x, seed, dst, 8);
+  ts_absorb(&x, binder, blen);
+  ts_squeeze(&x, out, 16);
+}
+
+static void joint_rand_part(const cfg_t *c, int agg_id, const uint8_t blind[16], const fe *meas_share,
+                            const uint8_t nonce[16], uint8_t out[16]) {
+  uint8_t dst[8], b = (uint8_t)agg_id, enc[16];
+  ts_t x;
+  dst_make(c, USAGE_JOINT_RAND_PART, dst);
+  xof_init(&x, blind, dst, 8);
+  ts_absorb(&x, &b, 1);
+  ts_absorb(&x, nonce, 16);
+  for (int i = 0; i < c->meas_len; i++) {
+    f_encode(c->F, meas_share[i], enc);
+    ts_absorb(&x, enc, (size_t)c->F->enc);
+  }
+  ts_squeeze(&x, out, 16);
+}
+
+static void joint_rand_seed(const cfg_t *c, const uint8_t part0[16], const uint8_t part1[16], uint8_t out[16]) {
+  uint8_t zero[16] = {0}, parts[32];
+  memcpy(parts, part0, 16);
+  memcpy(parts + 16, part1, 16);
+  derive_seed(c, zero, USAGE_JOINT_RAND_SEED, parts, 32, out);
+}
+
+static void joint_rands(const cfg_t *c, const uint8_t seed[16], fe *out) {
+  uint8_t binder = (uint8_t)c->proofs;
+  expand_into_vec(c, seed, USAGE_JOINT_RANDOMNESS, &binder, 1, out, (size_t)c->jr_len * c->proofs);
+}
+
+static void query_rands(const cfg_t *c, const uint8_t vk[16], const uint8_t nonce[16], fe *out) {
+  uint8_t binder[17];
+  binder[0] = (uint8_t)c->proofs;
+  memcpy(binder + 1, nonce, 16);
+  expand_into_vec(c, vk, USAGE_QUERY_RANDOMNESS, binder, 17, out, (size_t)c->qr_len * c->proofs);
+}
+
+static void helper_meas_share(const cfg_t *c, int agg_id, const uint8_t seed[16], fe *out) {
+  uint8_t binder = (uint8_t)agg_id;
+  expand_into_vec(c, seed, USAGE_MEAS_SHARE, &binder, 1, out, (size_t)c->meas_len);
+}
+
+static void helper_proofs_share(const cfg_t *c, int agg_id, const uint8_t seed[16], fe *out) {
+  uint8_t binder[2] = {(uint8_t)c->proofs, (uint8_t)agg_id};
+  expand_into_vec(c, seed, USAGE_PROOF_SHARE, binder, 2, out, (size_t)c->proof_len * c->proofs);
+}
+
+#define CFG_OR_FAIL(c)                                               \
+  cfg_t c;                                                           \
+  if (cfg_make(&c, algo, bits, length, chunk, proofs)) return -1;
+
+int jo_shard(int algo, int bits, int length, int chunk, int proofs, const uint64_t *measurement,
+             const uint8_t nonce[16], const uint8_t *rand, uint8_t *public_share, uint8_t *leader_input_share,
+             uint8_t *helper_input_share) {
+  CFG_OR_FAIL(c);
+  const field_t *F = c.F;
+  int E = F->enc, JR = c.jr_len > 0;
+  /* rand = k_helper_meas || k_helper_proofs || k_prove || [blind_L || blind_H] */
+  const uint8_t *k_hmeas = rand, *k_hproofs = rand + 16, *k_prove = rand + 32;
+  const uint8_t *blind_l = rand + 48, *blind_h = rand + 64;
+  fe *meas = calloc((size_t)c.meas_len, sizeof(fe)), *hmeas = calloc((size_t)c.meas_len, sizeof(fe));
+  fe *proofs_v = calloc((size_t)c.proof_len * proofs, sizeof(fe));
+  fe *hproofs = calloc((size_t)c.proof_len * proofs, sizeof(fe));
+  fe *prove_rands = calloc((size_t)c.prove_rand_len * proofs, sizeof(fe));
+  fe jr[2 * 256];
+  flp_encode(&c, measurement[0], measurement, meas);
+  helper_meas_share(&c, 1, k_hmeas, hmeas);
+  for (int i = 0; i < c.meas_len; i++) meas[i] = f_sub(F, meas[i], hmeas[i]); /* leader share */
+  uint8_t part_l[16], part_h[16];
+  if (JR) {
+    joint_rand_part(&c, 0, blind_l, meas, nonce, part_l);
+    joint_rand_part(&c, 1, blind_h, hmeas, nonce, part_h);
+    uint8_t seed[16];
+    joint_rand_seed(&c, part_l, part_h, seed);
+    joint_rands(&c, seed, jr);
+  }
+  {
+    uint8_t binder = (uint8_t)proofs;
+    expand_into_vec(&c, k_prove, USAGE_PROVE_RANDOMNESS, &binder, 1, prove_rands,
+                    (size_t)c.prove_rand_len * proofs);
+  }
+  /* full measurement for prove */
+  fe *full = calloc((size_t)c.meas_len, sizeof(fe));
+  flp_encode(&c, measurement[0], measurement, full);
+  for (int p = 0; p < proofs; p++)
+    flp_prove(&c, full, prove_rands + p * c.prove_rand_len, jr + p * c.jr_len, proofs_v + p * c.proof_len);
+  helper_proofs_share(&c, 1, k_hproofs, hproofs);
+  for (int i = 0; i < c.proof_len * proofs; i++) proofs_v[i] = f_sub(F, proofs_v[i], hproofs[i]);
+  /* encodings */
+  if (JR) {
+    memcpy(public_share, part_l, 16);
+    memcpy(public_share + 16, part_h, 16);
+  }
+  uint8_t *o = leader_input_share;
+  for (int i = 0; i < c.meas_len; i++, o += E) f_encode(F, meas[i], o);
+  for (int i = 0; i < c.proof_len * proofs; i++, o += E) f_encode(F, proofs_v[i], o);
+  if (JR) memcpy(o, blind_l, 16);
+  memcpy(helper_input_share, k_hmeas, 16);
+  memcpy(helper_input_share + 16, k_hproofs, 16);
+  if (JR) memcpy(helper_input_share + 32, blind_h, 16);
+  free(meas);
+  free(hmeas);
+  free(proofs_v);
+  free(hproofs);
+  free(prove_rands);
+  free(full);
+  return 0;
+}
+
+static int prep_init_cfg(const cfg_t *c, const uint8_t vk[16], int agg_id, const uint8_t nonce[16],
+                         const uint8_t *public_share, const uint8_t *input_share, uint8_t *prep_share,
+                         fe *out_share, uint8_t corrected[16]) {
+  const field_t *F = c->F;
+  int E = F->enc, JR = c->jr_len > 0, np = c->proofs;
+  fe *meas = calloc((size_t)c->meas_len, sizeof(fe));
+  fe *proofs_v = calloc((size_t)c->proof_len * np, sizeof(fe));
+  const uint8_t *blind = NULL;
+  int rc = 0;
+  if (agg_id == 0) {
+    const uint8_t *p = input_share;
+    for (int i = 0; i < c->meas_len; i++, p += E)
+      if (f_decode(F, p, &meas[i])) rc = JO_PREPARE_INIT_FAILURE;
+    for (int i = 0; i < c->proof_len * np; i++, p += E)
+      if (f_decode(F, p, &proofs_v[i])) rc = JO_PREPARE_INIT_FAILURE;
+    blind = p;
+  } else {
+    helper_meas_share(c, agg_id, input_share, meas);
+    helper_proofs_share(c, agg_id, input_share + 16, proofs_v);
+    blind = input_share + 32;
+  }
+  if (!rc) {
+    flp_truncate(c, meas, out_share);
+    fe jr[2 * 256] = {0}, qr[256];
+    uint8_t own_part[16];
+    if (JR) {
+      uint8_t parts[2][16];
+      joint_rand_part(c, agg_id, blind, meas, nonce, own_part);
+      memcpy(parts[0], public_share, 16);
+      memcpy(parts[1], public_share + 16, 16);
+      memcpy(parts[agg_id], own_part, 16);
+      joint_rand_seed(c, parts[0], parts[1], corrected);
+      joint_rands(c, corrected, jr);
+    }
+    query_rands(c, vk, nonce, qr);
+    fe *ver = calloc((size_t)c->verifier_len * np, sizeof(fe));
+    for (int p = 0; p < np && !rc; p++)
+      if (flp_query(c, meas, proofs_v + p * c->proof_len, qr + p * c->qr_len, jr + p * c->jr_len, 2,
+                    ver + p * c->verifier_len))
+        rc = JO_PREPARE_INIT_FAILURE;
+    if (!rc) {
+      uint8_t *o = prep_share;
+      for (int i = 0; i < c->verifier_len * np; i++, o += E) f_encode(F, ver[i], o);
+      if (JR) memcpy(o, own_part, 16);
+    }
+    free(ver);
+  }
+  free(meas);
+  free(proofs_v);
+  return rc;
+}
+
+int jo_prep_init(int algo, int bits, int length, int chunk, int proofs, const uint8_t verify_key[16], int agg_id,
+                 const uint8_t nonce[16], const uint8_t *public_share, const uint8_t *input_share,
+                 uint8_t *prep_share, uint8_t *out_share, uint8_t *corrected_seed) {
+  CFG_OR_FAIL(c);
+  fe *out = calloc((size_t)c.out_len, sizeof(fe));
+  uint8_t corr[16] = {0};
+  int rc = prep_init_cfg(&c, verify_key, agg_id, nonce, public_share, input_share, prep_share, out, corr);
+  if (!rc) {
+    for (int i = 0; i < c.out_len; i++) f_encode(c.F, out[i], out_share + (size_t)i * c.F->enc);
+    if (corrected_seed) memcpy(corrected_seed, corr, 16);
+  }
+  free(out);
+  return rc;
+}
+
+/* decode a prep share (Prio3PrepareShare): verifiers || [joint_rand_part] */
+static int decode_prep_share(const cfg_t *c, const uint8_t *b, size_t len, fe *ver, uint8_t part[16]) {
+  int E = c->F->enc, n = c->verifier_len * c->proofs;
+  size_t want = (size_t)n * E + (c->jr_len ? 16 : 0);
+  if (len != want) return -1;
+  for (int i = 0; i < n; i++)
+    if (f_decode(c->F, b + (size_t)i * E, &ver[i])) return -1;
+  if (c->jr_len) memcpy(part, b + (size_t)n * E, 16);
+  return 0;
+}
+
+static int prep_shares_to_prep_cfg(const cfg_t *c, const uint8_t *ls, size_t llen, const uint8_t *hs, size_t hlen,
+                                   uint8_t msg[16]) {
+  int n = c->verifier_len * c->proofs;
+  fe *lv = calloc((size_t)n, sizeof(fe)), *hv = calloc((size_t)n, sizeof(fe));
+  uint8_t lp[16], hp[16];
+  int rc = 0;
+  if (decode_prep_share(c, ls, llen, lv, lp) || decode_prep_share(c, hs, hlen, hv, hp)) {
+    rc = JO_PREP_SHARE_DECODE_FAILURE;
+  } else {
+    for (int i = 0; i < n; i++) lv[i] = f_add(c->F, lv[i], hv[i]);
+    for (int p = 0; p < c->proofs && !rc; p++)
+      if (!flp_decide(c, lv + p * c->verifier_len)) rc = JO_PREPARE_MESSAGE_FAILURE;
+    if (!rc && c->jr_len) joint_rand_seed(c, lp, hp, msg);
+  }
+  free(lv);
+  free(hv);
+  return rc;
+}
+
+int jo_prep_shares_to_prep(int algo, int bits, int length, int chunk, int proofs, const uint8_t *leader_prep_share,
+                           size_t leader_len, const uint8_t *helper_prep_share, size_t helper_len,
+                           uint8_t *prep_msg) {
+  CFG_OR_FAIL(c);
+  return prep_shares_to_prep_cfg(&c, leader_prep_share, leader_len, helper_prep_share, helper_len, prep_msg);
+}
+
+/* prio ping-pong helper_initialized + evaluate (topology::ping_pong), as called at
+ * aggregator/src/aggregator.rs:1947-1956; error mapping error.rs:379-424. */
+static int helper_prep_cfg(const cfg_t *c, const uint8_t vk[16], const uint8_t nonce[16], const uint8_t *ps,
+                           const uint8_t *his, const uint8_t *lps, size_t llen, uint8_t *msg, fe *out) {
+  uint32_t sz[JO_NSIZES];
+  jo_sizes(c->algo, c->bits, c->length, c->chunk, c->proofs, sz);
+  uint8_t *hshare = malloc(sz[8]);
+  uint8_t corrected[16] = {0}, m[16] = {0};
+  int rc = prep_init_cfg(c, vk, 1, nonce, ps, his, hshare, out, corrected);
+  if (!rc) {
+    rc = prep_shares_to_prep_cfg(c, lps, llen, hshare, sz[8], m);
+    /* prepare_next: prep_msg must equal the corrected joint-rand seed */
+    if (!rc && c->jr_len && memcmp(m, corrected, 16) != 0) rc = JO_PREPARE_NEXT_FAILURE;
+    if (!rc && msg && c->jr_len) memcpy(msg, m, 16);
+  }
+  free(hshare);
+  return rc;
+}
+
+int jo_helper_prep(int algo, int bits, int length, int chunk, int proofs, const uint8_t verify_key[16],
+                   const uint8_t nonce[16], const uint8_t *public_share, const uint8_t *helper_input_share,
+                   const uint8_t *leader_prep_share, size_t leader_len, uint8_t *prep_msg, uint8_t *out_share) {
+  CFG_OR_FAIL(c);
+  fe *out = calloc((size_t)c.out_len, sizeof(fe));
+  int rc = helper_prep_cfg(&c, verify_key, nonce, public_share, helper_input_share, leader_prep_share, leader_len,
+                           prep_msg, out);
+  if (!rc && out_share)
+    for (int i = 0; i < c.out_len; i++) f_encode(c.F, out[i], out_share + (size_t)i * c.F->enc);
+  free(out);
+  return rc;
+}
+
+/* ------------------------------------------------------------------------- */
+/* SHA-256 (FIPS 180-4), for ReportIdChecksum core/src/report_id.rs:19-42.      */
+
+static const uint32_t SHA_K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+static inline uint32_t ror32(uint32_t v, int n) { return (v >> n) | (v << (32 - n)); }
+
+static void sha256_block(uint32_t h[8], const uint8_t *blk) {
+  uint32_t w[64];
+  for (int i = 0; i < 16; i++)
+    w[i] = (uint32_t)blk[4 * i] << 24 | (uint32_t)blk[4 * i + 1] << 16 | (uint32_t)blk[4 * i + 2] << 8 | blk[4 * i + 3];
+  for (int i = 16; i < 64; i++) {
+    uint32_t s0 = ror32(w[i - 15], 7) ^ ror32(w[i - 15], 18) ^ (w[i - 15] >> 3);
+    uint32_t s1 = ror32(w[i - 2], 17) ^ ror32(w[i - 2], 19) ^ (w[i - 2] >> 10);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  for (int i = 0; i < 64; i++) {
+    uint32_t S1 = ror32(e, 6) ^ ror32(e, 11) ^ ror32(e, 25);
+    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t t1 = hh + S1 + ch + SHA_K[i] + w[i];
+    uint32_t S0 = ror32(a, 2) ^ ror32(a, 13) ^ ror32(a, 22);
+    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint32_t t2 = S0 + mj;
+    hh = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+  }
+  h[0] += a;
+  h[1] += b;
+  h[2] += c;
+  h[3] += d;
+  h[4] += e;
+  h[5] += f;
+  h[6] += g;
+  h[7] += hh;
+}
+
+void jo_sha256(const uint8_t *msg, size_t len, uint8_t out[32]) {
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  size_t i = 0;
+  for (; i + 64 <= len; i += 64) sha256_block(h, msg + i);
+  uint8_t blk[128] = {0};
+  size_t rem = len - i;
+  memcpy(blk, msg + i, rem);
+  blk[rem] = 0x80;
+  size_t tot = (rem + 9 <= 64) ? 64 : 128;
+  uint64_t bits = (uint64_t)len * 8;
+  for (int k = 0; k < 8; k++) blk[tot - 1 - k] = (uint8_t)(bits >> (8 * k));
+  sha256_block(h, blk);
+  if (tot == 128) sha256_block(h, blk + 64);
+  for (int k = 0; k < 8; k++) {
+    out[4 * k] = (uint8_t)(h[k] >> 24);
+    out[4 * k + 1] = (uint8_t)(h[k] >> 16);
+    out[4 * k + 2] = (uint8_t)(h[k] >> 8);
+    out[4 * k + 3] = (uint8_t)h[k];
+  }
+}
+
+/* ------------------------------------------------------------------------- */
+/* Batched drivers (pthreads, report-parallel).                               */
+
+typedef struct {
+  const cfg_t *c;
+  const uint8_t *vk;
+  uint64_t lo, hi;
+  const uint8_t *nonces, *ps, *his, *lps;
+  uint8_t *msgs, *verdicts, *outs;
+  fe *agg;
+  uint64_t count;
+  uint8_t checksum[32];
+  /* client/leader batch */
+  const uint64_t *meas;
+  const uint8_t *rands;
+  uint8_t *ps_out, *his_out, *lps_out, *lout;
+} job_t;
+
+static void *helper_worker(void *arg) {
+  job_t *j = arg;
+  const cfg_t *c = j->c;
+  uint32_t sz[JO_NSIZES];
+  jo_sizes(c->algo, c->bits, c->length, c->chunk, c->proofs, sz);
+  fe *out = calloc((size_t)c->out_len, sizeof(fe));
+  for (uint64_t r = j->lo; r < j->hi; r++) {
+    uint8_t msg[16] = {0};
+    int v = helper_prep_cfg(c, j->vk, j->nonces + 16 * r, j->ps + sz[5] * r, j->his + sz[7] * r,
+                            j->lps + sz[8] * r, sz[8], msg, out);
+    if (j->verdicts) j->verdicts[r] = (uint8_t)v;
+    if (j->msgs && sz[9]) memcpy(j->msgs + sz[9] * r, msg, sz[9]);
+    if (v == 0) {
+      if (j->outs)
+        for (int i = 0; i < c->out_len; i++) f_encode(c->F, out[i], j->outs + (sz[1] * r + i) * sz[10]);
+      if (j->agg)
+        for (int i = 0; i < c->out_len; i++) j->agg[i] = f_add(c->F, j->agg[i], out[i]);
+      j->count++;
+      uint8_t d[32];
+      jo_sha256(j->nonces + 16 * r, 16, d);
+      for (int k = 0; k < 32; k++) j->checksum[k] ^= d[k];
+    }
+  }
+  free(out);
+  return NULL;
+}
+
+int jo_helper_prep_batch(int algo, int bits, int length, int chunk, int proofs, const uint8_t verify_key[16],
+                         uint64_t n, const uint8_t *nonces, const uint8_t *public_shares,
+                         const uint8_t *helper_input_shares, const uint8_t *leader_prep_shares, uint8_t *prep_msgs,
+                         uint8_t *verdicts, uint8_t *out_shares, uint8_t *agg_out, uint64_t *count_out,
+                         uint8_t *checksum_out, int nthreads) {
+  CFG_OR_FAIL(c);
+  if (nthreads < 1) nthreads = 1;
+  if ((uint64_t)nthreads > n && n > 0) nthreads = (int)n;
+  job_t *jobs = calloc((size_t)nthreads, sizeof(job_t));
+  pthread_t *th = calloc((size_t)nthreads, sizeof(pthread_t));
+  for (int t = 0; t < nthreads; t++) {
+    job_t *j = &jobs[t];
+    j->c = &c;
+    j->vk = verify_key;
+    j->lo = n * t / nthreads;
+    j->hi = n * (t + 1) / nthreads;
+    j->nonces = nonces;
+    j->ps = public_shares;
+    j->his = helper_input_shares;
+    j->lps = leader_prep_shares;
+    j->msgs = prep_msgs;
+    j->verdicts = verdicts;
+    j->outs = out_shares;
+    j->agg = agg_out ? calloc((size_t)c.out_len, sizeof(fe)) : NULL;
+    pthread_create(&th[t], NULL, helper_worker, j);
+  }
+  fe *agg = calloc((size_t)c.out_len, sizeof(fe));
+  uint64_t count = 0;
+  uint8_t cs[32] = {0};
+  for (int t = 0; t < nthreads; t++) {
+    pthread_join(th[t], NULL);
+    if (jobs[t].agg) {
+      for (int i = 0; i < c.out_len; i++) agg[i] = f_add(c.F, agg[i], jobs[t].agg[i]);
+      free(jobs[t].agg);
+    }
+    count += jobs[t].count;
+    for (int k = 0; k < 32; k++) cs[k] ^= jobs[t].checksum[k];
+  }
+  if (agg_out)
+    for (int i = 0; i < c.out_len; i++) f_encode(c.F, agg[i], agg_out + (size_t)i * c.F->enc);
+  if (count_out) *count_out = count;
+  if (checksum_out) memcpy(checksum_out, cs, 32);
+  free(agg);
+  free(jobs);
+  free(th);
+  return 0;
+}
+
+static void *client_worker(void *arg) {
+  job_t *j = arg;
+  const cfg_t *c = j->c;
+  uint32_t sz[JO_NSIZES];
+  jo_sizes(c->algo, c->bits, c->length, c->chunk, c->proofs, sz);
+  int mstride = c->algo == JO_SUMVEC ? c->length : 1;
+  uint8_t *lin = malloc(sz[6]);
+  uint8_t corr[16];
+  for (uint64_t r = j->lo; r < j->hi; r++) {
+    jo_shard(c->algo, c->bits, c->length, c->chunk, c->proofs, j->meas + (size_t)mstride * r, j->nonces + 16 * r,
+             j->rands + (size_t)sz[11] * r, j->ps_out + (size_t)sz[5] * r, lin, j->his_out + (size_t)sz[7] * r);
+    fe *out = calloc((size_t)c->out_len, sizeof(fe));
+    int rc = prep_init_cfg(c, j->vk, 0, j->nonces + 16 * r, j->ps_out + (size_t)sz[5] * r, lin,
+                           j->lps_out + (size_t)sz[8] * r, out, corr);
+    if (rc) memset(j->lps_out + (size_t)sz[8] * r, 0xff, sz[8]);
+    if (j->lout)
+      for (int i = 0; i < c->out_len; i++) f_encode(c->F, out[i], j->lout + ((size_t)sz[1] * r + i) * sz[10]);
+    free(out);
+  }
+  free(lin);
+  return NULL;
+}
+
+int jo_client_leader_batch(int algo, int bits, int length, int chunk, int proofs, const uint8_t verify_key[16],
+                           uint64_t n, const uint64_t *measurements, const uint8_t *nonces, const uint8_t *rands,
+                           uint8_t *public_shares, uint8_t *helper_input_shares, uint8_t *leader_prep_shares,
+                           uint8_t *leader_out_shares, int nthreads) {
+  CFG_OR_FAIL(c);
+  if (nthreads < 1) nthreads = 1;
+  if ((uint64_t)nthreads > n && n > 0) nthreads = (int)n;
+  job_t *jobs = calloc((size_t)nthreads, sizeof(job_t));
+  pthread_t *th = calloc((size_t)nthreads, sizeof(pthread_t));
+  for (int t = 0; t < nthreads; t++) {
+    job_t *j = &jobs[t];
+    j->c = &c;
+    j->vk = verify_key;
+    j->lo = n * t / nthreads;
+    j->hi = n * (t + 1) / nthreads;
+    j->meas = measurements;
+    j->nonces = nonces;
+    j->rands = rands;
+    j->ps_out = public_shares;
+    j->his_out = helper_input_shares;
+    j->lps_out = leader_prep_shares;
+    j->lout = leader_out_shares;
+    pthread_create(&th[t], NULL, client_worker, j);
+  }
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  free(jobs);
+  free(th);
+  return 0;
+}
+
+int jo_aggregate(int algo, int bits, int length, int chunk, int proofs, uint64_t n, const uint8_t *out_shares,
+                 uint8_t *agg_out) {
+  CFG_OR_FAIL(c);
+  fe *agg = calloc((size_t)c.out_len, sizeof(fe));
+  for (uint64_t r = 0; r < n; r++)
+    for (int i = 0; i < c.out_len; i++) {
+      fe v;
+      if (f_decode(c.F, out_shares + ((size_t)r * c.out_len + i) * c.F->enc, &v)) {
+        free(agg);
+        return -1;
+      }
+      agg[i] = f_add(c.F, agg[i], v);
+    }
+  for (int i = 0; i < c.out_len; i++) f_encode(c.F, agg[i], agg_out + (size_t)i * c.F->enc);
+  free(agg);
+  return 0;
+}
+
+/* op: 0 add, 1 sub, 2 mul, 3 inv, 4 root(order 2^a[0]), 5 gen */
+int jo_field_op(int field64, int op, const uint8_t *a, const uint8_t *b, uint8_t *out) {
+  pthread_once(&fields_once, init_fields);
+  const field_t *F = field64 ? &F64 : &F128;
+  fe x = 0, y = 0, r = 0;
+  if (a && op != 4 && f_decode(F, a, &x)) return -1;
+  if (b && f_decode(F, b, &y)) return -1;
+  switch (op) {
+    case 0: r = f_add(F, x, y); break;
+    case 1: r = f_sub(F, x, y); break;
+    case 2: r = f_mul(F, x, y); break;
+    case 3: r = f_inv(F, x); break;
+    case 4: r = f_root(F, a[0]); break;
+    case 5: r = F->gen; break;
+    default: return -1;
+  }
+  f_encode(F, r, out);
+  return 0;
+}
