@@ -40,6 +40,13 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise EngineError(f"{LIB_PATH} is missing: build it with `python -m janus_amd.build` "
                           "(there is no CPU fallback)")
+    # One HIP runtime per process: torch bundles libamdhip64.so (soname libamdhip64.so.7).
+    # Loading torch first makes our NEEDED libamdhip64.so.7 resolve to that same runtime;
+    # loading ours first would put two HSA runtimes in the process and break torch.cuda.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, u8p = ctypes.c_void_p, ctypes.c_void_p
     i32, u32, u64 = ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64

@@ -1,0 +1,133 @@
+"""The device arithmetic headers (janus_amd/csrc/jx_field.h, jx_keccak.h, jx_sha256.h),
+compiled for the host, against Python integers / hashlib / the oracle's Keccak."""
+import ctypes
+import hashlib
+import os
+import random
+import subprocess
+
+import pytest
+
+from oracle import oracle as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+P128 = 2**128 - 28 * 2**64 + 1
+P64 = 2**64 - 2**32 + 1
+R = 2**128
+
+
+@pytest.fixture(scope="module")
+def ht():
+    src = os.path.join(HERE, "csrc", "hosttest.cpp")
+    so = os.path.join(HERE, "csrc", "libjx_hosttest.so")
+    hdrs = [os.path.join(HERE, "..", "janus_amd", "csrc", h) for h in ("jx_field.h", "jx_keccak.h", "jx_sha256.h")]
+    if not os.path.exists(so) or any(os.path.getmtime(h) > os.path.getmtime(so) for h in hdrs + [src]):
+        subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", so, src], check=True)
+    L = ctypes.CDLL(so)
+    vp = ctypes.c_void_p
+    L.ht_f128.argtypes = [ctypes.c_int, vp, vp, vp]
+    L.ht_reduce192.argtypes = [vp, vp]
+    L.ht_mont_lazy.argtypes = [vp, vp, vp]
+    L.ht_f64.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
+    L.ht_f64.restype = ctypes.c_uint64
+    L.ht_keccak_p12.argtypes = [vp]
+    L.ht_sha256_16.argtypes = [vp, vp]
+    L.ht_xof_block.argtypes = [ctypes.c_uint32, ctypes.c_uint32, vp, vp, ctypes.c_int, vp]
+    return L
+
+
+def _b(x, n=16):
+    return ctypes.create_string_buffer(x.to_bytes(n, "little"), n)
+
+
+def f128(L, op, a, b=None):
+    out = ctypes.create_string_buffer(16)
+    L.ht_f128(op, _b(a), _b(b) if b is not None else None, out)
+    return int.from_bytes(out.raw, "little")
+
+
+EDGE = [0, 1, 2, P128 - 1, P128 - 2, 2**127, 2**64, 2**64 - 1, 28 * 2**64 - 1, P128 // 2]
+
+
+def test_field128_add_sub(ht):
+    rnd = random.Random(1)
+    vals = EDGE + [rnd.randrange(P128) for _ in range(200)]
+    for a in vals[:60]:
+        for b in vals[:60]:
+            assert f128(ht, 0, a, b) == (a + b) % P128
+            assert f128(ht, 1, a, b) == (a - b) % P128
+
+
+def test_field128_montgomery(ht):
+    rnd = random.Random(2)
+    rinv = pow(R, P128 - 2, P128)
+    vals = EDGE + [rnd.randrange(P128) for _ in range(300)]
+    for a in vals[:80]:
+        for b in vals[:80]:
+            assert f128(ht, 2, a, b) == a * b * rinv % P128
+    for a in vals:
+        assert f128(ht, 3, a) == a * R % P128
+        assert f128(ht, 4, a) == a * rinv % P128
+
+
+def test_field128_mont_lazy_bound(ht):
+    rnd = random.Random(3)
+    rinv = pow(R, P128 - 2, P128)
+    for _ in range(500):
+        a, b = rnd.choice(EDGE + [rnd.randrange(P128)]), rnd.randrange(P128)
+        out = (ctypes.c_uint64 * 3)()
+        ht.ht_mont_lazy(_b(a), _b(b), out)
+        v = out[0] + (out[1] << 64) + (out[2] << 128)
+        assert v < 2 * P128 and v % P128 == a * b * rinv % P128
+
+
+def test_reduce192(ht):
+    rnd = random.Random(4)
+    cases = [0, 1, P128, 2**192 - 1, 2**128, 2**128 - 1, 64 * 2 * P128] + [rnd.randrange(2**192) for _ in range(500)]
+    for v in cases:
+        w = (ctypes.c_uint64 * 3)(v & (2**64 - 1), (v >> 64) & (2**64 - 1), v >> 128)
+        out = ctypes.create_string_buffer(16)
+        ht.ht_reduce192(w, out)
+        assert int.from_bytes(out.raw, "little") == v % P128, hex(v)
+
+
+def test_field64(ht):
+    rnd = random.Random(5)
+    vals = [0, 1, P64 - 1, P64 - 2, 2**32, 2**32 - 1, 2**63] + [rnd.randrange(P64) for _ in range(300)]
+    for a in vals[:70]:
+        for b in vals[:70]:
+            assert ht.ht_f64(0, a, b) == (a + b) % P64
+            assert ht.ht_f64(1, a, b) == (a - b) % P64
+            assert ht.ht_f64(2, a, b) == a * b % P64
+
+
+def test_keccak_p12_matches_oracle(ht):
+    rnd = random.Random(6)
+    for _ in range(10):
+        st = [rnd.getrandbits(64) for _ in range(25)]
+        arr = (ctypes.c_uint64 * 25)(*st)
+        ht.ht_keccak_p12(arr)
+        assert list(arr) == O.keccak_p1600(st, 12)
+
+
+def test_sha256_16(ht):
+    for _ in range(20):
+        rid = os.urandom(16)
+        out = ctypes.create_string_buffer(32)
+        ht.ht_sha256_16(rid, out)
+        assert out.raw == hashlib.sha256(rid).digest()
+
+
+@pytest.mark.parametrize("usage,binder", [(1, b"\x01"), (2, b"\x01\x01"), (5, b"\x01" + bytes(range(16))),
+                                          (6, bytes(range(32))), (3, b"\x01")])
+def test_xof_block_builder(ht, usage, binder):
+    """blk_xof_prefix + pad == the oracle's XofTurboShake128 message framing."""
+    seed = os.urandom(16)
+    for algo in (0, 2, 0xFFFF1003):
+        w = (ctypes.c_uint32 * 42)()
+        ht.ht_xof_block(algo, usage, seed, binder, len(binder), w)
+        dst = bytes([8, 0]) + algo.to_bytes(4, "big") + usage.to_bytes(2, "big")
+        msg = bytes([8]) + dst + seed + binder
+        blk = bytearray(msg) + b"\x01" + bytes(168 - len(msg) - 1)
+        blk[-1] ^= 0x80
+        assert b"".join(x.to_bytes(4, "little") for x in w) == bytes(blk)

@@ -1,0 +1,80 @@
+"""C oracle vs the independent pure-Python restatement (oracle/pyref.py), small configs.
+
+Also the semantic invariants Janus's integration tests rely on
+(integration_tests/tests/integration/common.rs:298-510): honest reports are accepted and
+leader + helper output shares sum to the encoded measurement; tampered leader shares are
+rejected with the same verdict by both restatements."""
+import random
+
+import pytest
+
+from oracle import oracle as O
+from oracle import pyref
+
+CFGS = [
+    ("count", O.COUNT, {}, (0, 0, 0)),
+    ("sum", O.SUM, dict(bits=5), (5, 0, 0)),
+    ("histogram", O.HISTOGRAM, dict(length=7, chunk=3), (0, 7, 3)),
+    ("sumvec", O.SUMVEC, dict(bits=3, length=4, chunk=5), (3, 4, 5)),
+    ("sumvec_padded", O.SUMVEC, dict(bits=2, length=5, chunk=4), (2, 5, 4)),
+]
+
+
+def _meas(name, rng, kw):
+    if name == "count":
+        return rng.randrange(2)
+    if name == "sum":
+        return rng.randrange(1 << kw["bits"])
+    if name == "histogram":
+        return rng.randrange(kw["length"])
+    return [rng.randrange(1 << kw["bits"]) for _ in range(kw["length"])]
+
+
+@pytest.mark.parametrize("name,algo,kw,args", CFGS, ids=[c[0] for c in CFGS])
+def test_c_oracle_equals_pyref(name, algo, kw, args):
+    rng = random.Random(hash(name) & 0xFFFF)
+    C = O.Prio3Oracle(algo, *args)
+    Py = pyref.Prio3(name.replace("_padded", ""), **kw)
+    vk = bytes(rng.randrange(256) for _ in range(16))
+    for _ in range(3):
+        nonce = bytes(rng.randrange(256) for _ in range(16))
+        rand = bytes(rng.randrange(256) for _ in range(C.sizes.client_rand))
+        m = _meas(name, rng, kw)
+        shard = C.shard(m, nonce, rand)
+        assert shard == Py.shard(m, nonce, rand)
+        ps, lin, hin = shard
+        rc, lshare, lout, _ = C.prep_init(vk, 0, nonce, ps, lin)
+        _, lshare_py = Py.prep_init(vk, 0, nonce, ps, lin)
+        assert rc == 0 and lshare == lshare_py
+        got = C.helper_prep(vk, nonce, ps, hin, lshare)
+        assert got == Py.helper_prep(vk, nonce, ps, hin, lshare)
+        assert got[0] == 0
+        # leader + helper output shares == truncate(encode(measurement))
+        agg = C.aggregate([lout, got[2]])
+        E = C.sizes.field_bytes
+        vals = [int.from_bytes(agg[i:i + E], "little") for i in range(0, len(agg), E)]
+        assert vals == Py.valid.truncate(Py.valid.encode(m))
+        # every single-bit flip of the leader prep share is rejected identically
+        for byte in range(0, len(lshare), max(1, len(lshare) // 9)):
+            t = bytearray(lshare)
+            t[byte] ^= 1 << rng.randrange(8)
+            v_c = C.helper_prep(vk, nonce, ps, hin, bytes(t))[0]
+            assert v_c == Py.helper_prep(vk, nonce, ps, hin, bytes(t))[0]
+            assert v_c in (2, 3, 4)
+
+
+def test_invalid_measurement_rejected():
+    """A client that shards an out-of-range value (bit = 2) fails decide (prepare_message_failure)."""
+    C = O.Prio3Oracle(O.SUMVEC, 1, 3, 2)
+    Py = pyref.Prio3("sumvec", bits=1, length=3, chunk=2)
+    vk, nonce, rand = bytes(16), bytes(range(16)), bytes(range(80))
+    # encode [1, 0, 1] -> meas bits; leader adds 1 to element 1 making it 1 -> still valid; add 2 -> invalid
+    ps, lin, hin = Py.shard([1, 0, 1], nonce, rand)
+    p = Py.F.p
+    lmeas = Py.F.decode_vec(lin[:48])
+    lmeas[1] = (lmeas[1] + 2) % p
+    bad_lin = Py.F.encode_vec(lmeas) + lin[48:]
+    # leader recomputes its prep share from the bad share (its joint-rand part changes too)
+    _, lshare = Py.prep_init(vk, 0, nonce, ps, bad_lin)
+    assert Py.helper_prep(vk, nonce, ps, hin, lshare)[0] in (3, 4)
+    assert C.helper_prep(vk, nonce, ps, hin, lshare)[0] == Py.helper_prep(vk, nonce, ps, hin, lshare)[0]
