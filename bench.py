@@ -120,6 +120,7 @@ def main():
     import torch
     import torch.distributed as dist
 
+    from janus_amd.distributed import ShardCombiner
     from janus_amd.engine import HelperEngine
     from janus_amd.vdaf import Prio3
 
@@ -152,20 +153,13 @@ def main():
     d_verdicts = torch.empty(R, dtype=torch.uint8, device=dev)
     d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
     eng = HelperEngine(vdaf, vk, device=local_rank)
-    out_bytes = vdaf.output_len * 16
-    part = torch.zeros(out_bytes, dtype=torch.uint8, device=dev)
-    gathered = torch.zeros(world * out_bytes, dtype=torch.uint8, device=dev)
-    combined = torch.zeros(out_bytes, dtype=torch.uint8, device=dev)
+    combiner = ShardCombiner(eng) if world > 1 else None
 
     def step():
         eng.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(), d_lps.data_ptr(), R,
                                       0, d_msgs.data_ptr(), d_verdicts.data_ptr())
-        if world > 1:
-            eng.export_aggregate_device(0, part.data_ptr())
-            eng.sync()
-            dist.all_gather_into_tensor(gathered, part)
-            torch.cuda.synchronize()
-            eng.combine_device(gathered.data_ptr(), world, combined.data_ptr())
+        if combiner is not None:  # shard records: RCCL all-gather + device mod-p merge
+            combiner.combine(0)
         eng.sync()
 
     for _ in range(args.warmup):
@@ -207,9 +201,9 @@ def main():
     verified = agg == exp and count == exp_count
     verdict_ok = bool(np.array_equal(d_verdicts.cpu().numpy(), np.tile(want["verdicts"], reps)[:R]))
     if world > 1:
-        combined_np = combined.cpu().numpy().tobytes()
+        c_agg, c_count, _ = combiner.result()
         exp_c = b"".join(((x * world) % P128).to_bytes(16, "little") for x in acc)
-        verified = verified and combined_np == exp_c
+        verified = verified and c_agg == exp_c and c_count == world * exp_count
 
     total_reports = R * world * args.steps
     value = total_reports / elapsed

@@ -124,6 +124,17 @@ int32_t jx_aggregate_reset(jx_engine* e);
 int32_t jx_aggregate_export_device(jx_engine* e, uint32_t segment, void* d_dst);
 int32_t jx_aggregate_combine_device(jx_engine* e, const void* d_parts, uint32_t nparts, void* d_out);
 
+/* Shard records for the multi-GPU combine. A record is the encoded aggregate
+ * share (OUT x FB) || report count (u64 LE) || checksum (32 B) of one aggregation: the state of
+ * one batch_aggregations shard row that compute_aggregate_share merges
+ * (aggregator/src/aggregator/aggregate_share.rs:55-96). Export writes this engine's record for
+ * `segment` to device memory; combine merges `nrecords` records laid out back to back (e.g. the
+ * output of an RCCL all-gather) into one: mod-p sum, count sum, checksum XOR. Both asynchronous
+ * on the engine stream. jx_shard_record_bytes gives the record size. */
+int32_t jx_shard_record_bytes(const jx_engine* e, uint32_t* bytes);
+int32_t jx_shard_record_export_device(jx_engine* e, uint32_t segment, void* d_dst);
+int32_t jx_shard_record_combine_device(jx_engine* e, const void* d_records, uint32_t nrecords, void* d_out);
+
 /* Wait for all work on the engine stream. */
 int32_t jx_engine_sync(jx_engine* e);
 /* The engine's HIP stream (hipStream_t), for callers that order their own work after it. */

@@ -16,7 +16,8 @@ EXPORTED_SYMBOLS = (
     "jx_engine_create", "jx_engine_destroy", "jx_engine_sizes", "jx_engine_set_capacity",
     "jx_helper_prep_batch", "jx_accumulate", "jx_helper_prep_aggregate", "jx_helper_prep_aggregate_device",
     "jx_aggregate_read", "jx_aggregate_checksum", "jx_aggregate_reset", "jx_aggregate_export_device",
-    "jx_aggregate_combine_device", "jx_engine_sync", "jx_engine_stream", "jx_engine_timing",
+    "jx_aggregate_combine_device", "jx_shard_record_bytes", "jx_shard_record_export_device",
+    "jx_shard_record_combine_device", "jx_engine_sync", "jx_engine_stream", "jx_engine_timing",
     "jx_engine_timing_read", "jx_engine_debug", "jx_status_str", "jx_last_error",
 )
 
@@ -65,6 +66,9 @@ def load():
         "jx_aggregate_reset": (i32, [vp]),
         "jx_aggregate_export_device": (i32, [vp, u32, vp]),
         "jx_aggregate_combine_device": (i32, [vp, vp, u32, vp]),
+        "jx_shard_record_bytes": (i32, [vp, P(u32)]),
+        "jx_shard_record_export_device": (i32, [vp, u32, vp]),
+        "jx_shard_record_combine_device": (i32, [vp, vp, u32, vp]),
         "jx_engine_sync": (i32, [vp]),
         "jx_engine_stream": (i32, [vp, P(vp)]),
         "jx_engine_timing": (i32, [vp, i32]),

@@ -44,6 +44,7 @@ struct jx_engine {
   // staging
   uint4 *d_meas = nullptr, *d_proof = nullptr, *d_outs = nullptr, *d_coef = nullptr, *d_consts = nullptr;
   uint32_t* d_flags = nullptr;
+  uint4* d_part = nullptr;
   uint8_t *d_verdicts = nullptr, *d_msgs = nullptr;
   // accumulation scratch: partials + selection bytes
   uint64_t* d_partials = nullptr;
@@ -184,9 +185,9 @@ static int32_t make_cfg(const jx_prio3_params* p, const uint8_t vk[16], Cfg& c, 
       why = "unknown algo_id";
       return JX_E_INVALID;
   }
-  if ((c.algo == ALGO_SUMVEC || c.algo == ALGO_HISTOGRAM) && psum_ppw(c.chunk) < 0) {
-    why = "chunk_length too large for the FLP kernel (<= 128 supported)";
-    return JX_E_UNSUPPORTED;
+  if (c.algo == ALGO_SUMVEC || c.algo == ALGO_HISTOGRAM) {
+    c.ppw = psum_ppw(c.chunk);
+    c.ngroups = (c.chunk + c.ppw - 1) / c.ppw;
   }
   c.P = next_pow2(1 + c.calls);
   c.logP = ilog2(c.P);
@@ -246,12 +247,14 @@ static std::vector<uint4> make_consts(const Cfg& c) {
 
 static void free_staging(jx_engine* e) {
   void* ptrs[] = {e->d_nonces, e->d_ps,       e->d_his,     e->d_lps,  e->d_meas, e->d_proof, e->d_outs,
-                  e->d_coef,   e->d_flags,    e->d_verdicts, e->d_msgs, e->d_partials, e->d_mask, e->d_seg};
+                  e->d_coef,   e->d_flags,    e->d_verdicts, e->d_msgs, e->d_partials, e->d_mask, e->d_seg,
+                  e->d_part};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   e->d_nonces = e->d_ps = e->d_his = e->d_lps = nullptr;
   e->d_meas = e->d_proof = e->d_outs = e->d_coef = nullptr;
   e->d_flags = nullptr;
+  e->d_part = nullptr;
   e->d_verdicts = e->d_msgs = nullptr;
   e->d_partials = nullptr;
   e->d_mask = nullptr;
@@ -263,6 +266,7 @@ static void free_staging(jx_engine* e) {
 static uint64_t per_report_bytes(const Cfg& c) {
   uint64_t b = 16ull * (c.meas_len + c.proof_len + c.ncoef + (c.out_is_meas ? 0 : c.out_len));
   b += 16 + c.ps_bytes + c.his_bytes + c.lps_bytes + 4 + 1 + 16 + 1 + 4 + 1;
+  b += 64ull * c.ngroups;  // FLP partial sums
   return b;
 }
 
@@ -281,6 +285,7 @@ static int32_t ensure_capacity(jx_engine* e, uint64_t n) {
   if (c.algo == ALGO_COUNT || !c.out_is_meas) HIPCHK(e, A((void**)&e->d_outs, cap * c.out_len * 16));
   HIPCHK(e, A((void**)&e->d_coef, cap * c.ncoef * 16));
   HIPCHK(e, A((void**)&e->d_flags, cap * 4));
+  HIPCHK(e, A((void**)&e->d_part, cap * 64ull * c.ngroups));
   HIPCHK(e, A((void**)&e->d_verdicts, cap));
   HIPCHK(e, A((void**)&e->d_msgs, cap * 16));
   HIPCHK(e, A((void**)&e->d_mask, cap));
@@ -367,6 +372,7 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
   b.outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? e->d_meas : e->d_outs;
   b.coef = e->d_coef;
   b.flags = e->d_flags;
+  b.part = e->d_part;
   b.verdicts = verdicts;
   b.msgs = msgs;
   b.consts = e->d_consts;
@@ -683,6 +689,29 @@ int32_t jx_aggregate_combine_device(jx_engine* e, const void* d_parts, uint32_t 
   if (!e || !d_parts || !d_out || nparts == 0) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
   HIPCHK(e, launch_combine(e->cfg, (const uint8_t*)d_parts, nparts, (uint8_t*)d_out, e->stream));
+  return JX_OK;
+}
+
+int32_t jx_shard_record_export_device(jx_engine* e, uint32_t segment, void* d_dst) {
+  if (!e || !d_dst) return JX_E_INVALID;
+  HIPCHK(e, hipSetDevice(e->device));
+  Segment* s = nullptr;
+  int32_t rc = get_segment(e, segment, &s);
+  if (rc) return rc;
+  HIPCHK(e, launch_record_export(e->cfg, s->agg, s->count, s->checksum, (uint8_t*)d_dst, e->stream));
+  return JX_OK;
+}
+
+int32_t jx_shard_record_combine_device(jx_engine* e, const void* d_records, uint32_t nrecords, void* d_out) {
+  if (!e || !d_records || !d_out || nrecords == 0) return JX_E_INVALID;
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, launch_record_combine(e->cfg, (const uint8_t*)d_records, nrecords, (uint8_t*)d_out, e->stream));
+  return JX_OK;
+}
+
+int32_t jx_shard_record_bytes(const jx_engine* e, uint32_t* bytes) {
+  if (!e || !bytes) return JX_E_INVALID;
+  *bytes = e->cfg.out_len * (e->cfg.algo == ALGO_COUNT ? 8u : 16u) + 40u;
   return JX_OK;
 }
 

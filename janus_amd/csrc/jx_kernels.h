@@ -13,6 +13,7 @@ enum : uint32_t {
   FLAG_INIT_FAIL = 1u,  // query randomness t is a P-th root of unity -> prepare_init_failure
   FLAG_NEXT_FAIL = 2u,  // leader's joint-rand part disagrees with the public share -> prepare_next_failure
   FLAG_SLOW = 4u,       // a rejected XOF sample shifted a stream: the slow kernel redoes this report
+  FLAG_DFAIL = 8u,      // a leader verifier element is >= p -> leader_prep_share_decode_failure
 };
 
 // Interleaved staging: element e of report r lives at [(r/64)][e][r%64] (16 bytes each),
@@ -25,6 +26,7 @@ struct Cfg {
   uint32_t ps_bytes, his_bytes, lps_bytes;
   uint32_t ncoef;        // coefficient slots per report
   uint32_t out_is_meas;  // truncate == identity (Histogram): output share aliases the meas staging
+  uint32_t ppw, ngroups; // ParallelSum FLP: chunk slots per group, groups per 64-report block
   uint32_t vk[4];
   // constant table offsets (uint4 units) in Bufs::consts
   uint32_t c_omega, c_S, c_misc;
@@ -52,6 +54,7 @@ struct Bufs {
   uint4* outs;
   uint4* coef;
   uint32_t* flags;
+  uint4* part;  // ParallelSum FLP partial sums [blk][group][4][lane]
   uint8_t* verdicts;
   uint8_t* msgs;
   const uint4* consts;
@@ -81,6 +84,9 @@ hipError_t launch_xof_slow(const Cfg& c, const Bufs& b, hipStream_t s);
 hipError_t launch_flp(const Cfg& c, const Bufs& b, hipStream_t s);
 hipError_t launch_accumulate(const Cfg& c, const AccArgs& a, uint4* agg, hipStream_t s);
 hipError_t launch_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, hipStream_t s);
+hipError_t launch_record_export(const Cfg& c, const uint4* agg, const unsigned long long* count,
+                                const uint32_t* checksum, uint8_t* dst, hipStream_t s);
+hipError_t launch_record_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, hipStream_t s);
 hipError_t launch_transpose_out(const Cfg& c, const uint4* outs, uint64_t n, uint8_t* dst, hipStream_t s);
 hipError_t launch_agg_encode(const Cfg& c, const uint4* agg, uint8_t* dst, hipStream_t s);
 

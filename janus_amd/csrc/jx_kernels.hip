@@ -16,6 +16,8 @@
 //
 // Prio3Count (Field64, 3 permutations) runs as one lane-per-report kernel.
 // Algorithm: draft-irtf-cfrg-vdaf-08 as implemented by prio 0.16.1; see DESIGN.md.
+#include <stdlib.h>
+
 #include "jx_field.h"
 #include "jx_kernels.h"
 #include "jx_keccak.h"
@@ -736,17 +738,32 @@ __global__ __launch_bounds__(256) void flp_sum_kernel(Cfg c, Bufs b) {
 }
 
 // Prio3SumVec / Prio3Histogram: gadget ParallelSum(Mul, chunk), arity 2*chunk.
-// One 64-report block per workgroup; wave w owns chunk positions [w*PPW, (w+1)*PPW).
-template <int PPW, bool HIST, int MAXT>
-__global__ __launch_bounds__(MAXT) void flp_psum_kernel(Cfg c, Bufs b) {
-  extern __shared__ uint4 sh[];
-  const uint32_t NW = blockDim.x >> 6;
-  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t blk = blockIdx.x;
+//
+// Phase 1 (flp_psum_part_kernel): one wave per (64-report block, slot group). Lanes are
+// reports (the interleaved staging makes every load a coalesced 1 KiB). Group g owns the
+// chunk slots [g*PPW, (g+1)*PPW) -- 2*PPW lazy wire accumulators per lane, small enough to
+// stay in registers at >= 3 waves/SIMD -- and the gadget-polynomial coefficients
+// [g*per, (g+1)*per). It writes four partial sums per report: sum_i Ve_i*Vo_i over its
+// slots, its share of v (sum_m g_m S_m), its share of G(t), and (Histogram) sum of x.
+// Phase 2 (flp_psum_final_kernel): one report per lane; adds the partials, the leader's
+// v and G(t), and decides.
+template <int PPW, bool HIST>
+__global__ __launch_bounds__(64) void flp_psum_part_kernel(Cfg c, Bufs b) {
+  const uint32_t NG = c.ngroups;
+  // Workgroup ids are dispatched round-robin over the 8 XCDs; map them so that the NG
+  // groups of one block run back to back on one XCD and share its L2 (coefficients,
+  // leader share).
+  const uint32_t bid = blockIdx.x;
+  const uint32_t xcd = bid & 7u, q = bid >> 3;
+  const uint32_t g = q % NG;
+  const uint64_t blk = (uint64_t)(q / NG) * 8 + xcd;
+  const uint64_t nblk = (b.n + 63) / 64;
+  if (blk >= nblk) return;
+  const uint32_t lane = threadIdx.x;
   const uint64_t r0 = blk * 64 + lane;
   const uint64_t r = r0 < b.n ? r0 : b.n - 1;
   const uint32_t NC = c.ncoef, C = c.calls, chunk = c.chunk, M = c.meas_len, A = 2 * chunk;
-  const uint32_t j0 = w * PPW;
+  const uint32_t j0 = g * PPW;
 
   acc192 ae[PPW], ao[PPW], sx;
 #pragma unroll
@@ -757,12 +774,13 @@ __global__ __launch_bounds__(MAXT) void flp_psum_kernel(Cfg c, Bufs b) {
   acc_zero(sx);
   const uint4* coefb = b.coef + il_idx(blk, NC, 0, lane);
   const uint4* measb = b.meas + il_idx(blk, M, 0, lane);
+  const bool full = j0 + PPW <= chunk;
+#pragma unroll 1
   for (uint32_t k = 1; k <= C; k++) {
     const f128 ck = u4_to_f(coefb[(COEF_K + 2 * (k - 1)) * IL]);
     const f128 dk = u4_to_f(coefb[(COEF_K + 2 * (k - 1) + 1) * IL]);
     const uint32_t nb = (k - 1) * chunk + j0;
-    if (k < C && j0 + PPW <= chunk) {
-      // steady state: all PPW positions valid
+    if (full && nb + PPW <= M) {
       f128 x[PPW];
 #pragma unroll
       for (int i = 0; i < PPW; i++) x[i] = u4_to_f(measb[(uint64_t)(nb + i) * IL]);
@@ -792,7 +810,7 @@ __global__ __launch_bounds__(MAXT) void flp_psum_kernel(Cfg c, Bufs b) {
       }
     }
   }
-  // ---- wires at t, add the leader's verifier share, partial decide sum
+  // ---- wires at t for this group's slots, plus the leader's verifier share
   const f128 LR = u4_to_f(coefb[COEF_L * IL]), c0R = u4_to_f(coefb[COEF_C0 * IL]);
   const f128 hs = u4_to_f(coefb[COEF_HALFSUM * IL]), tR = u4_to_f(coefb[COEF_T * IL]);
   const f128 rR = u4_to_f(coefb[COEF_R * IL]);
@@ -814,50 +832,53 @@ __global__ __launch_bounds__(MAXT) void flp_psum_kernel(Cfg c, Bufs b) {
       prod = add128(prod, mont128(Ve, Vo));
     }
   }
-  // ---- gadget polynomial: v-part = sum_m g_m * S_m, G(t) part, over this wave's m-range
+  // ---- gadget polynomial: v-part = sum_m g_m * S_m and the G(t) part over this group's m-range
   const uint32_t GL = c.gpoly_len;
-  const uint32_t per = (GL + NW - 1) / NW;
-  const uint32_t m0 = w * per, m1 = min(GL, m0 + per);
+  const uint32_t per = (GL + NG - 1) / NG;
+  const uint32_t m0 = g * per, m1 = min(GL, m0 + per);
   const uint4* Sm = b.consts + c.c_S;
   f128 vpart = make128(0, 0), gpart = make128(0, 0);
   if (m0 < m1) {
     for (uint32_t m = m1; m-- > m0;) {
-      f128 g = ld_il(b.proof, blk, c.proof_len, A + m, lane);
-      vpart = add128(vpart, mont128(g, u4_to_f(Sm[m])));
-      gpart = add128(mont128(gpart, tR), g);
+      f128 gm = ld_il(b.proof, blk, c.proof_len, A + m, lane);
+      vpart = add128(vpart, mont128(gm, u4_to_f(Sm[m])));
+      gpart = add128(mont128(gpart, tR), gm);
     }
     gpart = mont128(gpart, mpow(tR, m0));
   }
-  // ---- cross-wave reduction in LDS
-  uint4* shp = sh + (w * 64 + lane) * 4;
-  shp[0] = f_to_u4(prod);
-  shp[1] = f_to_u4(vpart);
-  shp[2] = f_to_u4(gpart);
-  shp[3] = HIST ? f_to_u4(acc_reduce(sx)) : make_uint4(0, 0, 0, 0);
-  __shared__ uint32_t dfs[16 * 64];
-  dfs[w * 64 + lane] = dfail;
-  __syncthreads();
-  if (w != 0) return;
+  uint4* pp = b.part + ((blk * NG + g) * 4) * IL + lane;
+  pp[0] = f_to_u4(prod);
+  pp[IL] = f_to_u4(vpart);
+  pp[2 * IL] = f_to_u4(gpart);
+  if (HIST) pp[3 * IL] = f_to_u4(acc_reduce(sx));
+  if (dfail && r0 < b.n) atomicOr(&b.flags[r0], FLAG_DFAIL);
+}
+
+template <bool HIST>
+__global__ __launch_bounds__(256) void flp_psum_final_kernel(Cfg c, Bufs b) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= b.n) return;
+  const uint64_t blk = r / 64;
+  const uint32_t lane = r % 64, NG = c.ngroups, A = 2 * c.chunk;
   f128 P = make128(0, 0), V = make128(0, 0), G = make128(0, 0), SX = make128(0, 0);
-  bool df = false;
-  for (uint32_t q = 0; q < NW; q++) {
-    const uint4* s = sh + (q * 64 + lane) * 4;
-    P = add128(P, u4_to_f(s[0]));
-    V = add128(V, u4_to_f(s[1]));
-    G = add128(G, u4_to_f(s[2]));
-    if (HIST) SX = add128(SX, u4_to_f(s[3]));
-    df |= dfs[q * 64 + lane] != 0;
+  const uint4* pp = b.part + (blk * NG * 4) * IL + lane;
+  for (uint32_t g = 0; g < NG; g++, pp += 4 * IL) {
+    P = add128(P, u4_to_f(pp[0]));
+    V = add128(V, u4_to_f(pp[IL]));
+    G = add128(G, u4_to_f(pp[2 * IL]));
+    if (HIST) SX = add128(SX, u4_to_f(pp[3 * IL]));
   }
   f128 vh = V;
   if (HIST) {
     // v = jr1 * range_check + jr1^2 * (sum(x) - 1/2)
-    const f128 r2R = u4_to_f(coefb[COEF_R2 * IL]);
+    const f128 r2R = ld_il(b.coef, blk, c.ncoef, COEF_R2, lane);
     const f128 half = u4_to_f(b.consts[c.c_misc + 1]);
     f128 sc = sub128(SX, half);
     vh = add128(mont128(V, r2R), mont128(sc, mont128(r2R, r2R)));
   }
-  f128 lv = ld_lead(b, c, r, 0, df), lg = ld_lead(b, c, r, A + 1, df);
   const uint32_t flags = b.flags[r];
+  bool df = (flags & FLAG_DFAIL) != 0;
+  f128 lv = ld_lead(b, c, r, 0, df), lg = ld_lead(b, c, r, A + 1, df);
   uint32_t verdict = 0;
   if (flags & FLAG_INIT_FAIL)
     verdict = 1;
@@ -870,7 +891,7 @@ __global__ __launch_bounds__(MAXT) void flp_psum_kernel(Cfg c, Bufs b) {
     else if (flags & FLAG_NEXT_FAIL)
       verdict = 4;
   }
-  if (r0 < b.n) b.verdicts[r0] = (uint8_t)verdict;
+  b.verdicts[r] = (uint8_t)verdict;
 }
 
 // ---------------------------------------------------------------------------- K4: accumulate
@@ -993,6 +1014,73 @@ __global__ void combine_kernel(Cfg c, const uint8_t* parts, uint32_t nparts, uin
   }
 }
 
+// shard record = encoded aggregate share || count (u64 LE) || checksum (32 B), see
+// janus_amd/distributed.py. Thread i < out_len writes element i; thread out_len the tail.
+__global__ void record_export_kernel(Cfg c, const uint4* agg, const unsigned long long* count,
+                                     const uint32_t* checksum, uint8_t* dst) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t fb = c.algo == ALGO_COUNT ? 8 : 16;
+  if (i < c.out_len) {
+    uint4 v = agg[i];
+    for (uint32_t k = 0; k < fb; k++) {
+      uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+      dst[(uint64_t)i * fb + k] = (uint8_t)(w >> (8 * (k & 3)));
+    }
+  } else if (i == c.out_len) {
+    uint8_t* t = dst + (uint64_t)c.out_len * fb;
+    const unsigned long long n = *count;
+    for (int k = 0; k < 8; k++) t[k] = (uint8_t)(n >> (8 * k));
+    for (int k = 0; k < 32; k++) t[8 + k] = (uint8_t)(checksum[k >> 2] >> (8 * (k & 3)));
+  }
+}
+
+// merge nparts shard records (compute_aggregate_share, aggregate_share.rs:87-95):
+// mod-p sum of the aggregate shares, sum of the counts, XOR of the checksums.
+__global__ void record_combine_kernel(Cfg c, const uint8_t* parts, uint32_t nparts, uint8_t* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t fb = c.algo == ALGO_COUNT ? 8 : 16;
+  const uint64_t stride = (uint64_t)c.out_len * fb + 40;
+  if (i < c.out_len) {
+    if (fb == 8) {
+      uint64_t s = 0;
+      for (uint32_t q = 0; q < nparts; q++) {
+        const uint8_t* p = parts + q * stride + (uint64_t)i * 8;
+        uint64_t v = 0;
+        for (int k = 7; k >= 0; k--) v = (v << 8) | p[k];
+        s = add64(s, v >= P64 ? v - P64 : v);
+      }
+      for (int k = 0; k < 8; k++) out[(uint64_t)i * 8 + k] = (uint8_t)(s >> (8 * k));
+    } else {
+      f128 s = make128(0, 0);
+      for (uint32_t q = 0; q < nparts; q++) {
+        const uint8_t* p = parts + q * stride + (uint64_t)i * 16;
+        uint64_t lo = 0, hi = 0;
+        for (int k = 7; k >= 0; k--) lo = (lo << 8) | p[k];
+        for (int k = 15; k >= 8; k--) hi = (hi << 8) | p[k];
+        f128 v = make128(lo, hi);
+        if (ge_p128(v)) v = sub128(v, make128(P128_LO, P128_HI));
+        s = add128(s, v);
+      }
+      for (int k = 0; k < 8; k++) out[(uint64_t)i * 16 + k] = (uint8_t)(s.lo >> (8 * k));
+      for (int k = 0; k < 8; k++) out[(uint64_t)i * 16 + 8 + k] = (uint8_t)(s.hi >> (8 * k));
+    }
+  } else if (i == c.out_len) {
+    const uint64_t tail = (uint64_t)c.out_len * fb;
+    uint64_t n = 0;
+    uint8_t cs[32];
+    for (int k = 0; k < 32; k++) cs[k] = 0;
+    for (uint32_t q = 0; q < nparts; q++) {
+      const uint8_t* p = parts + q * stride + tail;
+      uint64_t v = 0;
+      for (int k = 7; k >= 0; k--) v = (v << 8) | p[k];
+      n += v;
+      for (int k = 0; k < 32; k++) cs[k] ^= p[8 + k];
+    }
+    for (int k = 0; k < 8; k++) out[tail + k] = (uint8_t)(n >> (8 * k));
+    for (int k = 0; k < 32; k++) out[tail + 8 + k] = cs[k];
+  }
+}
+
 // interleaved output shares -> [r][i] LE bytes
 __global__ void transpose_out_kernel(Cfg c, const uint4* outs, uint64_t n, uint8_t* dst) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1036,18 +1124,22 @@ hipError_t launch_xof_slow(const Cfg& c, const Bufs& b, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Slots per FLP group: the widest of 4/2/1 unless a narrower one wastes fewer padded
+// slot-lanes (each group also pays a fixed per-call cost for its coefficient loads).
+// PPW = 8 needs > 200 VGPRs (2 waves/SIMD) and is only reachable through JX_PPW.
 int psum_ppw(uint32_t chunk) {
-  // positions per wave: minimise padded positions. Register-heavy widths (>= 8 positions,
-  // 2*PPW lazy accumulators) are limited to 8 waves (512 threads, 256 VGPRs); narrow ones to 16.
-  const int cands[] = {16, 11, 8, 4, 2, 1};
-  int best = -1, best_waste = 1 << 30;
+  if (const char* env = getenv("JX_PPW")) {
+    int v = atoi(env);
+    if (v == 8 || v == 4 || v == 2 || v == 1) return v;
+  }
+  const int cands[] = {4, 2, 1};
+  int best = 4, best_cost = 1 << 30;
   for (int p : cands) {
-    int nw = (chunk + p - 1) / p;
-    if (nw > (p >= 8 ? 8 : 16)) continue;
-    int waste = nw * p - (int)chunk;
-    if (waste < best_waste) {
+    int ng = (int)((chunk + p - 1) / p);
+    int cost = ng * p + 2 * ng;
+    if (cost < best_cost) {
       best = p;
-      best_waste = waste;
+      best_cost = cost;
     }
   }
   return best;
@@ -1055,14 +1147,15 @@ int psum_ppw(uint32_t chunk) {
 
 template <int PPW>
 static hipError_t launch_psum_t(const Cfg& c, const Bufs& b, hipStream_t s) {
-  uint32_t nb = nblk_of(b.n);
-  uint32_t nw = (c.chunk + PPW - 1) / PPW;
-  size_t shmem = (size_t)nw * 64 * 4 * sizeof(uint4);
-  constexpr int MAXT = PPW >= 8 ? 512 : 1024;
-  if (c.algo == ALGO_HISTOGRAM)
-    hipLaunchKernelGGL((flp_psum_kernel<PPW, true, MAXT>), dim3(nb), dim3(nw * 64), shmem, s, c, b);
-  else
-    hipLaunchKernelGGL((flp_psum_kernel<PPW, false, MAXT>), dim3(nb), dim3(nw * 64), shmem, s, c, b);
+  const uint32_t nb = nblk_of(b.n);
+  const uint32_t grid = ((nb + 7) / 8) * 8 * c.ngroups;
+  if (c.algo == ALGO_HISTOGRAM) {
+    hipLaunchKernelGGL((flp_psum_part_kernel<PPW, true>), dim3(grid), dim3(64), 0, s, c, b);
+    hipLaunchKernelGGL((flp_psum_final_kernel<true>), dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, c, b);
+  } else {
+    hipLaunchKernelGGL((flp_psum_part_kernel<PPW, false>), dim3(grid), dim3(64), 0, s, c, b);
+    hipLaunchKernelGGL((flp_psum_final_kernel<false>), dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, c, b);
+  }
   return hipGetLastError();
 }
 
@@ -1072,11 +1165,7 @@ hipError_t launch_flp(const Cfg& c, const Bufs& b, hipStream_t s) {
     hipLaunchKernelGGL(flp_sum_kernel, dim3((nb + 3) / 4), dim3(256), 0, s, c, b);
     return hipGetLastError();
   }
-  switch (psum_ppw(c.chunk)) {
-    case 16:
-      return launch_psum_t<16>(c, b, s);
-    case 11:
-      return launch_psum_t<11>(c, b, s);
+  switch (c.ppw) {
     case 8:
       return launch_psum_t<8>(c, b, s);
     case 4:
@@ -1104,6 +1193,17 @@ hipError_t launch_accumulate(const Cfg& c, const AccArgs& a, uint4* agg, hipStre
 
 hipError_t launch_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, hipStream_t s) {
   hipLaunchKernelGGL(combine_kernel, dim3((c.out_len + 255) / 256), dim3(256), 0, s, c, parts, nparts, out);
+  return hipGetLastError();
+}
+hipError_t launch_record_export(const Cfg& c, const uint4* agg, const unsigned long long* count,
+                                const uint32_t* checksum, uint8_t* dst, hipStream_t s) {
+  hipLaunchKernelGGL(record_export_kernel, dim3((c.out_len + 1 + 255) / 256), dim3(256), 0, s, c, agg, count,
+                     checksum, dst);
+  return hipGetLastError();
+}
+hipError_t launch_record_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(record_combine_kernel, dim3((c.out_len + 1 + 255) / 256), dim3(256), 0, s, c, parts, nparts,
+                     out);
   return hipGetLastError();
 }
 hipError_t launch_transpose_out(const Cfg& c, const uint4* outs, uint64_t n, uint8_t* dst, hipStream_t s) {

@@ -187,6 +187,21 @@ class HelperEngine:
         check(self._L.jx_aggregate_combine_device(self._h, d_parts, nparts, d_out), self._h,
               "jx_aggregate_combine_device")
 
+    def record_bytes(self) -> int:
+        b = ctypes.c_uint32()
+        check(self._L.jx_shard_record_bytes(self._h, ctypes.byref(b)), self._h, "jx_shard_record_bytes")
+        return b.value
+
+    def export_record_device(self, segment: int, d_dst: int):
+        """Write this engine's shard record (agg share || count || checksum) to device memory."""
+        check(self._L.jx_shard_record_export_device(self._h, segment, d_dst), self._h,
+              "jx_shard_record_export_device")
+
+    def combine_records_device(self, d_records: int, nrecords: int, d_out: int):
+        """Merge nrecords back-to-back shard records on the device (compute_aggregate_share)."""
+        check(self._L.jx_shard_record_combine_device(self._h, d_records, nrecords, d_out), self._h,
+              "jx_shard_record_combine_device")
+
     def set_capacity(self, reports: int):
         check(self._L.jx_engine_set_capacity(self._h, reports), self._h, "jx_engine_set_capacity")
 

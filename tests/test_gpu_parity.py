@@ -197,3 +197,36 @@ def test_multi_part_combine():
     assert out.cpu().numpy().tobytes() == want["agg"]
     for e in engs:
         e.close()
+
+
+@pytest.mark.parametrize("name", ["count", "sumvec_small", "histogram_256_16"])
+def test_shard_records_device_merge(name):
+    """Shard records exported per engine, merged on the device (the step after the RCCL
+    all-gather, janus_amd/distributed.py) == host merge == oracle over the whole batch."""
+    import torch
+
+    from janus_amd import distributed as D
+
+    vdaf = CASES[name]
+    vk = bytes(range(16))
+    orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
+    n, world = 150, 3
+    nonces, ps, his, lps = _random_batch(orc, vk, n, seed=21)
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16)
+    engs = [HelperEngine(vdaf, vk) for _ in range(world)]
+    nb = engs[0].record_bytes()
+    assert nb == D.record_bytes(vdaf.output_len, vdaf.field_bytes)
+    recs = torch.zeros((world, nb), dtype=torch.uint8, device="cuda")
+    for r, eng in enumerate(engs):
+        a, b = D.shard_range(n, r, world)
+        eng.prep_and_aggregate(nonces[a:b], ps[a:b], his[a:b], lps[a:b])
+        eng.export_record_device(0, recs[r].data_ptr())
+        eng.sync()
+    out = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+    engs[0].combine_records_device(recs.data_ptr(), world, out.data_ptr())
+    engs[0].sync()
+    agg, count, cs = D.unpack_record(out.cpu().numpy(), vdaf.field_bytes)
+    assert (agg, count, cs) == (want["agg"], want["count"], want["checksum"])
+    assert D.merge_records(recs.cpu().numpy(), vdaf.field_bytes) == (agg, count, cs)
+    for e in engs:
+        e.close()
