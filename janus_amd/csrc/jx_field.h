@@ -237,6 +237,81 @@ JX_HD void acc_add128(acc192& a, f128 v) { acc_add(a, v.lo, v.hi, 0); }
 JX_HD f128 acc_reduce(const acc192& a) { return reduce192(a.w0, a.w1, a.w2); }
 
 // ----------------------------------------------------------------------------
+// Wide lazy dot products for the FLP wire sums  sum_k x_k * c_k  (thousands of terms per
+// report). Operands are split into five 26-bit limbs; one limb product is < 2^52, so nine
+// 64-bit column accumulators absorb every partial product with a single v_mad_u64_u32 and
+// no carry handling for up to 4096 / 5 terms per column between normalisations. The sum is
+// reduced mod p once, at the end.
+
+struct limbs26 {
+  uint32_t l[5];
+};
+JX_HD limbs26 to_limbs26(f128 a) {
+  const uint32_t M = (1u << 26) - 1;
+  const uint32_t w0 = lo32(a.lo), w1 = hi32(a.lo), w2 = lo32(a.hi), w3 = hi32(a.hi);
+  limbs26 r;
+  r.l[0] = w0 & M;
+  r.l[1] = (uint32_t)(((((uint64_t)w1) << 32) | w0) >> 26) & M;
+  r.l[2] = (uint32_t)(((((uint64_t)w2) << 32) | w1) >> 20) & M;
+  r.l[3] = (uint32_t)(((((uint64_t)w3) << 32) | w2) >> 14) & M;
+  r.l[4] = w3 >> 8;
+  return r;
+}
+
+struct wacc26 {
+  uint64_t col[9];  // value = sum_s col[s] * 2^(26 s)
+};
+JX_HD void wacc_zero(wacc26& a) {
+#pragma unroll
+  for (int s = 0; s < 9; s++) a.col[s] = 0;
+}
+JX_HD void wacc_mac(wacc26& a, const limbs26& x, const limbs26& c) {
+#pragma unroll
+  for (int i = 0; i < 5; i++)
+#pragma unroll
+    for (int j = 0; j < 5; j++) a.col[i + j] += (uint64_t)x.l[i] * c.l[j];
+}
+// carry-propagate so that col[0..7] < 2^26 (keeps headroom for further terms)
+JX_HD void wacc_normalize(wacc26& a) {
+  const uint64_t M = (1ull << 26) - 1;
+#pragma unroll
+  for (int s = 0; s < 8; s++) {
+    a.col[s + 1] += a.col[s] >> 26;
+    a.col[s] &= M;
+  }
+}
+// value mod p (canonical), for values < 2^320
+JX_HD f128 wacc_reduce(wacc26 a) {
+  wacc_normalize(a);
+  // pack the 26-bit limbs (top limb wider) into five 64-bit words
+  uint64_t o[5] = {0, 0, 0, 0, 0};
+  int oi = 0, nb = 0;
+  uint64_t buf_lo = 0, buf_hi = 0;  // 128-bit bit buffer
+#pragma unroll
+  for (int s = 0; s < 9; s++) {
+    const uint64_t v = a.col[s];
+    // buf |= v << nb  (nb < 64)
+    buf_lo |= v << nb;
+    buf_hi |= nb ? (v >> (64 - nb)) : 0;
+    nb += 26;
+    if (nb >= 64) {
+      o[oi++] = buf_lo;
+      buf_lo = buf_hi;
+      buf_hi = 0;
+      nb -= 64;
+    }
+  }
+  // flush: the top limb may hold up to 64 bits beyond position 208
+  if (oi < 5) o[oi++] = buf_lo;
+  if (oi < 5) o[oi++] = buf_hi;
+  // Horner from the top word: r = (r * 2^64 + o[i]) mod p
+  f128 r = make128(0, 0);
+#pragma unroll
+  for (int i = 4; i >= 0; i--) r = reduce192(o[i], r.lo, r.hi);
+  return r;
+}
+
+// ----------------------------------------------------------------------------
 // Field64 (Goldilocks) p = 2^64 - 2^32 + 1, canonical representation
 
 constexpr uint64_t P64 = 0xFFFFFFFF00000001ull;

@@ -765,48 +765,66 @@ __global__ __launch_bounds__(64) void flp_psum_part_kernel(Cfg c, Bufs b) {
   const uint32_t NC = c.ncoef, C = c.calls, chunk = c.chunk, M = c.meas_len, A = 2 * chunk;
   const uint32_t j0 = g * PPW;
 
-  acc192 ae[PPW], ao[PPW], sx;
+  // wire sums over the calls: ae[i] = sum_k d_k x_{k,i} * R, ao[i] = sum_k c_k x_{k,i} * R
+  // (c_k, d_k are stored in Montgomery form), as unreduced 26-bit-limb column sums.
+  wacc26 ae[PPW], ao[PPW];
+  acc192 sx;
 #pragma unroll
   for (int i = 0; i < PPW; i++) {
-    acc_zero(ae[i]);
-    acc_zero(ao[i]);
+    wacc_zero(ae[i]);
+    wacc_zero(ao[i]);
   }
   acc_zero(sx);
   const uint4* coefb = b.coef + il_idx(blk, NC, 0, lane);
   const uint4* measb = b.meas + il_idx(blk, M, 0, lane);
-  const bool full = j0 + PPW <= chunk;
+  // calls whose PPW slots of this group are all real measurement elements run branch-free;
+  // the rest (the ragged last chunk, slots beyond chunk) take the guarded tail loop
+  uint32_t kf = 0;
+  if (j0 + PPW <= chunk && M >= j0 + PPW) kf = min(C, (M - j0 - PPW) / chunk + 1);
+  for (uint32_t k0 = 1; k0 <= kf; k0 += 512) {  // <= 5 * 512 limb products (< 2^52) per column
+    const uint32_t k1 = min(kf, k0 + 511);
 #pragma unroll 1
-  for (uint32_t k = 1; k <= C; k++) {
-    const f128 ck = u4_to_f(coefb[(COEF_K + 2 * (k - 1)) * IL]);
-    const f128 dk = u4_to_f(coefb[(COEF_K + 2 * (k - 1) + 1) * IL]);
-    const uint32_t nb = (k - 1) * chunk + j0;
-    if (full && nb + PPW <= M) {
+    for (uint32_t k = k0; k <= k1; k++) {
+      const limbs26 ck = to_limbs26(u4_to_f(coefb[(COEF_K + 2 * (k - 1)) * IL]));
+      const limbs26 dk = to_limbs26(u4_to_f(coefb[(COEF_K + 2 * (k - 1) + 1) * IL]));
+      const uint32_t nb = (k - 1) * chunk + j0;
       f128 x[PPW];
 #pragma unroll
       for (int i = 0; i < PPW; i++) x[i] = u4_to_f(measb[(uint64_t)(nb + i) * IL]);
 #pragma unroll
       for (int i = 0; i < PPW; i++) {
-        uint64_t lo, hi;
-        uint32_t top;
-        mont128_lazy(x[i], dk, lo, hi, top);
-        acc_add(ae[i], lo, hi, top);
-        mont128_lazy(x[i], ck, lo, hi, top);
-        acc_add(ao[i], lo, hi, top);
+        const limbs26 xl = to_limbs26(x[i]);
+        wacc_mac(ae[i], xl, dk);
+        wacc_mac(ao[i], xl, ck);
         if (HIST) acc_add128(sx, x[i]);
       }
-    } else {
+    }
+#pragma unroll
+    for (int i = 0; i < PPW; i++) {
+      wacc_normalize(ae[i]);
+      wacc_normalize(ao[i]);
+    }
+  }
+#pragma unroll 1
+  for (uint32_t k = kf + 1; k <= C; k++) {  // the ragged last call(s), or every call of a padded group
+    const limbs26 ck = to_limbs26(u4_to_f(coefb[(COEF_K + 2 * (k - 1)) * IL]));
+    const limbs26 dk = to_limbs26(u4_to_f(coefb[(COEF_K + 2 * (k - 1) + 1) * IL]));
+    const uint32_t nb = (k - 1) * chunk + j0;
+#pragma unroll
+    for (int i = 0; i < PPW; i++) {
+      if (j0 + i < chunk && nb + i < M) {
+        const f128 x = u4_to_f(measb[(uint64_t)(nb + i) * IL]);
+        const limbs26 xl = to_limbs26(x);
+        wacc_mac(ae[i], xl, dk);
+        wacc_mac(ao[i], xl, ck);
+        if (HIST) acc_add128(sx, x);
+      }
+    }
+    if (((k - kf) & 511u) == 0) {
 #pragma unroll
       for (int i = 0; i < PPW; i++) {
-        if (j0 + i < chunk && nb + i < M) {
-          f128 x = u4_to_f(measb[(uint64_t)(nb + i) * IL]);
-          uint64_t lo, hi;
-          uint32_t top;
-          mont128_lazy(x, dk, lo, hi, top);
-          acc_add(ae[i], lo, hi, top);
-          mont128_lazy(x, ck, lo, hi, top);
-          acc_add(ao[i], lo, hi, top);
-          if (HIST) acc_add128(sx, x);
-        }
+        wacc_normalize(ae[i]);
+        wacc_normalize(ao[i]);
       }
     }
   }
@@ -823,7 +841,8 @@ __global__ __launch_bounds__(64) void flp_psum_part_kernel(Cfg c, Bufs b) {
     if (j < chunk) {
       f128 se = ld_il(b.proof, blk, c.proof_len, 2 * j, lane);
       f128 so = ld_il(b.proof, blk, c.proof_len, 2 * j + 1, lane);
-      f128 E = acc_reduce(ae[i]), O = acc_reduce(ao[i]);
+      // from Montgomery form: E = sum_k d_k x_{k,i}, O = sum_k c_k x_{k,i} (canonical)
+      f128 E = mont128(wacc_reduce(ae[i]), make128(1, 0)), O = mont128(wacc_reduce(ao[i]), make128(1, 0));
       f128 We = mont128(add128(mont128(se, c0R), mont128(E, rpow)), LR);
       f128 Wo = mont128(sub128(add128(mont128(so, c0R), O), hs), LR);
       rpow = mont128(rpow, rR);
@@ -1124,19 +1143,20 @@ hipError_t launch_xof_slow(const Cfg& c, const Bufs& b, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Slots per FLP group: the widest of 4/2/1 unless a narrower one wastes fewer padded
-// slot-lanes (each group also pays a fixed per-call cost for its coefficient loads).
-// PPW = 8 needs > 200 VGPRs (2 waves/SIMD) and is only reachable through JX_PPW.
+// Slots per FLP group. Each slot holds two 9-column wide accumulators (36 VGPRs); PPW = 2
+// (152 VGPRs, 3 waves/SIMD) measured fastest on MI355X for SumVec(8x1000/88): K3 11.8 ms vs
+// 13.6 (PPW 1) and 12.5 (PPW 4, spills) per 312,500 reports. PPW = 1 only when it wastes
+// fewer padded slot-lanes (chunk_length 1). JX_PPW overrides (4/8 spill; experiments only).
 int psum_ppw(uint32_t chunk) {
   if (const char* env = getenv("JX_PPW")) {
     int v = atoi(env);
     if (v == 8 || v == 4 || v == 2 || v == 1) return v;
   }
-  const int cands[] = {4, 2, 1};
-  int best = 4, best_cost = 1 << 30;
+  const int cands[] = {2, 1};
+  int best = 2, best_cost = 1 << 30;
   for (int p : cands) {
     int ng = (int)((chunk + p - 1) / p);
-    int cost = ng * p + 2 * ng;
+    int cost = ng * p + 3 * ng;
     if (cost < best_cost) {
       best = p;
       best_cost = cost;

@@ -44,6 +44,17 @@ void ht_mont_lazy(const uint8_t* a, const uint8_t* b, uint64_t out[3]) {
   out[1] = hi;
   out[2] = top;
 }
+// sum_k xs[k] * cs[k] mod p through the 26-bit-limb column accumulator, normalising every
+// `norm_every` terms (the FLP kernel normalises every 512 calls)
+void ht_wide_dot(const uint8_t* xs, const uint8_t* cs, int n, int norm_every, uint8_t* out) {
+  wacc26 a;
+  wacc_zero(a);
+  for (int k = 0; k < n; k++) {
+    wacc_mac(a, to_limbs26(ld(xs + 16 * k)), to_limbs26(ld(cs + 16 * k)));
+    if (norm_every > 0 && (k + 1) % norm_every == 0) wacc_normalize(a);
+  }
+  st(out, wacc_reduce(a));
+}
 // op: 0 add, 1 sub, 2 mul
 uint64_t ht_f64(int op, uint64_t a, uint64_t b) {
   switch (op) {

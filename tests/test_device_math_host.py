@@ -27,6 +27,7 @@ def ht():
     vp = ctypes.c_void_p
     L.ht_f128.argtypes = [ctypes.c_int, vp, vp, vp]
     L.ht_reduce192.argtypes = [vp, vp]
+    L.ht_wide_dot.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp]
     L.ht_mont_lazy.argtypes = [vp, vp, vp]
     L.ht_f64.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
     L.ht_f64.restype = ctypes.c_uint64
@@ -131,3 +132,22 @@ def test_xof_block_builder(ht, usage, binder):
         blk = bytearray(msg) + b"\x01" + bytes(168 - len(msg) - 1)
         blk[-1] ^= 0x80
         assert b"".join(x.to_bytes(4, "little") for x in w) == bytes(blk)
+
+
+@pytest.mark.parametrize("n,norm", [(1, 0), (91, 0), (700, 0), (2000, 512), (5000, 512)])
+def test_wide_dot_accumulator(ht, n, norm):
+    """The FLP wire sums: sum x_k c_k mod p with 26-bit limbs and deferred reduction,
+    including worst-case operands (p - 1) at the term counts the kernel allows."""
+    rnd = random.Random(n)
+    for trial in range(3):
+        if trial == 0:
+            xs = [P128 - 1] * n
+            cs = [P128 - 1] * n
+        else:
+            xs = [rnd.randrange(P128) for _ in range(n)]
+            cs = [rnd.choice([rnd.randrange(P128), P128 - 1, 2**128 - 2**100]) % P128 for _ in range(n)]
+        xb = b"".join(x.to_bytes(16, "little") for x in xs)
+        cb = b"".join(c.to_bytes(16, "little") for c in cs)
+        out = ctypes.create_string_buffer(16)
+        ht.ht_wide_dot(xb, cb, n, norm, out)
+        assert int.from_bytes(out.raw, "little") == sum(x * c for x, c in zip(xs, cs)) % P128

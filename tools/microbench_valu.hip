@@ -15,9 +15,14 @@
     }                                                                           \
   } while (0)
 
-enum { OP_XOR, OP_BITOP3, OP_ALIGNBIT, OP_MAD64, OP_MULLO, OP_MULHI, OP_ADD64, OP_MAD24, OP_FMA64, NOPS };
-static const char* NAMES[NOPS] = {"v_xor_b32",    "v_bitop3_b32", "v_alignbit_b32", "v_mad_u64_u32", "v_mul_lo_u32",
-                                  "v_mul_hi_u32", "add_u64",      "v_mad_u32_u24",  "v_fma_f64"};
+enum {
+  OP_XOR, OP_BITOP3, OP_ALIGNBIT, OP_MAD64, OP_MULLO, OP_MULHI, OP_ADD64, OP_MAD24, OP_FMA64,
+  OP_XOR3, OP_ROT, OP_PERM, OP_LSHLOR, OP_ADD3, OP_ADDCO, NOPS
+};
+static const char* NAMES[NOPS] = {"v_xor_b32",      "v_bitop3_b32(a^~b&c)", "v_alignbit_b32", "v_mad_u64_u32",
+                                  "v_mul_lo_u32",   "v_mul_hi_u32+xor",     "add_u64",        "v_mad_u32_u24",
+                                  "v_fma_f64",      "v_bitop3_b32(xor3)",   "v_alignbit(rot)", "v_perm_b32",
+                                  "v_lshl_or_b32",  "v_add3_u32",           "v_add_co+addc"};
 
 template <int OP>
 __global__ __launch_bounds__(256) void bench(uint32_t* out, int iters, uint32_t k) {
@@ -57,9 +62,34 @@ __global__ __launch_bounds__(256) void bench(uint32_t* out, int iters, uint32_t 
       } else if constexpr (OP == OP_MAD24) {
 #pragma unroll
         for (int j = 0; j < 8; j++) x[j] = (x[j] & 0xffffffu) * (x[(j + 1) & 7] & 0xffffffu) + x[j];
-      } else {
+      } else if constexpr (OP == OP_FMA64) {
 #pragma unroll
         for (int j = 0; j < 8; j++) d[j] = __builtin_fma(d[j], d[(j + 1) & 7], d[j]);
+      } else if constexpr (OP == OP_XOR3) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = __builtin_amdgcn_bitop3_b32(x[j], x[(j + 1) & 7], x[(j + 2) & 7], 0x96);
+      } else if constexpr (OP == OP_ROT) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = __builtin_amdgcn_alignbit(x[(j + 1) & 7], x[(j + 1) & 7], k + j);
+      } else if constexpr (OP == OP_PERM) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = __builtin_amdgcn_perm(x[j], x[(j + 1) & 7], 0x05040302u);
+      } else if constexpr (OP == OP_LSHLOR) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = (x[j] << (k & 31)) | x[(j + 1) & 7];
+      } else if constexpr (OP == OP_ADD3) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = x[j] + x[(j + 1) & 7] + x[(j + 2) & 7];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          uint32_t lo = (uint32_t)y[j], hi = (uint32_t)(y[j] >> 32);
+          uint32_t blo = (uint32_t)y[(j + 1) & 7], bhi = (uint32_t)(y[(j + 1) & 7] >> 32);
+          uint32_t c;
+          lo = __builtin_addc(lo, blo, 0u, &c);
+          hi = __builtin_addc(hi, bhi, c, &c);
+          y[j] = ((uint64_t)hi << 32) | lo;
+        }
       }
     }
   }
@@ -102,6 +132,12 @@ int main(int argc, char** argv) {
   run<OP_ADD64>(blocks, iters, d);
   run<OP_MAD24>(blocks, iters, d);
   run<OP_FMA64>(blocks, iters, d);
+  run<OP_XOR3>(blocks, iters, d);
+  run<OP_ROT>(blocks, iters, d);
+  run<OP_PERM>(blocks, iters, d);
+  run<OP_LSHLOR>(blocks, iters, d);
+  run<OP_ADD3>(blocks, iters, d);
+  run<OP_ADDCO>(blocks, iters, d);
   CHK(hipFree(d));
   return 0;
 }
