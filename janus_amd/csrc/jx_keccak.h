@@ -4,8 +4,8 @@
 // drives (Cargo.lock:2537,4252). The 1600-bit state lives in
 // 50 VGPRs as (lo, hi) 32-bit halves of the 25 lanes; 64-bit rotations are two
 // v_alignbit_b32, theta's 5-way XOR and chi's a^(~b&c) lower to v_bitop3_b32 on
-// gfx950. Fully unrolled: every state index is a compile-time constant, so nothing
-// spills to scratch.
+// gfx950. Rounds are fully unrolled inside: every state index is a compile-time
+// constant, so nothing spills to scratch.
 #pragma once
 #include "jx_field.h"
 
@@ -89,40 +89,63 @@ JX_HD void rho_pi_all(const uint32_t* A, uint32_t* B, IndexSeq<Is...>) {
   (rho_pi_one<Is>(A, B), ...);
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+JX_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+#else
+JX_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return a ^ b ^ c; }
+#endif
+
+// One round of Keccak-f[1600] on a state of 25 (lo, hi) lanes: theta's 5-way column parity
+// is two 3-input XORs (v_bitop3_b32 0x96) per word, rho is two v_alignbit_b32 per lane,
+// chi's a ^ (~b & c) is one v_bitop3_b32 per word: 190 VALU instructions.
+JX_HD void keccak_round(uint32_t* s, uint32_t rc_lo, uint32_t rc_hi) {
+  uint32_t C[10], B[50];
+#pragma unroll
+  for (int x = 0; x < 5; x++) {
+    C[2 * x] = xor3(xor3(s[2 * x], s[2 * (x + 5)], s[2 * (x + 10)]), s[2 * (x + 15)], s[2 * (x + 20)]);
+    C[2 * x + 1] =
+        xor3(xor3(s[2 * x + 1], s[2 * (x + 5) + 1], s[2 * (x + 10) + 1]), s[2 * (x + 15) + 1], s[2 * (x + 20) + 1]);
+  }
+#pragma unroll
+  for (int x = 0; x < 5; x++) {
+    uint32_t lo = C[2 * ((x + 1) % 5)], hi = C[2 * ((x + 1) % 5) + 1];
+    rotl64<1>(lo, hi);
+    uint32_t dlo = C[2 * ((x + 4) % 5)] ^ lo, dhi = C[2 * ((x + 4) % 5) + 1] ^ hi;
+#pragma unroll
+    for (int y = 0; y < 5; y++) {
+      s[2 * (x + 5 * y)] ^= dlo;
+      s[2 * (x + 5 * y) + 1] ^= dhi;
+    }
+  }
+  rho_pi_all(s, B, typename MakeSeq<25>::type{});
+#pragma unroll
+  for (int y = 0; y < 5; y++) {
+#pragma unroll
+    for (int x = 0; x < 5; x++) {
+      int i = x + 5 * y, i1 = (x + 1) % 5 + 5 * y, i2 = (x + 2) % 5 + 5 * y;
+      s[2 * i] = B[2 * i] ^ (~B[2 * i1] & B[2 * i2]);
+      s[2 * i + 1] = B[2 * i + 1] ^ (~B[2 * i1 + 1] & B[2 * i2 + 1]);
+    }
+  }
+  s[0] ^= rc_lo;
+  s[1] ^= rc_hi;
+}
+
 // Keccak-p[1600, 12]: rounds 12..23 of Keccak-f[1600]. s[2i] = lo, s[2i+1] = hi of lane i.
 JX_HD void keccak_p12(uint32_t* s) {
 #pragma unroll 1
+  for (int ir = 12; ir < 24; ir++) keccak_round(s, KECCAK_RC_LO[ir], KECCAK_RC_HI[ir]);
+}
+
+// Two independent Keccak-p[1600, 12] permutations advanced round by round in one loop:
+// two independent instruction streams for the scheduler (the measurement-share squeeze and
+// the joint-randomness-part absorb of K1).
+JX_HD void keccak_p12_x2(uint32_t* a, uint32_t* b) {
+#pragma unroll 1
   for (int ir = 12; ir < 24; ir++) {
-    uint32_t C[10], B[50];
-#pragma unroll
-    for (int x = 0; x < 5; x++) {
-      C[2 * x] = s[2 * x] ^ s[2 * (x + 5)] ^ s[2 * (x + 10)] ^ s[2 * (x + 15)] ^ s[2 * (x + 20)];
-      C[2 * x + 1] =
-          s[2 * x + 1] ^ s[2 * (x + 5) + 1] ^ s[2 * (x + 10) + 1] ^ s[2 * (x + 15) + 1] ^ s[2 * (x + 20) + 1];
-    }
-#pragma unroll
-    for (int x = 0; x < 5; x++) {
-      uint32_t lo = C[2 * ((x + 1) % 5)], hi = C[2 * ((x + 1) % 5) + 1];
-      rotl64<1>(lo, hi);
-      uint32_t dlo = C[2 * ((x + 4) % 5)] ^ lo, dhi = C[2 * ((x + 4) % 5) + 1] ^ hi;
-#pragma unroll
-      for (int y = 0; y < 5; y++) {
-        s[2 * (x + 5 * y)] ^= dlo;
-        s[2 * (x + 5 * y) + 1] ^= dhi;
-      }
-    }
-    rho_pi_all(s, B, typename MakeSeq<25>::type{});
-#pragma unroll
-    for (int y = 0; y < 5; y++) {
-#pragma unroll
-      for (int x = 0; x < 5; x++) {
-        int i = x + 5 * y, i1 = (x + 1) % 5 + 5 * y, i2 = (x + 2) % 5 + 5 * y;
-        s[2 * i] = B[2 * i] ^ (~B[2 * i1] & B[2 * i2]);
-        s[2 * i + 1] = B[2 * i + 1] ^ (~B[2 * i1 + 1] & B[2 * i2 + 1]);
-      }
-    }
-    s[0] ^= KECCAK_RC_LO[ir];
-    s[1] ^= KECCAK_RC_HI[ir];
+    const uint32_t lo = KECCAK_RC_LO[ir], hi = KECCAK_RC_HI[ir];
+    keccak_round(a, lo, hi);
+    keccak_round(b, lo, hi);
   }
 }
 

@@ -409,19 +409,20 @@ __global__ __launch_bounds__(256) void xof_kernel(Cfg c, Bufs b) {
   const uint64_t r0 = blk * 64 + lane;
   const uint64_t r = r0 < b.n ? r0 : b.n - 1;
 
-  uint32_t nonce[4], kmeas[4], kproof[4], kblind[4];
-  load16(b.nonces + 16 * r, nonce);
   const uint8_t* hs = b.his + (uint64_t)c.his_bytes * r;
-  load16(hs, kmeas);
-  load16(hs + 16, kproof);
-  load16(hs + 32, kblind);
   uint32_t flags = 0;
 
   // ---- measurement share fused with the joint_rand_part absorb --------------------
   // S: XOF(k_meas, DST(1), [1])            (squeezing, 168 bytes per block)
   // J: XOF(k_blind, DST(7), [1] || nonce || enc(meas_share))   (absorbing those bytes)
+  // J's message block m is meas bytes [168m - 42, 168m + 126): the 42-byte header makes it a
+  // 16-bit funnel shift (v_alignbit_b32) of squeezed words of blocks m-1 and m. After block m
+  // is consumed, S (-> block m+1) and J (absorb block m) permute together: two independent
+  // streams (keccak_p12_x2).
   uint32_t S[50], J[50];
   {
+    uint32_t kmeas[4];
+    load16(hs, kmeas);
     Block m;
     blk_zero(m);
     int pos = blk_xof_prefix(m, c.algo, 1, kmeas);
@@ -431,6 +432,9 @@ __global__ __launch_bounds__(256) void xof_kernel(Cfg c, Bufs b) {
   }
   uint32_t hdr[11];
   {
+    uint32_t nonce[4], kblind[4];
+    load16(b.nonces + 16 * r, nonce);
+    load16(hs + 32, kblind);
     Block h;
     blk_zero(h);
     int pos = blk_xof_prefix(h, c.algo, 7, kblind);
@@ -440,47 +444,66 @@ __global__ __launch_bounds__(256) void xof_kernel(Cfg c, Bufs b) {
 #pragma unroll
     for (int w = 0; w < 11; w++) hdr[w] = h.w[w];  // 42 header bytes
   }
-#pragma unroll
-  for (int w = 0; w < 50; w++) J[w] = 0;
   const uint32_t MB = c.meas_len * 16;
   const uint32_t ML = 42 + MB;
-  const uint32_t NM = (MB + 167) / 168;
-  const uint32_t b_last = ML / 168;
+  const uint32_t NM = (MB + 167) / 168;  // squeezed blocks
+  const uint32_t b_last = ML / 168;      // last absorbed block (b_last <= NM)
   uint32_t prev[11];
-#pragma unroll
-  for (int w = 0; w < 11; w++) prev[w] = 0;
   uint32_t carry0 = 0, carry1 = 0;
   Trunc tr;
   acc_zero(tr.a);
   tr.j = 0;
   tr.i = 0;
-  for (uint32_t m = 0; m <= b_last; m++) {
-    const bool have = m < NM;
-    if (have) {
-      if (m > 0) keccak_p12(S);
-      const uint32_t e0 = 21 * (m >> 1);
-      if ((m & 1) == 0) {
+  // emit the measurement elements of squeezed block m (10 or 11, by parity)
+  auto emit_block = [&](uint32_t m) {
+    const uint32_t e0 = 21 * (m >> 1);
+    if ((m & 1) == 0) {
 #pragma unroll
-        for (int ci = 0; ci < 10; ci++)
-          emit_meas(c, b, blk, lane, e0 + ci, w4_to_f(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]), flags,
-                    tr);
-        carry0 = S[40];
-        carry1 = S[41];
-      } else {
-        emit_meas(c, b, blk, lane, e0 + 10, w4_to_f(carry0, carry1, S[0], S[1]), flags, tr);
+      for (int ci = 0; ci < 10; ci++)
+        emit_meas(c, b, blk, lane, e0 + ci, w4_to_f(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]), flags, tr);
+      carry0 = S[40];
+      carry1 = S[41];
+    } else {
+      emit_meas(c, b, blk, lane, e0 + 10, w4_to_f(carry0, carry1, S[0], S[1]), flags, tr);
 #pragma unroll
-        for (int ci = 0; ci < 10; ci++)
-          emit_meas(c, b, blk, lane, e0 + 11 + ci,
-                    w4_to_f(S[2 + 4 * ci], S[3 + 4 * ci], S[4 + 4 * ci], S[5 + 4 * ci]), flags, tr);
-      }
+      for (int ci = 0; ci < 10; ci++)
+        emit_meas(c, b, blk, lane, e0 + 11 + ci, w4_to_f(S[2 + 4 * ci], S[3 + 4 * ci], S[4 + 4 * ci], S[5 + 4 * ci]),
+                  flags, tr);
     }
-    // J block m: message bytes [168m, 168m + 168) = meas bytes [168m - 42, 168m + 126)
+  };
+  // J ^= message block m built from S (block m, if squeezed) and prev (block m-1)
+  auto absorb_block = [&](uint32_t m, bool have) {
+    const uint32_t s0 = have ? S[0] : 0u;
+    if (m == 0) {
+#pragma unroll
+      for (int w = 0; w < 10; w++) J[w] = hdr[w];
+      J[10] = (hdr[10] & 0xffffu) | (s0 << 16);
+#pragma unroll
+      for (int w = 11; w < 50; w++) J[w] = 0;
+    } else {
+#pragma unroll
+      for (int w = 0; w < 10; w++) J[w] ^= alignbit(prev[w + 1], prev[w], 16);
+      J[10] ^= alignbit(s0, prev[10], 16);
+    }
+    if (have) {
+#pragma unroll
+      for (int w = 11; w < 42; w++) J[w] ^= alignbit(S[w - 10], S[w - 11], 16);
+#pragma unroll
+      for (int w = 0; w < 11; w++) prev[w] = S[31 + w];
+    }
+  };
+  // last absorbed block m: only message bytes [168m, ML) are absorbed, then TurboSHAKE padding
+  // (D = 0x01 after the message, 0x80 in byte 167)
+  auto absorb_last = [&](uint32_t m, bool have) {
+    const uint32_t nb = ML - 168 * m;  // message bytes in this block (< 168)
     uint32_t jw[42];
     const uint32_t s0 = have ? S[0] : 0u;
     if (m == 0) {
 #pragma unroll
       for (int w = 0; w < 10; w++) jw[w] = hdr[w];
       jw[10] = (hdr[10] & 0xffffu) | (s0 << 16);
+#pragma unroll
+      for (int w = 0; w < 50; w++) J[w] = 0;
     } else {
 #pragma unroll
       for (int w = 0; w < 10; w++) jw[w] = alignbit(prev[w + 1], prev[w], 16);
@@ -488,31 +511,50 @@ __global__ __launch_bounds__(256) void xof_kernel(Cfg c, Bufs b) {
     }
 #pragma unroll
     for (int w = 11; w < 42; w++) jw[w] = have ? alignbit(S[w - 10], S[w - 11], 16) : 0u;
-    if (m == b_last) {
-      const uint32_t nb = ML - 168 * m;  // message bytes in this block (< 168)
 #pragma unroll
-      for (int w = 0; w < 42; w++) {
-        const uint32_t lo_b = 4 * w;
-        if (lo_b >= nb)
-          jw[w] = 0;
-        else if (lo_b + 4 > nb)
-          jw[w] &= (1u << (8 * (nb - lo_b))) - 1u;
-        if ((uint32_t)w == (nb >> 2)) jw[w] ^= 1u << (8 * (nb & 3));  // TurboSHAKE D = 0x01
-      }
-      jw[41] ^= 0x80000000u;
+    for (int w = 0; w < 42; w++) {
+      const uint32_t lo_b = 4 * w;
+      if (lo_b >= nb)
+        jw[w] = 0;
+      else if (lo_b + 4 > nb)
+        jw[w] &= (1u << (8 * (nb - lo_b))) - 1u;
+      if ((uint32_t)w == (nb >> 2)) jw[w] ^= 1u << (8 * (nb & 3));
     }
+    jw[41] ^= 0x80000000u;
 #pragma unroll
     for (int w = 0; w < 42; w++) J[w] ^= jw[w];
     keccak_p12(J);
-    if (have) {
-#pragma unroll
-      for (int w = 0; w < 11; w++) prev[w] = S[31 + w];
+  };
+  // blocks m = 0 .. b_last (b_last <= NM); squeezed blocks m < NM. Block 0 is peeled so
+  // that the 42-byte header is dead inside the main loop.
+  emit_block(0);
+  if (b_last == 0) {
+    absorb_last(0, true);
+  } else {
+    absorb_block(0, true);
+    if (1 < NM)
+      keccak_p12_x2(S, J);
+    else
+      keccak_p12(J);
+#pragma unroll 1
+    for (uint32_t m = 1; m < b_last; m++) {  // m < b_last <= NM: block m was squeezed
+      emit_block(m);
+      absorb_block(m, true);
+      if (m + 1 < NM)
+        keccak_p12_x2(S, J);
+      else
+        keccak_p12(J);
     }
+    const bool have = b_last < NM;
+    if (have) emit_block(b_last);
+    absorb_last(b_last, have);
   }
   uint32_t part_h[4] = {J[0], J[1], J[2], J[3]};
 
   // ---- proof share: XOF(k_proofs, DST(2), [PROOFS=1, agg_id=1]) -------------------
   {
+    uint32_t kproof[4];
+    load16(hs + 16, kproof);
     Block m;
     blk_zero(m);
     int pos = blk_xof_prefix(m, c.algo, 2, kproof);
@@ -540,9 +582,10 @@ __global__ __launch_bounds__(256) void xof_kernel(Cfg c, Bufs b) {
     }
   }
 
-  uint32_t part_l[4], lead_part[4];
+  uint32_t part_l[4], lead_part[4], nonce[4];
   load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
   load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
+  load16(b.nonces + 16 * r, nonce);
   flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, part_l, lead_part, part_h, flags, false);
   if (b.force_slow) flags |= FLAG_SLOW;
   if (r0 < b.n) b.flags[r0] = flags;
