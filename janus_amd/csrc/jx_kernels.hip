@@ -218,28 +218,55 @@ __device__ __forceinline__ void trunc_add(acc192& a, f128 x, uint32_t sh) {
   a.w2 = a.w2 + w2 + cc;
 }
 
+// Output-share truncation in the fast XOF kernel (SumVec / Sum):
+//   out_i = sum_{j<bits} 2^j x_{bits*i+j} mod p.
+// Word columns T_w = sum_j x_{j,w} 2^j (< 2^(32+bits) <= 2^64) cost one v_mad_u64_u32 per 32-bit
+// word of each element; the <= 160-bit total is reduced once per output element.
+struct TruncW {
+  uint64_t T[4];
+  uint32_t j, i;
+};
+__device__ __forceinline__ void truncw_zero(TruncW& t) {
+#pragma unroll
+  for (int w = 0; w < 4; w++) t.T[w] = 0;
+}
+__device__ __forceinline__ f128 truncw_value(const TruncW& t) {
+  // V = T0 + T1 2^32 + T2 2^64 + T3 2^96
+  uint32_t c = 0;
+  const uint64_t w0 = addc64(t.T[0], t.T[1] << 32, c);
+  const uint64_t w1 = addc64(t.T[2], (t.T[1] >> 32) | (t.T[3] << 32), c);
+  const uint64_t w2 = (t.T[3] >> 32) + c;
+  return reduce192(w0, w1, w2);
+}
+// Conservative ">= p" screen for a sampled Field128 element: true for every x >= p (and for
+// the 2^-59-probable x in [2^128 - 2^69, p), which the slow kernel then redoes exactly).
+// Tracked as a running max so that one compare per block decides.
+__device__ __forceinline__ uint32_t ge_screen(uint4 v) { return v.w & (v.z | 0x1Fu); }
+
 // one measurement element at static stream position e (fast path: no rejections)
-__device__ __forceinline__ void emit_meas(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t lane, uint32_t e,
-                                          f128 x, uint32_t& flags, Trunc& tr) {
+__device__ __forceinline__ void emit_meas(const Cfg& c, uint4* mp, uint4* op, uint32_t e, uint4 v, uint32_t& gmax,
+                                          TruncW& tr) {
   if (e >= c.meas_len) return;
-  if (ge_p128(x)) flags |= FLAG_SLOW;
-  st_il(b.meas, blk, c.meas_len, e, lane, x);
+  gmax = max(gmax, ge_screen(v));
+  mp[(uint64_t)e * IL] = v;
   if (!c.out_is_meas) {
-    trunc_add(tr.a, x, tr.j);
-    tr.j++;
-    if (tr.j == c.bits) {
-      st_il(b.outs, blk, c.out_len, tr.i, lane, acc_reduce(tr.a));
-      acc_zero(tr.a);
+    const uint32_t sh = 1u << tr.j;
+    tr.T[0] += (uint64_t)v.x * sh;
+    tr.T[1] += (uint64_t)v.y * sh;
+    tr.T[2] += (uint64_t)v.z * sh;
+    tr.T[3] += (uint64_t)v.w * sh;
+    if (++tr.j == c.bits) {
+      op[(uint64_t)tr.i * IL] = f_to_u4(truncw_value(tr));
+      truncw_zero(tr);
       tr.j = 0;
       tr.i++;
     }
   }
 }
-__device__ __forceinline__ void emit_proof(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t lane, uint32_t e,
-                                           f128 x, uint32_t& flags) {
+__device__ __forceinline__ void emit_proof(const Cfg& c, uint4* pp, uint32_t e, uint4 v, uint32_t& gmax) {
   if (e >= c.proof_len) return;
-  if (ge_p128(x)) flags |= FLAG_SLOW;
-  st_il(b.proof, blk, c.proof_len, e, lane, x);
+  gmax = max(gmax, ge_screen(v));
+  pp[(uint64_t)e * IL] = v;
 }
 
 // slot of c_k (k = 0..calls) in the coefficient table
@@ -450,25 +477,28 @@ __global__ __launch_bounds__(256) void xof_kernel(Cfg c, Bufs b) {
   const uint32_t b_last = ML / 168;      // last absorbed block (b_last <= NM)
   uint32_t prev[11];
   uint32_t carry0 = 0, carry1 = 0;
-  Trunc tr;
-  acc_zero(tr.a);
+  uint32_t gmax = 0;  // running ge_screen over every sampled element
+  TruncW tr;
+  truncw_zero(tr);
   tr.j = 0;
   tr.i = 0;
+  uint4* const mp = b.meas + il_idx(blk, c.meas_len, 0, lane);
+  uint4* const op = b.outs + il_idx(blk, c.out_len, 0, lane);
   // emit the measurement elements of squeezed block m (10 or 11, by parity)
   auto emit_block = [&](uint32_t m) {
     const uint32_t e0 = 21 * (m >> 1);
     if ((m & 1) == 0) {
 #pragma unroll
       for (int ci = 0; ci < 10; ci++)
-        emit_meas(c, b, blk, lane, e0 + ci, w4_to_f(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]), flags, tr);
+        emit_meas(c, mp, op, e0 + ci, make_uint4(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]), gmax, tr);
       carry0 = S[40];
       carry1 = S[41];
     } else {
-      emit_meas(c, b, blk, lane, e0 + 10, w4_to_f(carry0, carry1, S[0], S[1]), flags, tr);
+      emit_meas(c, mp, op, e0 + 10, make_uint4(carry0, carry1, S[0], S[1]), gmax, tr);
 #pragma unroll
       for (int ci = 0; ci < 10; ci++)
-        emit_meas(c, b, blk, lane, e0 + 11 + ci, w4_to_f(S[2 + 4 * ci], S[3 + 4 * ci], S[4 + 4 * ci], S[5 + 4 * ci]),
-                  flags, tr);
+        emit_meas(c, mp, op, e0 + 11 + ci, make_uint4(S[2 + 4 * ci], S[3 + 4 * ci], S[4 + 4 * ci], S[5 + 4 * ci]),
+                  gmax, tr);
     }
   };
   // J ^= message block m built from S (block m, if squeezed) and prev (block m-1)
@@ -564,23 +594,25 @@ __global__ __launch_bounds__(256) void xof_kernel(Cfg c, Bufs b) {
     sponge_oneblock(S, m);
   }
   const uint32_t NP = (c.proof_len * 16 + 167) / 168;
+  uint4* const pp = b.proof + il_idx(blk, c.proof_len, 0, lane);
+#pragma unroll 1
   for (uint32_t m = 0; m < NP; m++) {
     if (m > 0) keccak_p12(S);
     const uint32_t e0 = 21 * (m >> 1);
     if ((m & 1) == 0) {
 #pragma unroll
       for (int ci = 0; ci < 10; ci++)
-        emit_proof(c, b, blk, lane, e0 + ci, w4_to_f(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]), flags);
+        emit_proof(c, pp, e0 + ci, make_uint4(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]), gmax);
       carry0 = S[40];
       carry1 = S[41];
     } else {
-      emit_proof(c, b, blk, lane, e0 + 10, w4_to_f(carry0, carry1, S[0], S[1]), flags);
+      emit_proof(c, pp, e0 + 10, make_uint4(carry0, carry1, S[0], S[1]), gmax);
 #pragma unroll
       for (int ci = 0; ci < 10; ci++)
-        emit_proof(c, b, blk, lane, e0 + 11 + ci,
-                   w4_to_f(S[2 + 4 * ci], S[3 + 4 * ci], S[4 + 4 * ci], S[5 + 4 * ci]), flags);
+        emit_proof(c, pp, e0 + 11 + ci, make_uint4(S[2 + 4 * ci], S[3 + 4 * ci], S[4 + 4 * ci], S[5 + 4 * ci]), gmax);
     }
   }
+  if (gmax == 0xFFFFFFFFu) flags |= FLAG_SLOW;
 
   uint32_t part_l[4], lead_part[4], nonce[4];
   load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
