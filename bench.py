@@ -32,11 +32,15 @@ sys.path.insert(0, ROOT)
 METRIC = "helper reports/sec (prep_init+aggregate), Prio3SumVec len=1000 @1/2/4/8 GPU"
 P128 = 2**128 - 28 * 2**64 + 1
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz = 78.6 int32 Top/s
-# Algorithmic int32 VALU work: one Keccak-p[1600,12] permutation = 190 ops/round
-# x 12 rounds with v_bitop3/v_alignbit (theta 90, rho 48, chi 50, iota 2); one Field128 Montgomery
-# product = 16 v_mad_u64_u32 + 40 add/carry/select ops (~56 issue slots).
+HBM_PEAK_GBPS = 8000.0
+# Algorithmic int32 VALU work: one Keccak-p[1600,12] permutation = 190 instructions/round
+# x 12 rounds on gfx950 (theta 20 v_bitop3 + 10 v_alignbit + 60 xor, rho 48 v_alignbit, chi 50 v_bitop3,
+# iota 2); one Field128 Montgomery product (K1 coefficients / inversion) = 56; one Field128 product in the
+# FLP wire sums (K3, 2 per measurement element) = 16 32x32->64 partial products.
 OPS_PER_PERM = 190 * 12
 OPS_PER_MONT = 56
+OPS_PER_FMUL = 16
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v3_pmc_summary.json")
 
 
 def log(*a):
@@ -61,12 +65,27 @@ def sumvec_work(bits, length, chunk):
     perms = perms_meas + perms_part + perms_proof + perms_tail
     # K1 tail: t^P, L, batch inversion (3 per call) + ~143 for the inversion chain, d_k
     mont_k1 = 6 + 3 * (calls + 1) + 143 + 2 * calls + 8
-    # K3: two lazy products per measurement element, wire finish 4 per wire pair, v and G(t) 2 per coeff
-    mont_k3 = 2 * M + 5 * chunk + 2 * (2 * P - 1) + 20
-    return dict(perms=perms, mont_k1=mont_k1, mont_k3=mont_k3,
-                ops_k1=perms * OPS_PER_PERM + mont_k1 * OPS_PER_MONT, ops_k3=mont_k3 * OPS_PER_MONT,
+    # K3: two products per measurement element (wire sums), wire finish ~8 per slot, v and G(t) 2 per coeff
+    fmul_k3 = 2 * M
+    mont_k3 = 8 * chunk + 2 * (2 * P - 1) + 20
+    return dict(perms=perms, mont_k1=mont_k1, fmul_k3=fmul_k3, mont_k3=mont_k3,
+                ops_k1=perms * OPS_PER_PERM + mont_k1 * OPS_PER_MONT,
+                ops_k3=fmul_k3 * OPS_PER_FMUL + mont_k3 * OPS_PER_MONT,
                 hbm_k1=16 * (M + proof_len + 6 + 2 * calls) + 16 * length + 16 + 48 + 32 + 16,
                 hbm_k3=16 * (M + proof_len + 6 + 2 * calls) + 16 * (A + 3) + 1)
+
+
+def pmc_traffic(kernel: str, reports_per_launch: float):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (separate
+    FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction), scaled to this
+    run's reports per launch. None if the summary or kernel is missing."""
+    try:
+        d = json.load(open(PMC_SUMMARY))
+        e = d["kernels"][kernel]
+        per_report = (e["hbm_read_bytes"] + e["hbm_write_bytes"]) / d["workload"]["reports_per_launch"]
+        return int(per_report * reports_per_launch), os.path.relpath(PMC_SUMMARY, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def make_pool(vdaf, vk, K, seed=0x5EED, threads=16):
@@ -214,8 +233,10 @@ def main():
     k3_ms = kt["flp"]["ms"] / max(1, kt["flp"]["launches"])
     k1_tops = work["ops_k1"] * chunk_reports / (k1_ms * 1e-3) / 1e12
     k3_tops = work["ops_k3"] * chunk_reports / (k3_ms * 1e-3) / 1e12
-    dominant = "K1 xof_kernel" if kt["xof"]["ms"] >= kt["flp"]["ms"] else "K3 flp_psum_kernel"
+    dominant = "K1 xof_kernel" if kt["xof"]["ms"] >= kt["flp"]["ms"] else "K3 flp_psum_part_kernel"
     ach = k1_tops if dominant.startswith("K1") else k3_tops
+    traffic, traffic_src = pmc_traffic("jx::xof_kernel" if dominant.startswith("K1") else
+                                       "jx::flp_psum_part_kernel<2, false>", chunk_reports)
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -235,8 +256,13 @@ def main():
                    "reports_per_gpu": R, "global_reports_per_step": R * world,
                    "parallelism": f"report-sharded x{world} (RCCL all-gather + device mod-p combine)"},
         "roofline": {"bound": "valu", "kernel": dominant, "achieved": round(ach, 3), "peak": round(VALU_PEAK_TOPS, 2),
-                     "unit": "TOP/s (int32 VALU ops, algorithmic model)", "frac": round(ach / VALU_PEAK_TOPS, 4),
-                     "traffic": None},
+                     "unit": "TOP/s (int32 VALU instructions/s, algorithmic count: DESIGN.md §5)",
+                     "frac": round(ach / VALU_PEAK_TOPS, 4),
+                     "traffic": traffic, "traffic_unit": "HBM bytes per launch (rocprofv3 2*FETCH_SIZE + WRITE_SIZE)",
+                     "traffic_source": traffic_src,
+                     "algorithmic_bytes": int(work["hbm_k1"] * chunk_reports),
+                     "hbm_GBps": round(work["hbm_k1"] * chunk_reports / (k1_ms * 1e-3) / 1e9, 1),
+                     "hbm_peak_GBps": HBM_PEAK_GBPS},
         "kernels": {"k1_xof_ms_per_launch": round(k1_ms, 3), "k3_flp_ms_per_launch": round(k3_ms, 3),
                     "k4_acc_ms_per_launch": round(kt["accumulate"]["ms"] / max(1, kt["accumulate"]["launches"]), 3),
                     "slow_ms_per_launch": round(kt["slow"]["ms"] / max(1, kt["slow"]["launches"]), 3),

@@ -323,6 +323,15 @@ static int32_t ensure_tmp(jx_engine* e, size_t bytes) {
   return JX_OK;
 }
 
+// Reports per launch for an n-report fused call: the fewest launches that fit the staging
+// budget (default_chunk), split evenly (multiple of 64) so every launch has the same shape.
+static uint64_t launch_chunk(const jx_engine* e, uint64_t n) {
+  if (n <= e->default_chunk) return n;
+  const uint64_t launches = (n + e->default_chunk - 1) / e->default_chunk;
+  const uint64_t per = (n + launches - 1) / launches;
+  return (per + 63) / 64 * 64;
+}
+
 // ---------------------------------------------------------------------------- timing
 
 static hipError_t stage_begin(jx_engine* e, hipEvent_t* ev) {
@@ -580,7 +589,7 @@ int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces
   const Cfg& c = e->cfg;
   if (c.ps_bytes && !public_shares) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
-  const uint64_t chunk = n < e->default_chunk ? n : e->default_chunk;
+  const uint64_t chunk = launch_chunk(e, n);
   int32_t rc = ensure_capacity(e, chunk);
   if (rc) return rc;
   for (uint64_t off = 0; off < n; off += chunk) {
@@ -614,7 +623,7 @@ int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_
   const Cfg& c = e->cfg;
   if (c.ps_bytes && !d_ps) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
-  const uint64_t chunk = n < e->default_chunk ? n : e->default_chunk;
+  const uint64_t chunk = launch_chunk(e, n);
   int32_t rc = ensure_capacity(e, chunk);
   if (rc) return rc;
   const uint8_t *N = (const uint8_t*)d_nonces, *PS = (const uint8_t*)d_ps, *H = (const uint8_t*)d_his,
