@@ -823,7 +823,7 @@ __global__ __launch_bounds__(256) void flp_sum_kernel(Cfg c, Bufs b) {
 // Phase 2 (flp_psum_final_kernel): one report per lane; adds the partials, the leader's
 // v and G(t), and decides.
 template <int PPW, bool HIST>
-__global__ __launch_bounds__(64) void flp_psum_part_kernel(Cfg c, Bufs b) {
+__global__ __launch_bounds__(64, 4) void flp_psum_part_kernel(Cfg c, Bufs b) {
   const uint32_t NG = c.ngroups;
   // Workgroup ids are dispatched round-robin over the 8 XCDs; map them so that the NG
   // groups of one block run back to back on one XCD and share its L2 (coefficients,
@@ -858,14 +858,24 @@ __global__ __launch_bounds__(64) void flp_psum_part_kernel(Cfg c, Bufs b) {
   if (j0 + PPW <= chunk && M >= j0 + PPW) kf = min(C, (M - j0 - PPW) / chunk + 1);
   for (uint32_t k0 = 1; k0 <= kf; k0 += 512) {  // <= 5 * 512 limb products (< 2^52) per column
     const uint32_t k1 = min(kf, k0 + 511);
+    // software pipeline: the loads of call k+1 are in flight while call k multiplies
+    uint4 cn = coefb[(COEF_K + 2 * (k0 - 1)) * IL], dn = coefb[(COEF_K + 2 * (k0 - 1) + 1) * IL];
+    uint4 xn[PPW];
+#pragma unroll
+    for (int i = 0; i < PPW; i++) xn[i] = measb[(uint64_t)((k0 - 1) * chunk + j0 + i) * IL];
 #pragma unroll 1
     for (uint32_t k = k0; k <= k1; k++) {
-      const limbs26 ck = to_limbs26(u4_to_f(coefb[(COEF_K + 2 * (k - 1)) * IL]));
-      const limbs26 dk = to_limbs26(u4_to_f(coefb[(COEF_K + 2 * (k - 1) + 1) * IL]));
-      const uint32_t nb = (k - 1) * chunk + j0;
+      const limbs26 ck = to_limbs26(u4_to_f(cn));
+      const limbs26 dk = to_limbs26(u4_to_f(dn));
       f128 x[PPW];
 #pragma unroll
-      for (int i = 0; i < PPW; i++) x[i] = u4_to_f(measb[(uint64_t)(nb + i) * IL]);
+      for (int i = 0; i < PPW; i++) x[i] = u4_to_f(xn[i]);
+      if (k < k1) {
+        cn = coefb[(COEF_K + 2 * k) * IL];
+        dn = coefb[(COEF_K + 2 * k + 1) * IL];
+#pragma unroll
+        for (int i = 0; i < PPW; i++) xn[i] = measb[(uint64_t)(k * chunk + j0 + i) * IL];
+      }
 #pragma unroll
       for (int i = 0; i < PPW; i++) {
         const limbs26 xl = to_limbs26(x[i]);
