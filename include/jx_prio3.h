@@ -91,7 +91,26 @@ int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, co
                              const uint8_t* helper_input_shares, const uint8_t* leader_prep_shares,
                              uint8_t* out_prep_msgs, uint8_t* out_verdicts, uint8_t* out_output_shares);
 
-/* Accumulate the output shares of the last jx_helper_prep_batch into batch aggregations:
+/* ---- Leader role: the leader side of the same ping-pong exchange.
+ * jx_leader_prep_init_batch replaces the per-report vdaf.leader_initialized(verify_key, agg_param,
+ * nonce = report id, public_share, leader_input_share) of step_aggregation_job_aggregate_init
+ * (aggregator/src/aggregator/aggregation_job_driver.rs:344-362): prepare_init with agg_id 0 on the
+ * explicit leader input share (meas share || proofs share || [k_blind], LIS bytes each, see
+ * jx_engine_leader_sizes). out_prep_shares[n x LPS] receives the prep_share that goes into
+ * PingPongMessage::Initialize; out_verdicts[n]: JX_FINISHED (0) = initialized, or
+ * JX_PREPARE_INIT_FAILURE (an input-share element >= p, or t a P-th root of unity). The prepare
+ * state (output share + corrected joint-rand seed) stays on the device.
+ * jx_leader_prep_finish_batch replaces leader_continued on the helper's Finish{prep_msg}
+ * (aggregation_job_driver.rs:588-602): prepare_next fails (JX_PREPARE_NEXT_FAILURE) unless prep_msg
+ * equals the corrected seed. prep_msgs: n x PM (PM = 0: nullable). out_output_shares nullable.
+ * After finish, jx_accumulate aggregates the leader's finished output shares. */
+int32_t jx_engine_leader_sizes(const jx_engine* e, uint32_t* leader_input_share);
+int32_t jx_leader_prep_init_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
+                                  const uint8_t* leader_input_shares, uint8_t* out_prep_shares, uint8_t* out_verdicts);
+int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t n, const uint8_t* prep_msgs, uint8_t* out_verdicts,
+                                    uint8_t* out_output_shares);
+
+/* Accumulate the output shares of the last prepared batch (helper, or leader after finish) into batch aggregations:
  * report i is added iff verdict == FINISHED and accept_mask[i] != 0 (accept_mask nullable = all),
  * into aggregation `segment[i]` (segment nullable = 0). Adds to the aggregate share, the
  * report count and the ReportIdChecksum (XOR of SHA-256(report id)). */

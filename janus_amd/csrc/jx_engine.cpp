@@ -53,6 +53,11 @@ struct jx_engine {
   size_t tmp_bytes = 0;
   uint8_t* d_mask = nullptr;
   uint32_t* d_seg = nullptr;
+  // leader role staging (allocated on first leader call): input shares, outbound prep
+  // shares, inbound prep messages; the corrected seeds (prepare state) live in d_msgs
+  uint8_t *d_lis = nullptr, *d_lps_out = nullptr, *d_in_msgs = nullptr;
+  uint64_t leader_cap = 0;
+  bool leader_batch = false;
   std::map<uint32_t, Segment> segs;
   uint64_t last_n = 0;
   bool have_batch = false;
@@ -199,6 +204,7 @@ static int32_t make_cfg(const jx_prio3_params* p, const uint8_t vk[16], Cfg& c, 
   c.ps_bytes = jr ? 32 : 0;
   c.his_bytes = jr ? 48 : 32;
   c.lps_bytes = c.ver_len * fb + (jr ? 16 : 0);
+  c.lis_bytes = (c.meas_len + c.proof_len) * fb + (jr ? 16 : 0);
   if (c.algo == ALGO_COUNT)
     c.ncoef = 0;
   else if (c.algo == ALGO_SUM)
@@ -261,6 +267,11 @@ static void free_staging(jx_engine* e) {
   e->d_seg = nullptr;
   e->cap = 0;
   e->have_batch = false;
+  for (uint8_t** p : {&e->d_lis, &e->d_lps_out, &e->d_in_msgs}) {
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+  }
+  e->leader_cap = 0;
 }
 
 static uint64_t per_report_bytes(const Cfg& c) {
@@ -368,14 +379,19 @@ static int32_t drain_timing(jx_engine* e) {
 
 // Prepare n <= cap reports whose inputs are at the given device pointers.
 static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* his,
-                         const uint8_t* lps, uint8_t* verdicts, uint8_t* msgs) {
+                         const uint8_t* lps, uint8_t* verdicts, uint8_t* msgs, const uint8_t* lis = nullptr,
+                         uint8_t* lps_out = nullptr) {
   const Cfg& c = e->cfg;
+  const bool leader = lis != nullptr;
   Bufs b{};
   b.n = n;
   b.nonces = nonces;
   b.ps = ps;
   b.his = his;
   b.lps = lps;
+  b.lis = lis;
+  b.lps_out = lps_out;
+  b.leader = leader ? 1u : 0u;
   b.meas = e->d_meas;
   b.proof = e->d_proof;
   b.outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? e->d_meas : e->d_outs;
@@ -395,14 +411,34 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
     HIPCHK(e, stage_begin(e, &ev));
     HIPCHK(e, launch_xof(c, b, e->stream));
     HIPCHK(e, stage_end(e, ST_XOF, ev));
-    HIPCHK(e, stage_begin(e, &ev));
-    HIPCHK(e, launch_xof_slow(c, b, e->stream));
-    HIPCHK(e, stage_end(e, ST_SLOW, ev));
+    if (!leader) {  // the leader's shares are explicit: no rejection-sampled streams to redo
+      HIPCHK(e, stage_begin(e, &ev));
+      HIPCHK(e, launch_xof_slow(c, b, e->stream));
+      HIPCHK(e, stage_end(e, ST_SLOW, ev));
+    }
     HIPCHK(e, stage_begin(e, &ev));
     HIPCHK(e, launch_flp(c, b, e->stream));
     HIPCHK(e, stage_end(e, ST_FLP, ev));
   }
   e->batch_nonces = nonces;
+  e->leader_batch = leader;
+  return JX_OK;
+}
+
+static int32_t ensure_leader_capacity(jx_engine* e, uint64_t n) {
+  int32_t rc = ensure_capacity(e, n);
+  if (rc) return rc;
+  if (n <= e->leader_cap && e->d_lis) return JX_OK;
+  for (uint8_t** p : {&e->d_lis, &e->d_lps_out, &e->d_in_msgs}) {
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+  }
+  const Cfg& c = e->cfg;
+  const uint64_t cap = e->cap;
+  HIPCHK(e, hipMalloc((void**)&e->d_lis, cap * c.lis_bytes));
+  HIPCHK(e, hipMalloc((void**)&e->d_lps_out, cap * c.lps_bytes));
+  HIPCHK(e, hipMalloc((void**)&e->d_in_msgs, cap * 16));
+  e->leader_cap = cap;
   return JX_OK;
 }
 
@@ -495,6 +531,9 @@ void jx_engine_destroy(jx_engine* e) {
   }
   if (e->d_consts) (void)hipFree(e->d_consts);
   if (e->d_tmp) (void)hipFree(e->d_tmp);
+  if (e->d_lis) (void)hipFree(e->d_lis);
+  if (e->d_lps_out) (void)hipFree(e->d_lps_out);
+  if (e->d_in_msgs) (void)hipFree(e->d_in_msgs);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -553,6 +592,70 @@ int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, co
   e->last_n = n;
   e->have_batch = true;
   return drain_timing(e);
+}
+
+int32_t jx_engine_leader_sizes(const jx_engine* e, uint32_t* leader_input_share) {
+  if (!e) return JX_E_INVALID;
+  if (leader_input_share) *leader_input_share = e->cfg.lis_bytes;
+  return JX_OK;
+}
+
+int32_t jx_leader_prep_init_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
+                                  const uint8_t* leader_input_shares, uint8_t* out_prep_shares,
+                                  uint8_t* out_verdicts) {
+  if (!e || !nonces || !leader_input_shares || !out_prep_shares || !out_verdicts) return JX_E_INVALID;
+  const Cfg& c = e->cfg;
+  if (c.ps_bytes && !public_shares) return JX_E_INVALID;
+  if (n == 0) {
+    e->have_batch = true;
+    e->leader_batch = true;
+    e->last_n = 0;
+    return JX_OK;
+  }
+  HIPCHK(e, hipSetDevice(e->device));
+  int32_t rc = ensure_leader_capacity(e, n);
+  if (rc) return rc;
+  HIPCHK(e, hipMemcpyAsync(e->d_nonces, nonces, n * 16, hipMemcpyHostToDevice, e->stream));
+  if (c.ps_bytes) HIPCHK(e, hipMemcpyAsync(e->d_ps, public_shares, n * c.ps_bytes, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipMemcpyAsync(e->d_lis, leader_input_shares, n * c.lis_bytes, hipMemcpyHostToDevice, e->stream));
+  rc = prep_core(e, n, e->d_nonces, e->d_ps, nullptr, nullptr, e->d_verdicts, e->d_msgs, e->d_lis, e->d_lps_out);
+  if (rc) return rc;
+  HIPCHK(e, hipMemcpyAsync(out_verdicts, e->d_verdicts, n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(out_prep_shares, e->d_lps_out, n * c.lps_bytes, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  e->last_n = n;
+  e->have_batch = true;
+  return drain_timing(e);
+}
+
+int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t n, const uint8_t* prep_msgs, uint8_t* out_verdicts,
+                                    uint8_t* out_output_shares) {
+  if (!e || !out_verdicts) return JX_E_INVALID;
+  const Cfg& c = e->cfg;
+  if (!e->have_batch || !e->leader_batch || n != e->last_n)
+    return fail(e, JX_E_STATE, "leader finish: no leader batch of this size was initialized");
+  if (c.jr_len && !prep_msgs) return JX_E_INVALID;
+  if (n == 0) return JX_OK;
+  HIPCHK(e, hipSetDevice(e->device));
+  if (c.jr_len) {
+    HIPCHK(e, hipMemcpyAsync(e->d_in_msgs, prep_msgs, n * 16, hipMemcpyHostToDevice, e->stream));
+    Bufs b{};
+    b.n = n;
+    b.verdicts = e->d_verdicts;
+    b.msgs = e->d_msgs;
+    HIPCHK(e, launch_leader_finish(c, b, e->d_in_msgs, e->stream));
+  }
+  HIPCHK(e, hipMemcpyAsync(out_verdicts, e->d_verdicts, n, hipMemcpyDeviceToHost, e->stream));
+  if (out_output_shares) {
+    const uint32_t fb = c.algo == ALGO_COUNT ? 8 : 16;
+    int32_t rc = ensure_tmp(e, n * c.out_len * fb);
+    if (rc) return rc;
+    const uint4* outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? e->d_meas : e->d_outs;
+    HIPCHK(e, launch_transpose_out(c, outs, n, e->d_tmp, e->stream));
+    HIPCHK(e, hipMemcpyAsync(out_output_shares, e->d_tmp, n * c.out_len * fb, hipMemcpyDeviceToHost, e->stream));
+  }
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return JX_OK;
 }
 
 int32_t jx_accumulate(jx_engine* e, uint64_t n, const uint8_t* accept_mask, const uint32_t* segment) {

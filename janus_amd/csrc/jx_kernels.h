@@ -14,6 +14,7 @@ enum : uint32_t {
   FLAG_NEXT_FAIL = 2u,  // leader's joint-rand part disagrees with the public share -> prepare_next_failure
   FLAG_SLOW = 4u,       // a rejected XOF sample shifted a stream: the slow kernel redoes this report
   FLAG_DFAIL = 8u,      // a leader verifier element is >= p -> leader_prep_share_decode_failure
+  FLAG_INPUT_FAIL = 16u,  // leader: an explicit input-share element is >= p -> prepare_init_failure
 };
 
 // Interleaved staging: element e of report r lives at [(r/64)][e][r%64] (16 bytes each),
@@ -24,6 +25,7 @@ struct Cfg {
   uint32_t algo, bits, length, chunk;
   uint32_t meas_len, out_len, jr_len, proof_len, ver_len, calls, P, logP, gpoly_len;
   uint32_t ps_bytes, his_bytes, lps_bytes;
+  uint32_t lis_bytes;    // leader input share: meas || proofs || [k_blind]
   uint32_t ncoef;        // coefficient slots per report
   uint32_t out_is_meas;  // truncate == identity (Histogram): output share aliases the meas staging
   uint32_t ppw, ngroups; // ParallelSum FLP: chunk slots per group, groups per 64-report block
@@ -49,6 +51,9 @@ struct Bufs {
   const uint8_t* ps;
   const uint8_t* his;
   const uint8_t* lps;
+  const uint8_t* lis;   // leader role: explicit leader input shares (n x lis_bytes)
+  uint8_t* lps_out;     // leader role: outbound prep shares (n x lps_bytes)
+  uint32_t leader;      // 1: run prepare_init for agg_id 0 (leader_initialized)
   uint4* meas;
   uint4* proof;
   uint4* outs;
@@ -81,6 +86,7 @@ struct AccArgs {
 hipError_t launch_count(const Cfg& c, const Bufs& b, hipStream_t s);
 hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s);
 hipError_t launch_xof_slow(const Cfg& c, const Bufs& b, hipStream_t s);
+hipError_t launch_leader_finish(const Cfg& c, const Bufs& b, const uint8_t* prep_msgs, hipStream_t s);
 hipError_t launch_flp(const Cfg& c, const Bufs& b, hipStream_t s);
 hipError_t launch_accumulate(const Cfg& c, const AccArgs& a, uint4* agg, hipStream_t s);
 hipError_t launch_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, hipStream_t s);

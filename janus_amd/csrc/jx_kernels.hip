@@ -121,6 +121,9 @@ __device__ void sample64(uint32_t* S, uint64_t out[N]) {
 
 // ---------------------------------------------------------------------------- K0: Prio3Count
 
+// LEADER: prepare_init with agg_id 0 on the explicit leader input share (meas || proofs, Field64);
+// writes the leader's verifier share [v, W0, W1, G] as its prep share.
+template <bool LEADER>
 __global__ __launch_bounds__(256) void count_kernel(Cfg c, Bufs b) {
   const uint64_t r0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t nblk = (b.n + 63) / 64;
@@ -130,9 +133,22 @@ __global__ __launch_bounds__(256) void count_kernel(Cfg c, Bufs b) {
   const uint32_t lane = r0 % 64;
   uint32_t nonce[4], kmeas[4], kproof[4], S[50];
   load16(b.nonces + 16 * r, nonce);
+  uint64_t x[1], proof[5], t[1];
+  bool bad = false;
+  if (LEADER) {
+    const uint2* ls = reinterpret_cast<const uint2*>(b.lis + (uint64_t)c.lis_bytes * r);
+    uint2 q = ls[0];
+    x[0] = (uint64_t)q.x | ((uint64_t)q.y << 32);
+    bad |= x[0] >= P64;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+      q = ls[1 + i];
+      proof[i] = (uint64_t)q.x | ((uint64_t)q.y << 32);
+      bad |= proof[i] >= P64;
+    }
+  } else {
   load16(b.his + (uint64_t)c.his_bytes * r, kmeas);
   load16(b.his + (uint64_t)c.his_bytes * r + 16, kproof);
-  uint64_t x[1], proof[5], t[1];
   {  // helper_meas_share: XOF(k_meas, DST(usage 1), [agg_id=1])
     Block m;
     blk_zero(m);
@@ -151,6 +167,7 @@ __global__ __launch_bounds__(256) void count_kernel(Cfg c, Bufs b) {
     blk_pad(m, pos + 2);
     sponge_oneblock(S, m);
     sample64<5>(S, proof);
+  }
   }
   {  // query_rands: XOF(verify_key, DST(usage 5), [PROOFS=1] || nonce)
     Block m;
@@ -181,6 +198,18 @@ __global__ __launch_bounds__(256) void count_kernel(Cfg c, Bufs b) {
   // circuit: Mul(x,x) - x with the gadget replaced by gadget_poly(alpha^1) = g0 - g1 + g2
   uint64_t v = sub64(add64(sub64(proof[2], proof[3]), proof[4]), xm);
   uint64_t G = add64(proof[2], mul64(tt, add64(proof[3], mul64(tt, proof[4]))));
+  if (LEADER) {
+    if (r0 < b.n) {
+      uint2* o = reinterpret_cast<uint2*>(b.lps_out + (uint64_t)c.lps_bytes * r);
+      o[0] = make_uint2(lo32(v), hi32(v));
+      o[1] = make_uint2(lo32(W0), hi32(W0));
+      o[2] = make_uint2(lo32(W1), hi32(W1));
+      o[3] = make_uint2(lo32(G), hi32(G));
+      b.verdicts[r0] = (uint8_t)((verdict || bad) ? 1 : 0);
+    }
+    b.outs[il_idx(blk, 1, 0, lane)] = make_uint4(lo32(xm), hi32(xm), 0, 0);
+    return;
+  }
   // leader verifier share: [v, W0, W1, G] as 4 x 8-byte LE
   const uint8_t* lp = b.lps + (uint64_t)c.lps_bytes * r;
   uint64_t lv[4];
@@ -428,6 +457,17 @@ __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t
   return flags;
 }
 
+// Exact ">= p" test (decoding an explicit Field128 element, VDAF-08 decode rejects x >= p).
+__device__ __forceinline__ bool ge_exact(uint4 v) {
+  return v.w == 0xFFFFFFFFu && (v.z > 0xFFFFFFE4u || (v.z == 0xFFFFFFE4u && (v.x | v.y) != 0u));
+}
+
+// K1 for one role. HELPER (agg_id 1, aggregator.rs:1947): the measurement and proof shares are
+// expanded from seeds by TurboSHAKE128 and the squeeze runs alongside the joint_rand_part absorb.
+// LEADER (agg_id 0, leader_initialized, aggregation_job_driver.rs:345): the shares are explicit in
+// the leader input share (meas || proofs || k_blind, decoded here: elements >= p fail) and only the
+// joint_rand_part absorb runs through Keccak.
+template <bool LEADER>
 __global__ __launch_bounds__(256) void xof_kernel(Cfg c, Bufs b) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t blk = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -436,18 +476,37 @@ __global__ __launch_bounds__(256) void xof_kernel(Cfg c, Bufs b) {
   const uint64_t r0 = blk * 64 + lane;
   const uint64_t r = r0 < b.n ? r0 : b.n - 1;
 
-  const uint8_t* hs = b.his + (uint64_t)c.his_bytes * r;
+  const uint8_t* hs = LEADER ? nullptr : b.his + (uint64_t)c.his_bytes * r;
+  const uint8_t* ls = LEADER ? b.lis + (uint64_t)c.lis_bytes * r : nullptr;
   uint32_t flags = 0;
+  const uint32_t MB = c.meas_len * 16;
+  const uint32_t ML = 42 + MB;
+  const uint32_t NM = (MB + 167) / 168;  // measurement-share blocks of 168 bytes
+  const uint32_t b_last = ML / 168;      // last absorbed block (b_last <= NM)
 
   // ---- measurement share fused with the joint_rand_part absorb --------------------
-  // S: XOF(k_meas, DST(1), [1])            (squeezing, 168 bytes per block)
-  // J: XOF(k_blind, DST(7), [1] || nonce || enc(meas_share))   (absorbing those bytes)
+  // S: block m of the measurement share. Helper: XOF(k_meas, DST(1), [1]) squeezed 168 bytes
+  //    per block; leader: bytes [168m, 168m + 168) of its explicit share.
+  // J: XOF(k_blind, DST(7), [agg_id] || nonce || enc(meas_share))   (absorbing those bytes)
   // J's message block m is meas bytes [168m - 42, 168m + 126): the 42-byte header makes it a
-  // 16-bit funnel shift (v_alignbit_b32) of squeezed words of blocks m-1 and m. After block m
-  // is consumed, S (-> block m+1) and J (absorb block m) permute together: two independent
-  // streams (keccak_p12_x2).
+  // 16-bit funnel shift (v_alignbit_b32) of the words of blocks m-1 and m. On the helper, after
+  // block m is consumed S (-> block m+1) and J (absorb block m) permute together: two
+  // independent streams (keccak_p12_x2).
   uint32_t S[50], J[50];
-  {
+  // leader: load block m of the explicit share (words past the share's end read as 0)
+  auto load_block = [&](uint32_t m) {
+#pragma unroll
+    for (int q = 0; q < 21; q++) {
+      const uint32_t off = 168 * m + 8 * q;
+      uint2 v = make_uint2(0, 0);
+      if (off < MB) v = *reinterpret_cast<const uint2*>(ls + off);
+      S[2 * q] = v.x;
+      S[2 * q + 1] = v.y;
+    }
+  };
+  if (LEADER) {
+    load_block(0);
+  } else {
     uint32_t kmeas[4];
     load16(hs, kmeas);
     Block m;
@@ -461,47 +520,52 @@ __global__ __launch_bounds__(256) void xof_kernel(Cfg c, Bufs b) {
   {
     uint32_t nonce[4], kblind[4];
     load16(b.nonces + 16 * r, nonce);
-    load16(hs + 32, kblind);
+    load16(LEADER ? ls + MB + 16 * c.proof_len : hs + 32, kblind);
     Block h;
     blk_zero(h);
     int pos = blk_xof_prefix(h, c.algo, 7, kblind);
-    blk_put_byte(h, pos, 1);
+    blk_put_byte(h, pos, LEADER ? 0 : 1);  // agg_id
 #pragma unroll
     for (int i = 0; i < 4; i++) blk_put_word(h, pos + 1 + 4 * i, nonce[i]);
 #pragma unroll
     for (int w = 0; w < 11; w++) hdr[w] = h.w[w];  // 42 header bytes
   }
-  const uint32_t MB = c.meas_len * 16;
-  const uint32_t ML = 42 + MB;
-  const uint32_t NM = (MB + 167) / 168;  // squeezed blocks
-  const uint32_t b_last = ML / 168;      // last absorbed block (b_last <= NM)
   uint32_t prev[11];
   uint32_t carry0 = 0, carry1 = 0;
-  uint32_t gmax = 0;  // running ge_screen over every sampled element
+  uint32_t gmax = 0;  // helper: running ge_screen over every sampled element
+  bool bad = false;   // leader: an explicit element is >= p
   TruncW tr;
   truncw_zero(tr);
   tr.j = 0;
   tr.i = 0;
   uint4* const mp = b.meas + il_idx(blk, c.meas_len, 0, lane);
   uint4* const op = b.outs + il_idx(blk, c.out_len, 0, lane);
-  // emit the measurement elements of squeezed block m (10 or 11, by parity)
+  uint32_t unused_screen = 0;
+  auto emit = [&](uint32_t e, uint4 v) {
+    if (LEADER) {
+      if (e < c.meas_len) bad |= ge_exact(v);
+      emit_meas(c, mp, op, e, v, unused_screen, tr);
+    } else {
+      emit_meas(c, mp, op, e, v, gmax, tr);
+    }
+  };
+  // emit the measurement elements of block m (10 or 11, by parity)
   auto emit_block = [&](uint32_t m) {
     const uint32_t e0 = 21 * (m >> 1);
     if ((m & 1) == 0) {
 #pragma unroll
-      for (int ci = 0; ci < 10; ci++)
-        emit_meas(c, mp, op, e0 + ci, make_uint4(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]), gmax, tr);
+      for (int ci = 0; ci < 10; ci++) emit(e0 + ci, make_uint4(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]));
       carry0 = S[40];
       carry1 = S[41];
     } else {
-      emit_meas(c, mp, op, e0 + 10, make_uint4(carry0, carry1, S[0], S[1]), gmax, tr);
+      const uint32_t c0 = carry0, c1 = carry1;
+      emit(e0 + 10, make_uint4(c0, c1, S[0], S[1]));
 #pragma unroll
       for (int ci = 0; ci < 10; ci++)
-        emit_meas(c, mp, op, e0 + 11 + ci, make_uint4(S[2 + 4 * ci], S[3 + 4 * ci], S[4 + 4 * ci], S[5 + 4 * ci]),
-                  gmax, tr);
+        emit(e0 + 11 + ci, make_uint4(S[2 + 4 * ci], S[3 + 4 * ci], S[4 + 4 * ci], S[5 + 4 * ci]));
     }
   };
-  // J ^= message block m built from S (block m, if squeezed) and prev (block m-1)
+  // J ^= message block m built from S (block m, if present) and prev (block m-1)
   auto absorb_block = [&](uint32_t m, bool have) {
     const uint32_t s0 = have ? S[0] : 0u;
     if (m == 0) {
@@ -555,72 +619,105 @@ __global__ __launch_bounds__(256) void xof_kernel(Cfg c, Bufs b) {
     for (int w = 0; w < 42; w++) J[w] ^= jw[w];
     keccak_p12(J);
   };
-  // blocks m = 0 .. b_last (b_last <= NM); squeezed blocks m < NM. Block 0 is peeled so
-  // that the 42-byte header is dead inside the main loop.
+  // advance to block m+1: helper squeezes (together with J's permutation), leader loads
+  auto advance = [&](uint32_t m) {
+    if (LEADER) {
+      if (m + 1 < NM) load_block(m + 1);
+      keccak_p12(J);
+    } else if (m + 1 < NM) {
+      keccak_p12_x2(S, J);
+    } else {
+      keccak_p12(J);
+    }
+  };
+  // blocks m = 0 .. b_last (b_last <= NM); blocks m < NM hold measurement bytes. Block 0 is
+  // peeled so that the 42-byte header is dead inside the main loop.
   emit_block(0);
   if (b_last == 0) {
     absorb_last(0, true);
   } else {
     absorb_block(0, true);
-    if (1 < NM)
-      keccak_p12_x2(S, J);
-    else
-      keccak_p12(J);
+    advance(0);
 #pragma unroll 1
-    for (uint32_t m = 1; m < b_last; m++) {  // m < b_last <= NM: block m was squeezed
+    for (uint32_t m = 1; m < b_last; m++) {  // m < b_last <= NM: block m holds measurement bytes
       emit_block(m);
       absorb_block(m, true);
-      if (m + 1 < NM)
-        keccak_p12_x2(S, J);
-      else
-        keccak_p12(J);
+      advance(m);
     }
     const bool have = b_last < NM;
     if (have) emit_block(b_last);
     absorb_last(b_last, have);
   }
-  uint32_t part_h[4] = {J[0], J[1], J[2], J[3]};
+  uint32_t own_part[4] = {J[0], J[1], J[2], J[3]};
 
-  // ---- proof share: XOF(k_proofs, DST(2), [PROOFS=1, agg_id=1]) -------------------
-  {
-    uint32_t kproof[4];
-    load16(hs + 16, kproof);
-    Block m;
-    blk_zero(m);
-    int pos = blk_xof_prefix(m, c.algo, 2, kproof);
-    blk_put_byte(m, pos, 1);
-    blk_put_byte(m, pos + 1, 1);
-    blk_pad(m, pos + 2);
-    sponge_oneblock(S, m);
-  }
-  const uint32_t NP = (c.proof_len * 16 + 167) / 168;
+  // ---- proof share ------------------------------------------------------------------
   uint4* const pp = b.proof + il_idx(blk, c.proof_len, 0, lane);
+  if (LEADER) {
+    const uint4* src = reinterpret_cast<const uint4*>(ls + MB);
 #pragma unroll 1
-  for (uint32_t m = 0; m < NP; m++) {
-    if (m > 0) keccak_p12(S);
-    const uint32_t e0 = 21 * (m >> 1);
-    if ((m & 1) == 0) {
-#pragma unroll
-      for (int ci = 0; ci < 10; ci++)
-        emit_proof(c, pp, e0 + ci, make_uint4(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]), gmax);
-      carry0 = S[40];
-      carry1 = S[41];
-    } else {
-      emit_proof(c, pp, e0 + 10, make_uint4(carry0, carry1, S[0], S[1]), gmax);
-#pragma unroll
-      for (int ci = 0; ci < 10; ci++)
-        emit_proof(c, pp, e0 + 11 + ci, make_uint4(S[2 + 4 * ci], S[3 + 4 * ci], S[4 + 4 * ci], S[5 + 4 * ci]), gmax);
+    for (uint32_t e = 0; e < c.proof_len; e++) {
+      const uint4 v = src[e];
+      bad |= ge_exact(v);
+      pp[(uint64_t)e * IL] = v;
     }
+  } else {  // XOF(k_proofs, DST(2), [PROOFS=1, agg_id=1])
+    {
+      uint32_t kproof[4];
+      load16(hs + 16, kproof);
+      Block m;
+      blk_zero(m);
+      int pos = blk_xof_prefix(m, c.algo, 2, kproof);
+      blk_put_byte(m, pos, 1);
+      blk_put_byte(m, pos + 1, 1);
+      blk_pad(m, pos + 2);
+      sponge_oneblock(S, m);
+    }
+    const uint32_t NP = (c.proof_len * 16 + 167) / 168;
+#pragma unroll 1
+    for (uint32_t m = 0; m < NP; m++) {
+      if (m > 0) keccak_p12(S);
+      const uint32_t e0 = 21 * (m >> 1);
+      if ((m & 1) == 0) {
+#pragma unroll
+        for (int ci = 0; ci < 10; ci++)
+          emit_proof(c, pp, e0 + ci, make_uint4(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]), gmax);
+        carry0 = S[40];
+        carry1 = S[41];
+      } else {
+        emit_proof(c, pp, e0 + 10, make_uint4(carry0, carry1, S[0], S[1]), gmax);
+#pragma unroll
+        for (int ci = 0; ci < 10; ci++)
+          emit_proof(c, pp, e0 + 11 + ci, make_uint4(S[2 + 4 * ci], S[3 + 4 * ci], S[4 + 4 * ci], S[5 + 4 * ci]),
+                     gmax);
+      }
+    }
+    if (gmax == 0xFFFFFFFFu) flags |= FLAG_SLOW;
   }
-  if (gmax == 0xFFFFFFFFu) flags |= FLAG_SLOW;
 
-  uint32_t part_l[4], lead_part[4], nonce[4];
-  load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
-  load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
+  uint32_t nonce[4];
   load16(b.nonces + 16 * r, nonce);
-  flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, part_l, lead_part, part_h, flags, false);
-  if (b.force_slow) flags |= FLAG_SLOW;
-  if (r0 < b.n) b.flags[r0] = flags;
+  if (LEADER) {
+    // corrected seed = XOF(0, DST(6), own part || helper's part from the public share): the
+    // leader's prepare state (written to msgs), and own part goes out in the prep share
+    uint32_t part_h[4];
+    load16(b.ps + (uint64_t)c.ps_bytes * r + 16, part_h);
+    flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, own_part, own_part, part_h, flags, false);
+    if (flags & FLAG_SLOW)  // a rejected joint/query randomness sample (~2^-120): redo exactly
+      flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, own_part, own_part, part_h, flags & ~FLAG_SLOW, true);
+    if (bad) flags |= FLAG_INPUT_FAIL;
+    if (r0 < b.n) {
+      *reinterpret_cast<uint4*>(b.lps_out + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16) =
+          make_uint4(own_part[0], own_part[1], own_part[2], own_part[3]);
+      b.flags[r0] = flags;
+    }
+  } else {
+    uint32_t part_l[4], lead_part[4];
+    load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
+    load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
+    flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, part_l, lead_part, own_part, flags, false);
+    if (b.force_slow) flags |= FLAG_SLOW;
+    if (r0 < b.n) b.flags[r0] = flags;
+  }
 }
 
 // ---------------------------------------------------------------------------- K1': slow XOF path
@@ -758,6 +855,8 @@ __device__ __forceinline__ f128 ld_lead(const Bufs& b, const Cfg& c, uint64_t r,
 }
 
 // Prio3Sum: gadget PolyEval(x^2 - x), arity 1, `bits` calls; one report per lane.
+// LEADER: writes the leader's verifier share [v, W0, G(t)] as its prep share.
+template <bool LEADER>
 __global__ __launch_bounds__(256) void flp_sum_kernel(Cfg c, Bufs b) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t blk = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -792,6 +891,16 @@ __global__ __launch_bounds__(256) void flp_sum_kernel(Cfg c, Bufs b) {
   }
   f128 G = make128(0, 0);
   for (uint32_t m = GL; m-- > 0;) G = add128(mont128(G, tR), ld_il(b.proof, blk, c.proof_len, 1 + m, lane));
+  if (LEADER) {
+    if (r0 < b.n) {
+      uint4* o = reinterpret_cast<uint4*>(b.lps_out + (uint64_t)c.lps_bytes * r);
+      o[0] = f_to_u4(v);
+      o[1] = f_to_u4(W0);
+      o[2] = f_to_u4(G);
+      b.verdicts[r0] = (b.flags[r] & (FLAG_INIT_FAIL | FLAG_INPUT_FAIL)) ? 1 : 0;
+    }
+    return;
+  }
   bool dfail = false;
   f128 lv = ld_lead(b, c, r, 0, dfail), lw = ld_lead(b, c, r, 1, dfail), lg = ld_lead(b, c, r, 2, dfail);
   const uint32_t flags = b.flags[r];
@@ -822,7 +931,7 @@ __global__ __launch_bounds__(256) void flp_sum_kernel(Cfg c, Bufs b) {
 // slots, its share of v (sum_m g_m S_m), its share of G(t), and (Histogram) sum of x.
 // Phase 2 (flp_psum_final_kernel): one report per lane; adds the partials, the leader's
 // v and G(t), and decides.
-template <int PPW, bool HIST>
+template <int PPW, bool HIST, bool LEADER>
 __global__ __launch_bounds__(64, 4) void flp_psum_part_kernel(Cfg c, Bufs b) {
   const uint32_t NG = c.ngroups;
   // Workgroup ids are dispatched round-robin over the 8 XCDs; map them so that the NG
@@ -931,9 +1040,17 @@ __global__ __launch_bounds__(64, 4) void flp_psum_part_kernel(Cfg c, Bufs b) {
       f128 We = mont128(add128(mont128(se, c0R), mont128(E, rpow)), LR);
       f128 Wo = mont128(sub128(add128(mont128(so, c0R), O), hs), LR);
       rpow = mont128(rpow, rR);
-      f128 Ve = add128(We, ld_lead(b, c, r, 1 + 2 * j, dfail));
-      f128 Vo = add128(Wo, ld_lead(b, c, r, 2 + 2 * j, dfail));
-      prod = add128(prod, mont128(Ve, Vo));
+      if (LEADER) {  // the leader's verifier share: wire values at t
+        if (r0 < b.n) {
+          uint4* o = reinterpret_cast<uint4*>(b.lps_out + (uint64_t)c.lps_bytes * r);
+          o[1 + 2 * j] = f_to_u4(We);
+          o[2 + 2 * j] = f_to_u4(Wo);
+        }
+      } else {
+        f128 Ve = add128(We, ld_lead(b, c, r, 1 + 2 * j, dfail));
+        f128 Vo = add128(Wo, ld_lead(b, c, r, 2 + 2 * j, dfail));
+        prod = add128(prod, mont128(Ve, Vo));
+      }
     }
   }
   // ---- gadget polynomial: v-part = sum_m g_m * S_m and the G(t) part over this group's m-range
@@ -958,7 +1075,7 @@ __global__ __launch_bounds__(64, 4) void flp_psum_part_kernel(Cfg c, Bufs b) {
   if (dfail && r0 < b.n) atomicOr(&b.flags[r0], FLAG_DFAIL);
 }
 
-template <bool HIST>
+template <bool HIST, bool LEADER>
 __global__ __launch_bounds__(256) void flp_psum_final_kernel(Cfg c, Bufs b) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= b.n) return;
@@ -981,6 +1098,13 @@ __global__ __launch_bounds__(256) void flp_psum_final_kernel(Cfg c, Bufs b) {
     vh = add128(mont128(V, r2R), mont128(sc, mont128(r2R, r2R)));
   }
   const uint32_t flags = b.flags[r];
+  if (LEADER) {  // verifier share [v, wires(t)..., G(t)]; wires were written by the part kernel
+    uint4* o = reinterpret_cast<uint4*>(b.lps_out + (uint64_t)c.lps_bytes * r);
+    o[0] = f_to_u4(vh);
+    o[A + 1] = f_to_u4(G);
+    b.verdicts[r] = (flags & (FLAG_INIT_FAIL | FLAG_INPUT_FAIL)) ? 1 : 0;
+    return;
+  }
   bool df = (flags & FLAG_DFAIL) != 0;
   f128 lv = ld_lead(b, c, r, 0, df), lg = ld_lead(b, c, r, A + 1, df);
   uint32_t verdict = 0;
@@ -996,6 +1120,18 @@ __global__ __launch_bounds__(256) void flp_psum_final_kernel(Cfg c, Bufs b) {
       verdict = 4;
   }
   b.verdicts[r] = (uint8_t)verdict;
+}
+
+// ---------------------------------------------------------------------------- leader prepare_next
+// leader_continued on PingPongMessage::Finish{prep_msg} (aggregation_job_driver.rs:588-602):
+// prio prepare_next fails unless prep_msg equals the corrected joint-rand seed of the state.
+__global__ __launch_bounds__(256) void leader_finish_kernel(Cfg c, Bufs b, const uint8_t* prep_msgs) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= b.n) return;
+  if (b.verdicts[r] != 0 || c.jr_len == 0) return;
+  const uint4 m = *reinterpret_cast<const uint4*>(prep_msgs + 16 * r);
+  const uint4 k = *reinterpret_cast<const uint4*>(b.msgs + 16 * r);
+  if (m.x != k.x || m.y != k.y || m.z != k.z || m.w != k.w) b.verdicts[r] = 4;
 }
 
 // ---------------------------------------------------------------------------- K4: accumulate
@@ -1215,12 +1351,22 @@ static inline uint32_t nblk_of(uint64_t n) { return (uint32_t)((n + 63) / 64); }
 
 hipError_t launch_count(const Cfg& c, const Bufs& b, hipStream_t s) {
   uint32_t nb = nblk_of(b.n);
-  hipLaunchKernelGGL(count_kernel, dim3((nb * 64 + 255) / 256), dim3(256), 0, s, c, b);
+  if (b.leader)
+    hipLaunchKernelGGL(count_kernel<true>, dim3((nb * 64 + 255) / 256), dim3(256), 0, s, c, b);
+  else
+    hipLaunchKernelGGL(count_kernel<false>, dim3((nb * 64 + 255) / 256), dim3(256), 0, s, c, b);
   return hipGetLastError();
 }
 hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
   uint32_t nb = nblk_of(b.n);
-  hipLaunchKernelGGL(xof_kernel, dim3((nb + 3) / 4), dim3(256), 0, s, c, b);
+  if (b.leader)
+    hipLaunchKernelGGL(xof_kernel<true>, dim3((nb + 3) / 4), dim3(256), 0, s, c, b);
+  else
+    hipLaunchKernelGGL(xof_kernel<false>, dim3((nb + 3) / 4), dim3(256), 0, s, c, b);
+  return hipGetLastError();
+}
+hipError_t launch_leader_finish(const Cfg& c, const Bufs& b, const uint8_t* prep_msgs, hipStream_t s) {
+  hipLaunchKernelGGL(leader_finish_kernel, dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, c, b, prep_msgs);
   return hipGetLastError();
 }
 hipError_t launch_xof_slow(const Cfg& c, const Bufs& b, hipStream_t s) {
@@ -1250,24 +1396,35 @@ int psum_ppw(uint32_t chunk) {
   return best;
 }
 
-template <int PPW>
-static hipError_t launch_psum_t(const Cfg& c, const Bufs& b, hipStream_t s) {
+template <int PPW, bool HIST, bool LEADER>
+static void launch_psum_r(const Cfg& c, const Bufs& b, hipStream_t s) {
   const uint32_t nb = nblk_of(b.n);
   const uint32_t grid = ((nb + 7) / 8) * 8 * c.ngroups;
-  if (c.algo == ALGO_HISTOGRAM) {
-    hipLaunchKernelGGL((flp_psum_part_kernel<PPW, true>), dim3(grid), dim3(64), 0, s, c, b);
-    hipLaunchKernelGGL((flp_psum_final_kernel<true>), dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, c, b);
-  } else {
-    hipLaunchKernelGGL((flp_psum_part_kernel<PPW, false>), dim3(grid), dim3(64), 0, s, c, b);
-    hipLaunchKernelGGL((flp_psum_final_kernel<false>), dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, c, b);
-  }
+  hipLaunchKernelGGL((flp_psum_part_kernel<PPW, HIST, LEADER>), dim3(grid), dim3(64), 0, s, c, b);
+  hipLaunchKernelGGL((flp_psum_final_kernel<HIST, LEADER>), dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s,
+                     c, b);
+}
+template <int PPW>
+static hipError_t launch_psum_t(const Cfg& c, const Bufs& b, hipStream_t s) {
+  const bool hist = c.algo == ALGO_HISTOGRAM;
+  if (hist && b.leader)
+    launch_psum_r<PPW, true, true>(c, b, s);
+  else if (hist)
+    launch_psum_r<PPW, true, false>(c, b, s);
+  else if (b.leader)
+    launch_psum_r<PPW, false, true>(c, b, s);
+  else
+    launch_psum_r<PPW, false, false>(c, b, s);
   return hipGetLastError();
 }
 
 hipError_t launch_flp(const Cfg& c, const Bufs& b, hipStream_t s) {
   if (c.algo == ALGO_SUM) {
     uint32_t nb = nblk_of(b.n);
-    hipLaunchKernelGGL(flp_sum_kernel, dim3((nb + 3) / 4), dim3(256), 0, s, c, b);
+    if (b.leader)
+      hipLaunchKernelGGL(flp_sum_kernel<true>, dim3((nb + 3) / 4), dim3(256), 0, s, c, b);
+    else
+      hipLaunchKernelGGL(flp_sum_kernel<false>, dim3((nb + 3) / 4), dim3(256), 0, s, c, b);
     return hipGetLastError();
   }
   switch (c.ppw) {

@@ -60,6 +60,12 @@ def _u8(a, n: int, width: int, what: str) -> np.ndarray:
 
 
 @dataclass
+class LeaderInit:
+    verdicts: np.ndarray       # uint8[n]: 0 initialized, 1 prepare_init_failure
+    prep_shares: np.ndarray    # uint8[n, LPS]: payloads of PingPongMessage::Initialize
+
+
+@dataclass
 class BatchResult:
     verdicts: np.ndarray       # uint8[n]
     prep_msgs: np.ndarray      # uint8[n, PM]
@@ -70,7 +76,10 @@ class BatchResult:
 
 
 class HelperEngine:
-    """One engine per (Prio3 instance, verify key, GPU)."""
+    """One engine per (Prio3 instance, verify key, GPU). Serves the helper role (the north-star
+    path) and the leader role of the same ping-pong exchange."""
+
+    _leader_n = 0
 
     def __init__(self, vdaf: Prio3, verify_key: bytes, device: int = 0):
         if len(verify_key) != 16:
@@ -89,6 +98,9 @@ class HelperEngine:
         check(L.jx_engine_sizes(h, *[ctypes.byref(s) for s in sizes]), h, "jx_engine_sizes")
         self.public_share_len, self.helper_input_share_len, self.prep_share_len, self.prep_msg_len, \
             self.output_len, self.field_bytes = (s.value for s in sizes)
+        lis = ctypes.c_uint32()
+        check(L.jx_engine_leader_sizes(h, ctypes.byref(lis)), h, "jx_engine_leader_sizes")
+        self.leader_input_share_len = lis.value
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):
@@ -133,6 +145,39 @@ class HelperEngine:
                                           _ptr(verdicts), _ptr(outs))
         check(st, self._h, "jx_helper_prep_batch")
         return BatchResult(verdicts[:n], msgs[:n, : self.prep_msg_len], outs[:n] if outs is not None else None)
+
+    # ------------------------------------------------------------------ leader role
+    def leader_initialized_batch(self, nonces, public_shares, leader_input_shares) -> "LeaderInit":
+        """prio ping-pong leader_initialized for n reports (aggregation_job_driver.rs:344-362):
+        prepare_init with agg_id 0 on the explicit leader input shares. Returns the verdicts
+        (0 = initialized, 1 = prepare_init_failure) and the prep shares that go into each
+        PingPongMessage::Initialize. The prepare states stay on the device for
+        leader_continued_batch."""
+        n = int(np.asarray(nonces).reshape(-1, 16).shape[0])
+        nn = _u8(nonces, n, 16, "nonces")
+        ps = _u8(public_shares, n, self.public_share_len, "public_shares")
+        lis = _u8(leader_input_shares, n, self.leader_input_share_len, "leader_input_shares")
+        verdicts = np.zeros(max(n, 1), np.uint8)
+        shares = np.zeros((max(n, 1), self.prep_share_len), np.uint8)
+        st = self._L.jx_leader_prep_init_batch(self._h, n, _ptr(nn), _ptr(ps) if self.public_share_len else None,
+                                               _ptr(lis), _ptr(shares), _ptr(verdicts))
+        check(st, self._h, "jx_leader_prep_init_batch")
+        self._leader_n = n
+        return LeaderInit(verdicts[:n], shares[:n])
+
+    def leader_continued_batch(self, prep_msgs, want_out_shares: bool = False) -> BatchResult:
+        """prio ping-pong leader_continued on the helper's Finish{prep_msg} for the batch of the
+        last leader_initialized_batch (aggregation_job_driver.rs:588-602): prepare_next."""
+        n = self._leader_n
+        msgs = None
+        if self.prep_msg_len:
+            msgs = _u8(prep_msgs, n, self.prep_msg_len, "prep_msgs")
+        verdicts = np.zeros(max(n, 1), np.uint8)
+        outs = np.zeros((max(n, 1), self.output_len * self.field_bytes), np.uint8) if want_out_shares else None
+        st = self._L.jx_leader_prep_finish_batch(self._h, n, _ptr(msgs), _ptr(verdicts), _ptr(outs))
+        check(st, self._h, "jx_leader_prep_finish_batch")
+        return BatchResult(verdicts[:n], msgs[:n] if msgs is not None else np.zeros((n, 0), np.uint8),
+                           outs[:n] if outs is not None else None)
 
     def accumulate(self, n: int, accept_mask: np.ndarray | None = None, segments: np.ndarray | None = None):
         """Merge the finished output shares of the last batch into batch aggregations."""
@@ -228,4 +273,6 @@ class HelperEngine:
         check(self._L.jx_engine_debug(self._h, option, value), self._h, "jx_engine_debug")
 
 
-__all__ = ["HelperEngine", "BatchResult", "EngineError", "VERDICT_LABELS", "FINISHED"]
+Prio3Engine = HelperEngine
+
+__all__ = ["HelperEngine", "Prio3Engine", "BatchResult", "LeaderInit", "EngineError", "VERDICT_LABELS", "FINISHED"]
