@@ -22,7 +22,8 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from .engine import FINISHED, VERDICT_LABELS, HelperEngine
-from .messages import CodecError, PingPongMessage, PrepareError, PrepareInit, PrepareResp, PrepareStepResult
+from .messages import (CodecError, HpkeCiphertext, PingPongMessage, PrepareError, PrepareInit, PrepareResp,  # noqa: F401
+                       PrepareStepResult, ReportMetadata, ReportShare)
 
 
 @dataclass
@@ -95,4 +96,115 @@ def handle_aggregate_init(engine: HelperEngine, prepare_inits: list[PrepareInit]
             finished[i] = True
         engine.accumulate(m, accept, seg)
     responses = [PrepareResp(ids[i], results[i]) for i in range(n)]
+    return AggregateInitOutcome(responses, finished, failures)
+
+
+# ----------------------------------------------------------------------------- leader side
+# Mirror of AggregationJobDriver::step_aggregation_job_aggregate_init and
+# process_response_from_helper (aggregator/src/aggregator/aggregation_job_driver.rs:259-436,
+# 540-701) minus the HTTP exchange and the datastore: the leader's per-report
+# leader_initialized / leader_continued calls become two engine batch calls.
+
+
+@dataclass
+class LeaderReport:
+    metadata: ReportMetadata
+    public_share: bytes
+    leader_input_share: bytes                  # decoded at upload time in Janus; encoded here
+    helper_encrypted_input_share: HpkeCiphertext
+
+
+@dataclass
+class LeaderStep:
+    prepare_inits: list[PrepareInit]           # the AggregationJobInitializeReq body
+    stepped: list[int]                         # report index of each PrepareInit
+    failed: dict[int, PrepareError]            # reports that failed before the helper
+    n: int                                     # reports in the engine's leader batch
+    step_failures: Counter = field(default_factory=Counter)
+
+
+def leader_aggregate_init(engine: HelperEngine, reports: list[LeaderReport]) -> LeaderStep:
+    """Prepare every report of a new aggregation job on the leader (agg_id 0) and build the
+    PrepareInits to send to the helper (aggregation_job_driver.rs:301-386)."""
+    v = engine.vdaf
+    n = len(reports)
+    failures: Counter = Counter()
+    failed: dict[int, PrepareError] = {}
+    ok = [i for i, r in enumerate(reports) if len(r.leader_input_share) == engine.leader_input_share_len
+          and len(r.public_share) == v.public_share_len]
+    for i in set(range(n)) - set(ok):
+        failed[i] = PrepareError.InvalidMessage
+        failures["input_share_decode_failure"] += 1
+    inits: list[PrepareInit] = []
+    stepped: list[int] = []
+    if ok:
+        nonces = np.frombuffer(b"".join(reports[i].metadata.report_id for i in ok), np.uint8).reshape(len(ok), 16)
+        ps = np.frombuffer(b"".join(reports[i].public_share for i in ok), np.uint8)
+        lis = np.frombuffer(b"".join(reports[i].leader_input_share for i in ok), np.uint8)
+        res = engine.leader_initialized_batch(nonces, ps, lis)
+        for j, i in enumerate(ok):
+            if res.verdicts[j] != FINISHED:  # handle_ping_pong_error(Role::Leader, ...)
+                failed[i] = PrepareError.VdafPrepError
+                failures[VERDICT_LABELS[int(res.verdicts[j])]] += 1
+                continue
+            r = reports[i]
+            inits.append(PrepareInit(ReportShare(r.metadata, r.public_share, r.helper_encrypted_input_share),
+                                     PingPongMessage.initialize(res.prep_shares[j].tobytes())))
+            stepped.append(i)
+    step = LeaderStep(inits, stepped, failed, len(ok), failures)
+    step._batch_index = {i: j for j, i in enumerate(ok)}  # report index -> engine batch row
+    return step
+
+
+def leader_process_helper_response(engine: HelperEngine, step: LeaderStep, prepare_resps: list[PrepareResp],
+                                   segments: list[int] | None = None) -> AggregateInitOutcome:
+    """Finish the leader's reports from the helper's AggregationJobResp and accumulate the
+    finished ones (process_response_from_helper, aggregation_job_driver.rs:540-701)."""
+    if len(prepare_resps) != len(step.stepped) or any(
+            resp.report_id != step.prepare_inits[k].report_share.metadata.report_id
+            for k, resp in enumerate(prepare_resps)):
+        raise ValueError("missing, duplicate, out-of-order, or unexpected prepare steps in response")
+    failures = Counter(step.step_failures)
+    nrep = max([*step.stepped, *step.failed, -1]) + 1
+    finished = np.zeros(nrep, bool)
+    results: dict[int, PrepareError | None] = dict(step.failed)
+    pm = engine.prep_msg_len
+    msgs = np.zeros((step.n, max(pm, 1)), np.uint8)
+    continued = np.zeros(step.n, bool)
+    for k, resp in enumerate(prepare_resps):
+        i = step.stepped[k]
+        row = step._batch_index[i]
+        res = resp.result
+        if res.kind == 2:                        # Reject(err): the helper's error
+            results[i] = res.error
+            failures["helper_step_failure"] += 1
+        elif res.kind == 1:                      # Finished, but a 1-round leader is still Continued
+            results[i] = PrepareError.VdafPrepError
+            failures["finish_mismatch"] += 1
+        elif res.message.kind != PingPongMessage.FINISH or len(res.message.prep_msg) != pm:
+            results[i] = PrepareError.VdafPrepError  # PingPongError::PeerMessageMismatch / CodecPrepMessage
+            failures["leader_ping_pong_message_mismatch"] += 1
+        else:
+            if pm:
+                msgs[row, :pm] = np.frombuffer(res.message.prep_msg, np.uint8)
+            continued[row] = True
+    fin = engine.leader_continued_batch(msgs[:, :pm] if pm else None)
+    accept = np.zeros(step.n, np.uint8)
+    seg = np.zeros(step.n, np.uint32)
+    for i, row in step._batch_index.items():
+        if not continued[row]:
+            continue
+        if fin.verdicts[row] != FINISHED:
+            results[i] = PrepareError.VdafPrepError
+            failures[VERDICT_LABELS[int(fin.verdicts[row])]] += 1
+            continue
+        results[i] = None
+        accept[row] = 1
+        seg[row] = segments[i] if segments else 0
+        finished[i] = True
+    engine.accumulate(step.n, accept, seg)
+    responses = [PrepareResp(step.prepare_inits[k].report_share.metadata.report_id,
+                             PrepareStepResult(1) if results[i] is None else
+                             PrepareStepResult(2, error=results[i]))
+                 for k, i in enumerate(step.stepped)]
     return AggregateInitOutcome(responses, finished, failures)

@@ -130,3 +130,45 @@ def test_ping_pong_leader_helper_on_device(name):
     for i in np.nonzero(fin.verdicts == 0)[0][:8]:
         _, _, out, _ = orc.prep_init(vk, 0, nonces[i].tobytes(), ps[i].tobytes(), lis[i].tobytes())
         assert fin.out_shares[i].tobytes() == out
+
+
+def test_dap_handlers_end_to_end():
+    """The DAP-level mirrors: leader_aggregate_init -> helper handle_aggregate_init (with one
+    replayed report and one malformed leader message) -> leader_process_helper_response; the
+    two batch aggregations add up to the measurements of the reports both sides finished."""
+    from janus_amd.aggregator import (LeaderReport, handle_aggregate_init, leader_aggregate_init,
+                                      leader_process_helper_response)
+    from janus_amd.messages import HpkeCiphertext, PingPongMessage, PrepareError, PrepareInit, ReportMetadata
+
+    v = Prio3.sum_vec(4, 50, 7)
+    vk = bytes(range(7, 23))
+    orc = O.Prio3Oracle(v.algo_id, v.bits, v.length, v.chunk_length)
+    n = 40
+    meas, nonces, ps, lis, his = _shard(orc, v, n, seed=99)
+    reports = [LeaderReport(ReportMetadata(nonces[i].tobytes(), 1_700_000_000 + i), ps[i].tobytes(),
+                            lis[i].tobytes(), HpkeCiphertext(1, b"enc", b"ct")) for i in range(n)]
+    reports[6] = LeaderReport(reports[6].metadata, reports[6].public_share, reports[6].leader_input_share[:-1],
+                              reports[6].helper_encrypted_input_share)  # truncated leader share
+    with HelperEngine(v, vk) as leader, HelperEngine(v, vk) as helper:
+        step = leader_aggregate_init(leader, reports)
+        assert step.failed == {6: PrepareError.InvalidMessage}
+        inits = list(step.prepare_inits)
+        k9 = step.stepped.index(9)
+        bad = inits[k9]
+        inits[k9] = PrepareInit(bad.report_share, PingPongMessage.initialize(bad.message.prep_share[:-1]))
+        helper_shares = [his[i].tobytes() for i in step.stepped]
+        replayed = {nonces[12].tobytes()}
+        out = handle_aggregate_init(helper, inits, helper_shares, replayed=replayed)
+        by_id = {r.report_id: r.result for r in out.responses}
+        assert by_id[nonces[9].tobytes()].error == PrepareError.VdafPrepError
+        assert by_id[nonces[12].tobytes()].error == PrepareError.ReportReplayed
+        assert out.step_failures["leader_prep_share_decode_failure"] == 1
+        lead = leader_process_helper_response(leader, step, out.responses)
+        ok = np.zeros(n, bool)
+        ok[[i for i in range(n) if lead.finished[i]]] = True
+        assert not ok[[6, 9, 12]].any() and ok.sum() == n - 3
+        agg_l, cnt_l, _ = leader.aggregate_share(0)
+        agg_h, cnt_h, _ = helper.aggregate_share(0)
+    assert cnt_l == cnt_h == n - 3
+    total = [(a + b) % P128 for a, b in zip(_decode(agg_l, 16), _decode(agg_h, 16))]
+    assert total == _expected_total(v, meas, ok)
