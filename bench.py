@@ -81,10 +81,12 @@ def pmc_traffic(kernel: str, reports_per_launch: float):
     run's reports per launch. None if the summary or kernel is missing."""
     try:
         d = json.load(open(PMC_SUMMARY))
-        e = d["kernels"][kernel]
+        names = [k for k in d["kernels"] if k == kernel] or \
+            [k for k in d["kernels"] if k.startswith(kernel) and "<true" not in k and "true>" not in k]
+        e = d["kernels"][names[0]]
         per_report = (e["hbm_read_bytes"] + e["hbm_write_bytes"]) / d["workload"]["reports_per_launch"]
         return int(per_report * reports_per_launch), os.path.relpath(PMC_SUMMARY, ROOT)
-    except (OSError, KeyError, ValueError):
+    except (OSError, KeyError, ValueError, IndexError):
         return None, None
 
 
@@ -236,7 +238,7 @@ def main():
     dominant = "K1 xof_kernel" if kt["xof"]["ms"] >= kt["flp"]["ms"] else "K3 flp_psum_part_kernel"
     ach = k1_tops if dominant.startswith("K1") else k3_tops
     traffic, traffic_src = pmc_traffic("jx::xof_kernel" if dominant.startswith("K1") else
-                                       "jx::flp_psum_part_kernel<2, false>", chunk_reports)
+                                       "jx::flp_psum_part_kernel", chunk_reports)
     out = {
         "metric": METRIC,
         "value": round(value, 1),
