@@ -9,8 +9,9 @@ import subprocess
 import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-SOURCES = [os.path.join(_HERE, "csrc", f) for f in ("jx_kernels.hip", "jx_engine.cpp")]
-HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("jx_field.h", "jx_keccak.h", "jx_sha256.h", "jx_kernels.h")]
+SOURCES = [os.path.join(_HERE, "csrc", f) for f in ("jx_kernels.hip", "jx_engine.cpp", "jx_hpke.hip")]
+HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("jx_field.h", "jx_keccak.h", "jx_sha256.h", "jx_kernels.h",
+                                                  "jx_hpke.h")]
 OUT = os.path.join(_HERE, "lib", "libjanus_prio3.so")
 ARCH = os.environ.get("JX_OFFLOAD_ARCH", "gfx950")
 
@@ -19,7 +20,7 @@ def _stale() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = SOURCES + HEADERS + [os.path.join(_HERE, "..", "include", "jx_prio3.h")]
+    deps = SOURCES + HEADERS + [os.path.join(_HERE, "..", "include", h) for h in ("jx_prio3.h", "jx_hpke.h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 

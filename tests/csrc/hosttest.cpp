@@ -7,6 +7,7 @@
 #include "../../janus_amd/csrc/jx_field.h"
 #include "../../janus_amd/csrc/jx_keccak.h"
 #include "../../janus_amd/csrc/jx_sha256.h"
+#include "../../janus_amd/csrc/jx_hpke.h"
 
 using namespace jx;
 
@@ -54,6 +55,96 @@ void ht_wide_dot(const uint8_t* xs, const uint8_t* cs, int n, int norm_every, ui
     if (norm_every > 0 && (k + 1) % norm_every == 0) wacc_normalize(a);
   }
   st(out, wacc_reduce(a));
+}
+// ---- HPKE primitives (jx_hpke.h)
+void ht_x25519(const uint8_t k[32], const uint8_t u[32], uint8_t out[32]) {
+  uint8_t kc[32];
+  memcpy(kc, k, 32);
+  kc[0] &= 248;
+  kc[31] &= 127;
+  kc[31] |= 64;
+  uint32_t kw[8], uw[8], ow[8];
+  memcpy(kw, kc, 32);
+  memcpy(uw, u, 32);
+  x25519_ladder(ow, kw, uw);
+  memcpy(out, ow, 32);
+}
+// op: 0 mul, 1 sq, 2 sub, 3 invert, 4 mul_small(121665); inputs/outputs canonical 32-byte LE
+void ht_fe(int op, const uint8_t a[32], const uint8_t b[32], uint8_t out[32]) {
+  uint32_t aw[8], bw[8], ow[8];
+  memcpy(aw, a, 32);
+  memcpy(bw, b, 32);
+  fe x, y, r;
+  fe_from_bytes(x, aw);
+  fe_from_bytes(y, bw);
+  switch (op) {
+    case 0: fe_mul(r, x, y); break;
+    case 1: fe_sq(r, x); break;
+    case 2: fe_sub(r, x, y); break;
+    case 3: fe_invert(r, x); break;
+    default: fe_mul_small(r, x, 121665); break;
+  }
+  fe_to_bytes(ow, r);
+  memcpy(out, ow, 32);
+}
+static uint8_t HT_SBOX[256];
+static void ht_sbox_init() {
+  // FIPS 197 S-box generated from GF(2^8) inverses (independent of the kernel's table)
+  uint8_t inv[256] = {0};
+  for (int x = 1; x < 256; x++)
+    for (int y = 1; y < 256; y++) {
+      int a = x, b = y, r = 0;
+      for (int i = 0; i < 8; i++) {
+        if (b & 1) r ^= a;
+        int hi = a & 0x80;
+        a = (a << 1) & 0xff;
+        if (hi) a ^= 0x1b;
+        b >>= 1;
+      }
+      if (r == 1) {
+        inv[x] = (uint8_t)y;
+        break;
+      }
+    }
+  for (int x = 0; x < 256; x++) {
+    int b = inv[x], s = b;
+    for (int i = 1; i < 5; i++) s ^= ((b << i) | (b >> (8 - i))) & 0xff;
+    HT_SBOX[x] = (uint8_t)(s ^ 0x63);
+  }
+}
+void ht_aes128(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]) {
+  ht_sbox_init();
+  uint32_t k[4], rk[44], i4[4], o4[4];
+  memcpy(k, key, 16);
+  memcpy(i4, in, 16);
+  aes128_expand_key(HT_SBOX, k, rk);
+  aes128_encrypt(HT_SBOX, rk, i4, o4);
+  memcpy(out, o4, 16);
+}
+// x, h: 16-byte blocks; out = x * h in GF(2^128) (GCM bit order)
+void ht_ghash_mul(const uint8_t x[16], const uint8_t h[16], uint8_t out[16]) {
+  uint32_t xw[4], hw[4];
+  for (int i = 0; i < 4; i++) {
+    xw[i] = (uint32_t)x[4 * i] << 24 | (uint32_t)x[4 * i + 1] << 16 | (uint32_t)x[4 * i + 2] << 8 | x[4 * i + 3];
+    hw[i] = (uint32_t)h[4 * i] << 24 | (uint32_t)h[4 * i + 1] << 16 | (uint32_t)h[4 * i + 2] << 8 | h[4 * i + 3];
+  }
+  ghash_mul(xw, hw);
+  for (int i = 0; i < 4; i++)
+    for (int k = 0; k < 4; k++) out[4 * i + k] = (uint8_t)(xw[i] >> (24 - 8 * k));
+}
+// HMAC-SHA256 with a 32-byte key over msg (len <= 119) through hmac_pads/sha256_finish64/hmac_outer
+void ht_hmac32(const uint8_t key[32], const uint8_t* msg, int len, uint8_t out[32]) {
+  uint32_t kb[8], ist[8], ost[8], inner[8], o[8];
+  for (int i = 0; i < 8; i++)
+    kb[i] = (uint32_t)key[4 * i] << 24 | (uint32_t)key[4 * i + 1] << 16 | (uint32_t)key[4 * i + 2] << 8 | key[4 * i + 3];
+  hmac_pads(kb, ist, ost);
+  Msg128 m;
+  m_zero(m);
+  for (int i = 0; i < len; i++) m_byte(m, i, msg[i]);
+  sha256_finish64(inner, ist, m, len);
+  hmac_outer(o, ost, inner);
+  for (int i = 0; i < 8; i++)
+    for (int k = 0; k < 4; k++) out[4 * i + k] = (uint8_t)(o[i] >> (24 - 8 * k));
 }
 // op: 0 add, 1 sub, 2 mul
 uint64_t ht_f64(int op, uint64_t a, uint64_t b) {

@@ -11,8 +11,8 @@ from janus_amd import _lib
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_symbols():
-    src = open(os.path.join(ROOT, "include", "jx_prio3.h")).read()
+def header_symbols(header="jx_prio3.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     return sorted(set(re.findall(r"^\s*(?:int32_t|void|const char\*)\s+(jx_\w+)\s*\(", src, re.M)))
 
 
@@ -29,12 +29,15 @@ def test_header_lists_match(lib):
 
 
 def test_all_symbols_exported(lib):
+    from janus_amd import hpke
+    assert header_symbols("jx_hpke.h") == sorted(hpke.EXPORTED_SYMBOLS)
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T (jx_\w+)", out))
-    missing = set(header_symbols()) - exported
-    assert not missing, missing
-    for s in header_symbols():
-        assert getattr(lib, s) is not None
+    for header in ("jx_prio3.h", "jx_hpke.h"):
+        missing = set(header_symbols(header)) - exported
+        assert not missing, missing
+        for s in header_symbols(header):
+            assert getattr(lib, s) is not None
 
 
 def test_status_strings(lib):

@@ -20,7 +20,8 @@ R = 2**128
 def ht():
     src = os.path.join(HERE, "csrc", "hosttest.cpp")
     so = os.path.join(HERE, "csrc", "libjx_hosttest.so")
-    hdrs = [os.path.join(HERE, "..", "janus_amd", "csrc", h) for h in ("jx_field.h", "jx_keccak.h", "jx_sha256.h")]
+    hdrs = [os.path.join(HERE, "..", "janus_amd", "csrc", h) for h in ("jx_field.h", "jx_keccak.h", "jx_sha256.h",
+                                                                         "jx_hpke.h")]
     if not os.path.exists(so) or any(os.path.getmtime(h) > os.path.getmtime(so) for h in hdrs + [src]):
         subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", so, src], check=True)
     L = ctypes.CDLL(so)
@@ -28,6 +29,11 @@ def ht():
     L.ht_f128.argtypes = [ctypes.c_int, vp, vp, vp]
     L.ht_reduce192.argtypes = [vp, vp]
     L.ht_wide_dot.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp]
+    L.ht_x25519.argtypes = [vp, vp, vp]
+    L.ht_fe.argtypes = [ctypes.c_int, vp, vp, vp]
+    L.ht_aes128.argtypes = [vp, vp, vp]
+    L.ht_ghash_mul.argtypes = [vp, vp, vp]
+    L.ht_hmac32.argtypes = [vp, vp, ctypes.c_int, vp]
     L.ht_mont_lazy.argtypes = [vp, vp, vp]
     L.ht_f64.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
     L.ht_f64.restype = ctypes.c_uint64
@@ -151,3 +157,65 @@ def test_wide_dot_accumulator(ht, n, norm):
         out = ctypes.create_string_buffer(16)
         ht.ht_wide_dot(xb, cb, n, norm, out)
         assert int.from_bytes(out.raw, "little") == sum(x * c for x, c in zip(xs, cs)) % P128
+
+
+# ---------------------------------------------------------------------------- HPKE primitives (jx_hpke.h)
+P25519 = 2**255 - 19
+
+
+def _buf32(x: int) -> bytes:
+    return x.to_bytes(32, "little")
+
+
+def test_fe25519_ops(ht):
+    from oracle import hpke_oracle as H  # noqa: F401
+    rnd = random.Random(5)
+    vals = [0, 1, 2, 19, P25519 - 1, P25519 - 19, 2**254, 2**255 - 20] + [rnd.randrange(P25519) for _ in range(40)]
+    out = ctypes.create_string_buffer(32)
+    for a in vals:
+        for b in vals[:12]:
+            for op, want in ((0, a * b), (2, a - b)):
+                ht.ht_fe(op, _buf32(a), _buf32(b), out)
+                assert int.from_bytes(out.raw, "little") == want % P25519, (op, a, b)
+        ht.ht_fe(1, _buf32(a), _buf32(0), out)
+        assert int.from_bytes(out.raw, "little") == a * a % P25519
+        ht.ht_fe(4, _buf32(a), _buf32(0), out)
+        assert int.from_bytes(out.raw, "little") == a * 121665 % P25519
+        if a:
+            ht.ht_fe(3, _buf32(a), _buf32(0), out)
+            assert int.from_bytes(out.raw, "little") == pow(a, P25519 - 2, P25519)
+
+
+def test_x25519_vs_oracle(ht):
+    from oracle import hpke_oracle as H
+    rnd = random.Random(11)
+    out = ctypes.create_string_buffer(32)
+    cases = [(bytes.fromhex("a546e36bf0527c9d3b16154b82465edd62144c0ac1fc5a18506a2244ba449ac4"),
+              bytes.fromhex("e6db6867583030db3594c1a424b15f7c726624ec26b3353b10a903a6d0ab1c4c"))]
+    cases += [(rnd.randbytes(32), rnd.randbytes(32)) for _ in range(6)]
+    cases += [(rnd.randbytes(32), (9).to_bytes(32, "little")), (rnd.randbytes(32), bytes(32)),
+              (rnd.randbytes(32), b"\xff" * 32)]
+    for k, u in cases:
+        ht.ht_x25519(k, u, out)
+        assert out.raw == H.x25519(k, u)
+
+
+def test_aes_ghash_hmac_vs_oracle(ht):
+    import hashlib
+    import hmac as hm
+
+    from oracle import hpke_oracle as H
+    rnd = random.Random(3)
+    out = ctypes.create_string_buffer(32)
+    for _ in range(20):
+        key, blk = rnd.randbytes(16), rnd.randbytes(16)
+        ht.ht_aes128(key, blk, out)
+        assert out.raw[:16] == H.aes128_encrypt_block(H.aes128_expand(key), blk)
+        x, h = rnd.randbytes(16), rnd.randbytes(16)
+        ht.ht_ghash_mul(x, h, out)
+        want = H._ghash_mul(int.from_bytes(x, "big"), int.from_bytes(h, "big")).to_bytes(16, "big")
+        assert out.raw[:16] == want
+    for n in (0, 1, 23, 51, 55, 56, 63, 64, 92, 95, 119):
+        key, msg = rnd.randbytes(32), rnd.randbytes(n)
+        ht.ht_hmac32(key, msg, n, out)
+        assert out.raw == hm.new(key, msg, hashlib.sha256).digest(), n

@@ -17,12 +17,13 @@
 
 enum {
   OP_XOR, OP_BITOP3, OP_ALIGNBIT, OP_MAD64, OP_MULLO, OP_MULHI, OP_ADD64, OP_MAD24, OP_FMA64,
-  OP_XOR3, OP_ROT, OP_PERM, OP_LSHLOR, OP_ADD3, OP_ADDCO, NOPS
+  OP_XOR3, OP_ROT, OP_PERM, OP_LSHLOR, OP_ADD3, OP_ADDCO, OP_MIX_AX, OP_MIX_ABX, NOPS
 };
 static const char* NAMES[NOPS] = {"v_xor_b32",      "v_bitop3_b32(a^~b&c)", "v_alignbit_b32", "v_mad_u64_u32",
                                   "v_mul_lo_u32",   "v_mul_hi_u32+xor",     "add_u64",        "v_mad_u32_u24",
                                   "v_fma_f64",      "v_bitop3_b32(xor3)",   "v_alignbit(rot)", "v_perm_b32",
-                                  "v_lshl_or_b32",  "v_add3_u32",           "v_add_co+addc"};
+                                  "v_lshl_or_b32",  "v_add3_u32",           "v_add_co+addc",
+                                  "mix 4 alignbit + 4 xor", "mix 3 alignbit + 3 bitop3 + 2 xor"};
 
 template <int OP>
 __global__ __launch_bounds__(256) void bench(uint32_t* out, int iters, uint32_t k) {
@@ -80,6 +81,22 @@ __global__ __launch_bounds__(256) void bench(uint32_t* out, int iters, uint32_t 
       } else if constexpr (OP == OP_ADD3) {
 #pragma unroll
         for (int j = 0; j < 8; j++) x[j] = x[j] + x[(j + 1) & 7] + x[(j + 2) & 7];
+      } else if constexpr (OP == OP_MIX_AX) {
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          x[j] = __builtin_amdgcn_alignbit(x[j], x[(j + 1) & 7], k + j);
+          x[j + 1] = __builtin_amdgcn_bitop3_b32(x[j + 1], x[(j + 2) & 7], 0u, 0x3c);  // a ^ b
+        }
+      } else if constexpr (OP == OP_MIX_ABX) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          if (j % 8 < 3)
+            x[j] = __builtin_amdgcn_alignbit(x[j], x[(j + 1) & 7], k + j);
+          else if (j % 8 < 6)
+            x[j] = __builtin_amdgcn_bitop3_b32(x[j], x[(j + 1) & 7], x[(j + 2) & 7], 0xd2);
+          else
+            x[j] = x[j] ^ x[(j + 3) & 7] ^ k;
+        }
       } else {
 #pragma unroll
         for (int j = 0; j < 8; j++) {
@@ -138,6 +155,8 @@ int main(int argc, char** argv) {
   run<OP_LSHLOR>(blocks, iters, d);
   run<OP_ADD3>(blocks, iters, d);
   run<OP_ADDCO>(blocks, iters, d);
+  run<OP_MIX_AX>(blocks, iters, d);
+  run<OP_MIX_ABX>(blocks, iters, d);
   CHK(hipFree(d));
   return 0;
 }
