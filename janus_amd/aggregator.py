@@ -22,8 +22,9 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from .engine import FINISHED, VERDICT_LABELS, HelperEngine
-from .messages import (CodecError, HpkeCiphertext, PingPongMessage, PrepareError, PrepareInit, PrepareResp,  # noqa: F401
-                       PrepareStepResult, ReportMetadata, ReportShare)
+from .messages import (EXTENSION_TASKPROV, CodecError, HpkeCiphertext, PingPongMessage,  # noqa: F401
+                       PlaintextInputShare, PrepareError, PrepareInit, PrepareResp, PrepareStepResult, ReportMetadata,
+                       ReportShare)
 
 
 @dataclass
@@ -207,4 +208,73 @@ def leader_process_helper_response(engine: HelperEngine, step: LeaderStep, prepa
                              PrepareStepResult(1) if results[i] is None else
                              PrepareStepResult(2, error=results[i]))
                  for k, i in enumerate(step.stepped)]
+    return AggregateInitOutcome(responses, finished, failures)
+
+
+# ----------------------------------------------------------------------------- HPKE + prepare
+
+
+def handle_aggregate_init_encrypted(engine: HelperEngine, opener, hpke_config_id: int, task_id: bytes,
+                                    prepare_inits: list[PrepareInit], segments: list[int] | None = None,
+                                    replayed: set[bytes] | None = None) -> AggregateInitOutcome:
+    """The helper's aggregate-init loop including the decryption of the report shares
+    (aggregator.rs:1763-1893): one batched HPKE open on the GPU (janus_amd.hpke.HpkeOpener) for
+    the whole request, then PlaintextInputShare decoding and extension checks on the host, then
+    handle_aggregate_init for the reports that survive. Failures map as in the reference:
+    unknown HPKE config id -> HpkeUnknownConfigId, HPKE failure -> HpkeDecryptError, plaintext
+    decode failure / duplicate or unexpected taskprov extension -> InvalidMessage."""
+    from .hpke import input_share_aad
+
+    n = len(prepare_inits)
+    failures: Counter = Counter()
+    errors: dict[int, PrepareError] = {}
+    to_open = []
+    for i, pi in enumerate(prepare_inits):
+        rs = pi.report_share
+        if rs.encrypted_input_share.config_id != hpke_config_id:
+            errors[i] = PrepareError.HpkeUnknownConfigId
+            failures["unknown_hpke_config_id"] += 1
+        else:
+            to_open.append(i)
+    opened = opener.open_batch(
+        [prepare_inits[i].report_share.encrypted_input_share.encapsulated_key for i in to_open],
+        [prepare_inits[i].report_share.encrypted_input_share.payload for i in to_open],
+        [input_share_aad(task_id, prepare_inits[i].report_share.metadata.report_id,
+                         prepare_inits[i].report_share.metadata.time, prepare_inits[i].report_share.public_share)
+         for i in to_open]) if to_open else []
+    payloads: dict[int, bytes] = {}
+    for i, pt in zip(to_open, opened):
+        if pt is None:
+            errors[i] = PrepareError.HpkeDecryptError
+            failures["decrypt_failure"] += 1
+            continue
+        try:
+            pis = PlaintextInputShare.decode(pt)
+        except CodecError:
+            errors[i] = PrepareError.InvalidMessage
+            failures["plaintext_input_share_decode_failure"] += 1
+            continue
+        types = [e.extension_type for e in pis.extensions]
+        if len(set(types)) != len(types):
+            errors[i] = PrepareError.InvalidMessage
+            failures["duplicate_extension"] += 1
+            continue
+        if EXTENSION_TASKPROV in types:  # taskprov is not enabled for these tasks
+            errors[i] = PrepareError.InvalidMessage
+            failures["unexpected_taskprov_extension"] += 1
+            continue
+        payloads[i] = pis.payload
+    keep = [i for i in range(n) if i in payloads]
+    inner = handle_aggregate_init(engine, [prepare_inits[i] for i in keep], [payloads[i] for i in keep],
+                                  [segments[i] for i in keep] if segments else None, replayed)
+    failures.update(inner.step_failures)
+    by_row = dict(zip(keep, range(len(keep))))
+    finished = np.zeros(n, bool)
+    responses = []
+    for i, pi in enumerate(prepare_inits):
+        if i in errors:
+            responses.append(PrepareResp(pi.report_share.metadata.report_id, PrepareStepResult(2, error=errors[i])))
+        else:
+            responses.append(inner.responses[by_row[i]])
+            finished[i] = inner.finished[by_row[i]]
     return AggregateInitOutcome(responses, finished, failures)

@@ -213,3 +213,44 @@ class PrepareResp:
             raise CodecError("unexpected PrepareStepResult")
         r.done()
         return cls(rid, res)
+
+
+# ----------------------------------------------------------------------------- PlaintextInputShare
+
+EXTENSION_TBD, EXTENSION_TASKPROV = 0x0000, 0xFF00  # messages/src/lib.rs:924-927
+
+
+@dataclass(frozen=True)
+class Extension:
+    extension_type: int
+    extension_data: bytes = b""
+
+    def encode(self) -> bytes:
+        return struct.pack(">H", self.extension_type) + _o16(self.extension_data)
+
+
+@dataclass(frozen=True)
+class PlaintextInputShare:
+    """extensions (u16-length-prefixed list) || payload (u32-length-prefixed), the HPKE plaintext
+    of a report share (messages/src/lib.rs:1323-1326)."""
+
+    extensions: tuple = ()
+    payload: bytes = b""
+
+    def encode(self) -> bytes:
+        ext = b"".join(e.encode() for e in self.extensions)
+        return _o16(ext) + _o32(self.payload)
+
+    @classmethod
+    def decode(cls, b: bytes) -> "PlaintextInputShare":
+        r = _Reader(b)
+        er = _Reader(r.opaque16())
+        exts = []
+        while er.i < len(er.b):
+            t = er.u16()
+            if t not in (EXTENSION_TBD, EXTENSION_TASKPROV):
+                raise CodecError("unknown extension type")
+            exts.append(Extension(t, er.opaque16()))
+        payload = r.opaque32()
+        r.done()
+        return cls(tuple(exts), payload)

@@ -46,3 +46,19 @@ def test_finish_message_shape():
     m = PingPongMessage.finish(bytes(range(16)))
     assert m.encode() == b"\x02" + (16).to_bytes(4, "big") + bytes(range(16))
     assert PingPongMessage.decode(m.encode()) == m
+
+
+def test_plaintext_input_share_codec():
+    import pytest
+
+    from janus_amd.messages import (EXTENSION_TASKPROV, EXTENSION_TBD, CodecError, Extension,
+                                    PlaintextInputShare)
+    p = PlaintextInputShare((Extension(EXTENSION_TBD, b"ab"), Extension(EXTENSION_TASKPROV)), b"\x01" * 48)
+    enc = p.encode()
+    assert enc[:2] == (4 + 2 + 4).to_bytes(2, "big")
+    assert PlaintextInputShare.decode(enc) == p
+    assert PlaintextInputShare.decode(PlaintextInputShare((), b"xyz").encode()).payload == b"xyz"
+    with pytest.raises(CodecError):
+        PlaintextInputShare.decode(enc + b"\x00")  # trailing bytes
+    with pytest.raises(CodecError):  # unknown extension type
+        PlaintextInputShare.decode((6).to_bytes(2, "big") + b"\x12\x34\x00\x00\x00\x00" + (0).to_bytes(4, "big"))
