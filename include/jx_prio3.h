@@ -58,7 +58,15 @@ extern "C" {
 /* Prio3 instance, mirroring janus_core::vdaf::VdafInstance (core/src/vdaf.rs:65-108).
  * algo_id: 0 Prio3Count, 1 Prio3Sum{bits}, 2 Prio3SumVec{bits,length,chunk_length},
  *          3 Prio3Histogram{length,chunk_length}  (== Prio3 algorithm ids, messages/src/taskprov.rs:358-363)
- * num_proofs must be 1 (all TurboSHAKE Prio3 variants Janus dispatches, core/src/vdaf.rs:203-262). */
+ *          4 Prio3SumVecField64MultiproofHmacSha256Aes128{proofs,bits,length,chunk_length}
+ *            (core/src/vdaf.rs:173-199: Field64, XofHmacSha256Aes128, 32-byte seeds and verify key;
+ *            DST algorithm id 0xFFFF1003; prep messages and joint-rand parts are 32 bytes)
+ * num_proofs: 1 for ids 0-3 (the TurboSHAKE variants, core/src/vdaf.rs:203-262); 2..8 for id 4. */
+#define JX_ALGO_COUNT 0
+#define JX_ALGO_SUM 1
+#define JX_ALGO_SUMVEC 2
+#define JX_ALGO_HISTOGRAM 3
+#define JX_ALGO_SUMVEC_F64_MULTIPROOF_HMACSHA256_AES128 4
 typedef struct {
   uint32_t algo_id;
   uint32_t bits;
@@ -73,6 +81,10 @@ typedef struct jx_engine jx_engine;
  * core/src/vdaf.rs:16) on HIP device `device`. */
 int32_t jx_engine_create(const jx_prio3_params* params, const uint8_t verify_key[16], int32_t device,
                          jx_engine** out);
+/* Same with an explicit verify key length: 16 (VERIFY_KEY_LENGTH) or, for algo_id 4, 32
+ * (VERIFY_KEY_LENGTH_HMACSHA256_AES128, core/src/vdaf.rs:24). */
+int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify_key, uint32_t verify_key_len,
+                            int32_t device, jx_engine** out);
 void jx_engine_destroy(jx_engine* e);
 
 /* Encoded sizes (bytes) for this instance. Any pointer may be NULL. */

@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libjanus_prio3.so")
 
 # Every symbol include/jx_prio3.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
-    "jx_engine_create", "jx_engine_destroy", "jx_engine_sizes", "jx_engine_set_capacity",
+    "jx_engine_create", "jx_engine_create_ex", "jx_engine_destroy", "jx_engine_sizes", "jx_engine_set_capacity",
     "jx_helper_prep_batch", "jx_engine_leader_sizes", "jx_leader_prep_init_batch", "jx_leader_prep_finish_batch",
     "jx_accumulate", "jx_helper_prep_aggregate", "jx_helper_prep_aggregate_device",
     "jx_aggregate_read", "jx_aggregate_checksum", "jx_aggregate_reset", "jx_aggregate_export_device",
@@ -55,6 +55,7 @@ def load():
     P = ctypes.POINTER
     sig = {
         "jx_engine_create": (i32, [P(JxParams), u8p, i32, P(vp)]),
+        "jx_engine_create_ex": (i32, [P(JxParams), u8p, u32, i32, P(vp)]),
         "jx_engine_destroy": (None, [vp]),
         "jx_engine_sizes": (i32, [vp, P(u32), P(u32), P(u32), P(u32), P(u32), P(u32)]),
         "jx_engine_set_capacity": (i32, [vp, u64]),

@@ -9,9 +9,9 @@ import subprocess
 import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-SOURCES = [os.path.join(_HERE, "csrc", f) for f in ("jx_kernels.hip", "jx_engine.cpp", "jx_hpke.hip")]
+SOURCES = [os.path.join(_HERE, "csrc", f) for f in ("jx_kernels.hip", "jx_engine.cpp", "jx_hpke.hip", "jx_mp64.hip")]
 HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("jx_field.h", "jx_keccak.h", "jx_sha256.h", "jx_kernels.h",
-                                                  "jx_hpke.h")]
+                                                  "jx_hpke.h", "jx_sha_aes.h")]
 OUT = os.path.join(_HERE, "lib", "libjanus_prio3.so")
 ARCH = os.environ.get("JX_OFFLOAD_ARCH", "gfx950")
 
@@ -30,7 +30,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     objs = []
-    # compile the two translation units in parallel
+    # compile the translation units in parallel
     procs = []
     for src in SOURCES:
         obj = os.path.join(os.path.dirname(OUT), os.path.basename(src) + ".o")

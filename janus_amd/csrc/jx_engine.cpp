@@ -18,6 +18,7 @@
 #include "../../include/jx_prio3.h"
 #include "jx_field.h"
 #include "jx_kernels.h"
+#include "jx_sha_aes.h"
 
 using namespace jx;
 
@@ -133,13 +134,30 @@ int psum_ppw(uint32_t chunk);
 
 // ---------------------------------------------------------------------------- configuration
 
-static int32_t make_cfg(const jx_prio3_params* p, const uint8_t vk[16], Cfg& c, std::string& why) {
+// HMAC-SHA256 states after the key block for a 32-byte key (little-endian memory words)
+static void host_hmac_pads(const uint8_t key[32], uint32_t ist[8], uint32_t ost[8]) {
+  uint32_t kbe[8];
+  for (int i = 0; i < 8; i++)
+    kbe[i] = ((uint32_t)key[4 * i] << 24) | ((uint32_t)key[4 * i + 1] << 16) | ((uint32_t)key[4 * i + 2] << 8) |
+             key[4 * i + 3];
+  hmac_pads(kbe, ist, ost);
+}
+
+static int32_t make_cfg(const jx_prio3_params* p, const uint8_t* vk, uint32_t vk_len, Cfg& c, std::string& why) {
   memset(&c, 0, sizeof c);
-  if (p->num_proofs != 1) {
-    why = "num_proofs must be 1";
+  const bool mp = p->algo_id == ALGO_SUMVEC_F64_MULTIPROOF;
+  if (mp ? (p->num_proofs < 2 || p->num_proofs > MP_MAX_PROOFS) : p->num_proofs != 1) {
+    why = mp ? "num_proofs must be in [2, 8]" : "num_proofs must be 1";
     return JX_E_UNSUPPORTED;
   }
+  if (vk_len != (mp ? 32u : 16u)) {
+    why = "verify key length must be 16 (32 for Prio3SumVecField64MultiproofHmacSha256Aes128)";
+    return JX_E_INVALID;
+  }
   c.algo = p->algo_id;
+  c.np = p->num_proofs;
+  c.seed = mp ? 32 : 16;
+  c.dst_id = mp ? 0xFFFF1003u : p->algo_id;  // core/src/vdaf.rs:18-20
   c.bits = p->bits;
   c.length = p->length;
   c.chunk = p->chunk_length;
@@ -164,6 +182,7 @@ static int32_t make_cfg(const jx_prio3_params* p, const uint8_t vk[16], Cfg& c, 
       arity = 1;
       break;
     case ALGO_SUMVEC:
+    case ALGO_SUMVEC_F64_MULTIPROOF:
       if (p->bits < 1 || p->bits > 32 || p->length < 1 || p->chunk_length < 1) {
         why = "Prio3SumVec needs 1 <= bits <= 32, length >= 1, chunk_length >= 1";
         return JX_E_UNSUPPORTED;
@@ -190,22 +209,34 @@ static int32_t make_cfg(const jx_prio3_params* p, const uint8_t vk[16], Cfg& c, 
       why = "unknown algo_id";
       return JX_E_INVALID;
   }
-  if (c.algo == ALGO_SUMVEC || c.algo == ALGO_HISTOGRAM) {
+  if (c.algo == ALGO_SUMVEC || c.algo == ALGO_HISTOGRAM || mp) {
     c.ppw = psum_ppw(c.chunk);
     c.ngroups = (c.chunk + c.ppw - 1) / c.ppw;
   }
   c.P = next_pow2(1 + c.calls);
+  if (mp && c.P > (1u << 30)) {
+    why = "too many gadget calls for Field64";
+    return JX_E_UNSUPPORTED;
+  }
   c.logP = ilog2(c.P);
   c.gpoly_len = 2 * (c.P - 1) + 1;
   c.proof_len = arity + c.gpoly_len;
   c.ver_len = arity + 2;
-  const uint32_t fb = c.algo == ALGO_COUNT ? 8 : 16;
+  const uint32_t fb = (c.algo == ALGO_COUNT || mp) ? 8 : 16;
+  c.fb = fb;
   const bool jr = c.jr_len > 0;
-  c.ps_bytes = jr ? 32 : 0;
-  c.his_bytes = jr ? 48 : 32;
-  c.lps_bytes = c.ver_len * fb + (jr ? 16 : 0);
-  c.lis_bytes = (c.meas_len + c.proof_len) * fb + (jr ? 16 : 0);
-  if (c.algo == ALGO_COUNT)
+  const uint32_t S = c.seed;
+  c.ps_bytes = jr ? 2 * S : 0;
+  c.his_bytes = jr ? 3 * S : 2 * S;
+  c.lps_bytes = c.np * c.ver_len * fb + (jr ? S : 0);
+  c.lis_bytes = (c.meas_len + c.np * c.proof_len) * fb + (jr ? S : 0);
+  if (mp) {
+    c.nco = MCOEF_K + 2 * c.calls;
+    c.ncoef = 0;
+    host_hmac_pads(vk, c.vk_ist, c.vk_ost);
+    const uint8_t zero[32] = {0};
+    host_hmac_pads(zero, c.zero_ist, c.zero_ost);
+  } else if (c.algo == ALGO_COUNT)
     c.ncoef = 0;
   else if (c.algo == ALGO_SUM)
     c.ncoef = COEF_K + c.calls;
@@ -221,9 +252,36 @@ static int32_t make_cfg(const jx_prio3_params* p, const uint8_t vk[16], Cfg& c, 
 }
 
 // constant tables: w^k R (k < P), S_m R = (sum_{k=1..calls} w^{km}) R (m < gpoly_len), misc
+static uint4 h_u4_64(uint64_t v) {
+  uint4 r;
+  r.x = lo32(v);
+  r.y = hi32(v);
+  r.z = r.w = 0;
+  return r;
+}
+
 static std::vector<uint4> make_consts(const Cfg& c) {
   std::vector<uint4> t(c.P + c.gpoly_len + 4);
   if (c.algo == ALGO_COUNT) return t;
+  if (c.algo == ALGO_SUMVEC_F64_MULTIPROOF) {
+    // Field64: GEN = 7^((p-1)/2^32) (order 2^32), w = GEN^(2^(32 - logP)); canonical values
+    uint64_t w = pow64_h(pow64_h(7, (P64 - 1) >> 32), 1ull << (32 - c.logP));
+    std::vector<uint64_t> pw(c.P);
+    uint64_t wk = 1;
+    for (uint32_t k = 0; k < c.P; k++) {
+      pw[k] = wk;
+      t[c.c_omega + k] = h_u4_64(wk);
+      wk = mul64(wk, w);
+    }
+    for (uint32_t m = 0; m < c.gpoly_len; m++) {
+      uint64_t s = 0;
+      for (uint32_t k = 1; k <= c.calls; k++) s = add64(s, pw[(uint64_t)(k * m) % c.P]);
+      t[c.c_S + m] = h_u4_64(s);
+    }
+    t[c.c_misc + 0] = h_u4_64(pow64_h(c.P, P64 - 2));  // 1/P
+    t[c.c_misc + 1] = h_u4_64(pow64_h(2, P64 - 2));    // 1/2
+    return t;
+  }
   // GEN = 7^((p-1)/2^66), order 2^66; w = GEN^(2^(66 - logP))
   f128 gen = h_mpow(to_mont128(h_from_u64(7)), 4611686018427387897ull);
   f128 w = gen;
@@ -274,10 +332,18 @@ static void free_staging(jx_engine* e) {
   e->leader_cap = 0;
 }
 
+// staging element bytes: the multiproof Field64 kernels use 8-byte elements (outputs stay uint4)
+static uint32_t stage_eb(const Cfg& c) { return c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? 8u : 16u; }
+static uint64_t coef_elems(const Cfg& c) { return c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? (uint64_t)c.np * c.nco : c.ncoef; }
+static uint64_t part_bytes(const Cfg& c) {
+  return c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? 24ull * c.np * c.ngroups : 64ull * c.ngroups;
+}
+
 static uint64_t per_report_bytes(const Cfg& c) {
-  uint64_t b = 16ull * (c.meas_len + c.proof_len + c.ncoef + (c.out_is_meas ? 0 : c.out_len));
-  b += 16 + c.ps_bytes + c.his_bytes + c.lps_bytes + 4 + 1 + 16 + 1 + 4 + 1;
-  b += 64ull * c.ngroups;  // FLP partial sums
+  uint64_t b = (uint64_t)stage_eb(c) * (c.meas_len + (uint64_t)c.np * c.proof_len + coef_elems(c));
+  b += 16ull * (c.out_is_meas ? 0 : c.out_len);
+  b += 16 + c.ps_bytes + c.his_bytes + c.lps_bytes + 4 + 1 + c.seed + 1 + 4 + 1;
+  b += part_bytes(c);  // FLP partial sums
   return b;
 }
 
@@ -291,14 +357,15 @@ static int32_t ensure_capacity(jx_engine* e, uint64_t n) {
   HIPCHK(e, A((void**)&e->d_ps, cap * c.ps_bytes));
   HIPCHK(e, A((void**)&e->d_his, cap * c.his_bytes));
   HIPCHK(e, A((void**)&e->d_lps, cap * c.lps_bytes));
-  HIPCHK(e, A((void**)&e->d_meas, cap * c.meas_len * 16));
-  HIPCHK(e, A((void**)&e->d_proof, cap * c.proof_len * 16));
+  const uint64_t eb = stage_eb(c);
+  HIPCHK(e, A((void**)&e->d_meas, cap * c.meas_len * eb));
+  HIPCHK(e, A((void**)&e->d_proof, cap * c.np * c.proof_len * eb));
   if (c.algo == ALGO_COUNT || !c.out_is_meas) HIPCHK(e, A((void**)&e->d_outs, cap * c.out_len * 16));
-  HIPCHK(e, A((void**)&e->d_coef, cap * c.ncoef * 16));
+  HIPCHK(e, A((void**)&e->d_coef, cap * coef_elems(c) * eb));
   HIPCHK(e, A((void**)&e->d_flags, cap * 4));
-  HIPCHK(e, A((void**)&e->d_part, cap * 64ull * c.ngroups));
+  HIPCHK(e, A((void**)&e->d_part, cap * part_bytes(c)));
   HIPCHK(e, A((void**)&e->d_verdicts, cap));
-  HIPCHK(e, A((void**)&e->d_msgs, cap * 16));
+  HIPCHK(e, A((void**)&e->d_msgs, cap * c.seed));
   HIPCHK(e, A((void**)&e->d_mask, cap));
   HIPCHK(e, A((void**)&e->d_seg, cap * 4));
   size_t pbytes = (size_t)e->acc_chunks * c.out_len * 3 * sizeof(uint64_t) + cap;
@@ -407,6 +474,18 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
     HIPCHK(e, stage_begin(e, &ev));
     HIPCHK(e, launch_count(c, b, e->stream));
     HIPCHK(e, stage_end(e, ST_XOF, ev));
+  } else if (c.algo == ALGO_SUMVEC_F64_MULTIPROOF) {
+    HIPCHK(e, stage_begin(e, &ev));
+    HIPCHK(e, launch_mp_xof(c, b, e->stream));
+    HIPCHK(e, stage_end(e, ST_XOF, ev));
+    if (!leader) {
+      HIPCHK(e, stage_begin(e, &ev));
+      HIPCHK(e, launch_mp_slow(c, b, e->stream));
+      HIPCHK(e, stage_end(e, ST_SLOW, ev));
+    }
+    HIPCHK(e, stage_begin(e, &ev));
+    HIPCHK(e, launch_mp_flp(c, b, e->stream));
+    HIPCHK(e, stage_end(e, ST_FLP, ev));
   } else {
     HIPCHK(e, stage_begin(e, &ev));
     HIPCHK(e, launch_xof(c, b, e->stream));
@@ -437,7 +516,7 @@ static int32_t ensure_leader_capacity(jx_engine* e, uint64_t n) {
   const uint64_t cap = e->cap;
   HIPCHK(e, hipMalloc((void**)&e->d_lis, cap * c.lis_bytes));
   HIPCHK(e, hipMalloc((void**)&e->d_lps_out, cap * c.lps_bytes));
-  HIPCHK(e, hipMalloc((void**)&e->d_in_msgs, cap * 16));
+  HIPCHK(e, hipMalloc((void**)&e->d_in_msgs, cap * c.seed));
   e->leader_cap = cap;
   return JX_OK;
 }
@@ -477,6 +556,11 @@ extern "C" {
 
 int32_t jx_engine_create(const jx_prio3_params* params, const uint8_t verify_key[16], int32_t device,
                          jx_engine** out) {
+  return jx_engine_create_ex(params, verify_key, 16, device, out);
+}
+
+int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify_key, uint32_t verify_key_len,
+                            int32_t device, jx_engine** out) {
   if (!params || !verify_key || !out) return JX_E_INVALID;
   *out = nullptr;
   int ndev = 0;
@@ -484,7 +568,7 @@ int32_t jx_engine_create(const jx_prio3_params* params, const uint8_t verify_key
   if (device < 0 || device >= ndev) return JX_E_INVALID;
   jx_engine* e = new jx_engine();
   std::string why;
-  int32_t rc = make_cfg(params, verify_key, e->cfg, why);
+  int32_t rc = make_cfg(params, verify_key, verify_key_len, e->cfg, why);
   if (rc) {
     delete e;
     return rc;
@@ -545,9 +629,9 @@ int32_t jx_engine_sizes(const jx_engine* e, uint32_t* ps, uint32_t* his, uint32_
   if (ps) *ps = c.ps_bytes;
   if (his) *his = c.his_bytes;
   if (lps) *lps = c.lps_bytes;
-  if (pm) *pm = c.jr_len ? 16 : 0;
+  if (pm) *pm = c.jr_len ? c.seed : 0;
   if (out_len) *out_len = c.out_len;
-  if (fb) *fb = c.algo == ALGO_COUNT ? 8 : 16;
+  if (fb) *fb = c.fb;
   return JX_OK;
 }
 
@@ -579,9 +663,9 @@ int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, co
   if (rc) return rc;
   HIPCHK(e, hipMemcpyAsync(out_verdicts, e->d_verdicts, n, hipMemcpyDeviceToHost, e->stream));
   if (out_prep_msgs && c.jr_len)
-    HIPCHK(e, hipMemcpyAsync(out_prep_msgs, e->d_msgs, n * 16, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(out_prep_msgs, e->d_msgs, n * c.seed, hipMemcpyDeviceToHost, e->stream));
   if (out_output_shares) {
-    const uint32_t fb = c.algo == ALGO_COUNT ? 8 : 16;
+    const uint32_t fb = c.fb;
     rc = ensure_tmp(e, n * c.out_len * fb);
     if (rc) return rc;
     const uint4* outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? e->d_meas : e->d_outs;
@@ -638,7 +722,7 @@ int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t n, const uint8_t* pre
   if (n == 0) return JX_OK;
   HIPCHK(e, hipSetDevice(e->device));
   if (c.jr_len) {
-    HIPCHK(e, hipMemcpyAsync(e->d_in_msgs, prep_msgs, n * 16, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->d_in_msgs, prep_msgs, n * c.seed, hipMemcpyHostToDevice, e->stream));
     Bufs b{};
     b.n = n;
     b.verdicts = e->d_verdicts;
@@ -647,7 +731,7 @@ int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t n, const uint8_t* pre
   }
   HIPCHK(e, hipMemcpyAsync(out_verdicts, e->d_verdicts, n, hipMemcpyDeviceToHost, e->stream));
   if (out_output_shares) {
-    const uint32_t fb = c.algo == ALGO_COUNT ? 8 : 16;
+    const uint32_t fb = c.fb;
     int32_t rc = ensure_tmp(e, n * c.out_len * fb);
     if (rc) return rc;
     const uint4* outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? e->d_meas : e->d_outs;
@@ -712,7 +796,7 @@ int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces
     if (out_verdicts)
       HIPCHK(e, hipMemcpyAsync(out_verdicts + off, e->d_verdicts, m, hipMemcpyDeviceToHost, e->stream));
     if (out_prep_msgs && c.jr_len)
-      HIPCHK(e, hipMemcpyAsync(out_prep_msgs + off * 16, e->d_msgs, m * 16, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipMemcpyAsync(out_prep_msgs + off * c.seed, e->d_msgs, m * c.seed, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
   }
   e->have_batch = false;  // staging no longer holds one whole batch
@@ -734,7 +818,7 @@ int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_
   for (uint64_t off = 0; off < n; off += chunk) {
     const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
     uint8_t* vout = d_out_verdicts ? (uint8_t*)d_out_verdicts + off : e->d_verdicts;
-    uint8_t* mout = (d_out_prep_msgs && c.jr_len) ? (uint8_t*)d_out_prep_msgs + off * 16 : e->d_msgs;
+    uint8_t* mout = (d_out_prep_msgs && c.jr_len) ? (uint8_t*)d_out_prep_msgs + off * c.seed : e->d_msgs;
     rc = prep_core(e, m, N + off * 16, PS ? PS + off * c.ps_bytes : nullptr, H + off * c.his_bytes,
                    L + off * c.lps_bytes, vout, mout);
     if (rc) return rc;
@@ -749,7 +833,7 @@ int32_t jx_aggregate_read(jx_engine* e, uint32_t segment, uint8_t* out_agg, uint
   if (!e) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
   const Cfg& c = e->cfg;
-  const uint32_t fb = c.algo == ALGO_COUNT ? 8 : 16;
+  const uint32_t fb = c.fb;
   Segment* s = nullptr;
   int32_t rc = get_segment(e, segment, &s);
   if (rc) return rc;
@@ -823,7 +907,7 @@ int32_t jx_shard_record_combine_device(jx_engine* e, const void* d_records, uint
 
 int32_t jx_shard_record_bytes(const jx_engine* e, uint32_t* bytes) {
   if (!e || !bytes) return JX_E_INVALID;
-  *bytes = e->cfg.out_len * (e->cfg.algo == ALGO_COUNT ? 8u : 16u) + 40u;
+  *bytes = e->cfg.out_len * e->cfg.fb + 40u;
   return JX_OK;
 }
 

@@ -343,4 +343,71 @@ JX_HD uint64_t mul64(uint64_t a, uint64_t b) {
   return r;
 }
 
+
+// 192-bit value w0 + w1 2^64 + w2 2^128 mod p64 (2^64 == 2^32 - 1, 2^128 == -2^32)
+JX_HD uint64_t reduce192_p64(uint64_t w0, uint64_t w1, uint64_t w2) {
+  const uint64_t a = w0 >= P64 ? w0 - P64 : w0;
+  const uint64_t b = w1 >= P64 ? w1 - P64 : w1;
+  const uint64_t d = w2 >= P64 ? w2 - P64 : w2;
+  return add64(add64(a, mul64(b, 0xFFFFFFFFull)), mul64(d, P64 - 0x100000000ull));
+}
+
+// Field64 wire sums without per-product reduction (the multiproof SumVec FLP): x < 2^64 as two
+// 32-bit limbs, the coefficient c < 2^64 as 22/22/20-bit limbs; each of the six limb products
+// (< 2^54) goes into its own 64-bit column with one v_mad_u64_u32, exact for up to 1024 products
+// per column; column weights 2^0, 2^22, 2^44 (x0) and 2^32, 2^54, 2^76 (x1).
+struct c64limbs {
+  uint32_t l0, l1, l2;
+};
+JX_HD c64limbs to_c64limbs(uint64_t c) {
+  c64limbs r;
+  r.l0 = (uint32_t)c & 0x3FFFFFu;
+  r.l1 = (uint32_t)(c >> 22) & 0x3FFFFFu;
+  r.l2 = (uint32_t)(c >> 44);
+  return r;
+}
+struct wacc64 {
+  uint64_t w[6];
+};
+constexpr uint32_t WACC64_MAX_TERMS = 1024;
+JX_HD void wacc64_zero(wacc64& a) {
+#pragma unroll
+  for (int i = 0; i < 6; i++) a.w[i] = 0;
+}
+JX_HD void wacc64_mac(wacc64& a, uint64_t x, const c64limbs& c) {
+  const uint32_t x0 = lo32(x), x1 = hi32(x);
+  a.w[0] += (uint64_t)x0 * c.l0;
+  a.w[1] += (uint64_t)x0 * c.l1;
+  a.w[2] += (uint64_t)x0 * c.l2;
+  a.w[3] += (uint64_t)x1 * c.l0;
+  a.w[4] += (uint64_t)x1 * c.l1;
+  a.w[5] += (uint64_t)x1 * c.l2;
+}
+// the column sum as a canonical Field64 element
+JX_HD uint64_t wacc64_reduce(const wacc64& a) {
+  uint64_t w0 = 0, w1 = 0, w2 = 0;
+  auto add = [&](uint64_t lo, uint64_t hi, uint64_t top) {
+    uint32_t c = 0;
+    w0 = addc64(w0, lo, c);
+    w1 = addc64(w1, hi, c);
+    w2 += top + c;
+  };
+  add(a.w[0], 0, 0);
+  add(a.w[1] << 22, a.w[1] >> 42, 0);
+  add(a.w[2] << 44, a.w[2] >> 20, 0);
+  add(a.w[3] << 32, a.w[3] >> 32, 0);
+  add(a.w[4] << 54, a.w[4] >> 10, 0);
+  add(0, a.w[5] << 12, a.w[5] >> 52);
+  return reduce192_p64(w0, w1, w2);
+}
+JX_HD uint64_t pow64_h(uint64_t a, uint64_t e) {
+  uint64_t r = 1;
+  while (e) {
+    if (e & 1) r = mul64(r, a);
+    a = mul64(a, a);
+    e >>= 1;
+  }
+  return r;
+}
+
 }  // namespace jx

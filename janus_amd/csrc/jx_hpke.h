@@ -9,9 +9,9 @@
 //    the ladder's conditional swaps are wave-uniform branches.
 //  * SHA-256 / HMAC / HKDF over messages whose layout is fixed at compile time (every byte
 //    position is a constant after unrolling, so message buffers live in registers).
-//  * AES-128 with the S-box in LDS (device) and packed-byte MixColumns; GHASH bit-serial.
+//  * SHA-256 / HMAC and AES-128 come from jx_sha_aes.h; GHASH is bit-serial.
 #pragma once
-#include "jx_sha256.h"
+#include "jx_sha_aes.h"
 
 namespace jx {
 
@@ -232,177 +232,6 @@ JX_HD void x25519_ladder(uint32_t out[8], const uint32_t k[8], const uint32_t u[
   fe_invert(t, z2);
   fe_mul(x2, x2, t);
   fe_to_bytes(out, x2);
-}
-
-// ============================================================================ SHA-256 / HMAC
-
-// a message of up to 128 bytes following a 64-byte prefix already absorbed into the state
-// (HMAC's key block); bytes are written big-endian into 32 words at compile-time positions
-struct Msg128 {
-  uint32_t w[32];
-};
-JX_HD void m_zero(Msg128& m) {
-#pragma unroll
-  for (int i = 0; i < 32; i++) m.w[i] = 0;
-}
-JX_HD void m_byte(Msg128& m, int pos, uint32_t v) { m.w[pos >> 2] |= (v & 0xffu) << (24 - 8 * (pos & 3)); }
-JX_HD int m_str(Msg128& m, int pos, const char* s) {  // string literal (compile-time)
-  for (int i = 0; s[i]; i++) m_byte(m, pos++, (uint8_t)s[i]);
-  return pos;
-}
-// 32 bytes held as 8 little-endian memory words
-JX_HD int m_le32(Msg128& m, int pos, const uint32_t w[8]) {
-#pragma unroll
-  for (int i = 0; i < 32; i++) m_byte(m, pos + i, w[i >> 2] >> (8 * (i & 3)));
-  return pos + 32;
-}
-// 32 bytes held as 8 big-endian words (a SHA-256 digest)
-JX_HD int m_be32(Msg128& m, int pos, const uint32_t h[8]) {
-#pragma unroll
-  for (int i = 0; i < 32; i++) m_byte(m, pos + i, h[i >> 2] >> (24 - 8 * (i & 3)));
-  return pos + 32;
-}
-
-constexpr uint32_t SHA256_IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
-                                   0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-
-JX_HD void sha256_compress(uint32_t st[8], const uint32_t* blk) {  // 16 big-endian words
-  uint32_t w[16];
-#pragma unroll
-  for (int i = 0; i < 16; i++) w[i] = blk[i];
-  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll
-  for (int i = 0; i < 64; i++) {
-    uint32_t wi;
-    if (i < 16) {
-      wi = w[i];
-    } else {
-      uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      uint32_t s0 = ror32(w15, 7) ^ ror32(w15, 18) ^ (w15 >> 3);
-      uint32_t s1 = ror32(w2, 17) ^ ror32(w2, 19) ^ (w2 >> 10);
-      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-      w[i & 15] = wi;
-    }
-    uint32_t S1 = ror32(e, 6) ^ ror32(e, 11) ^ ror32(e, 25);
-    uint32_t ch = (e & f) ^ (~e & g);
-    uint32_t t1 = h + S1 + ch + SHA256_K[i] + wi;
-    uint32_t S0 = ror32(a, 2) ^ ror32(a, 13) ^ ror32(a, 22);
-    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
-    h = g;
-    g = f;
-    f = e;
-    e = d + t1;
-    d = c;
-    c = b;
-    b = a;
-    a = t1 + S0 + mj;
-  }
-  st[0] += a;
-  st[1] += b;
-  st[2] += c;
-  st[3] += d;
-  st[4] += e;
-  st[5] += f;
-  st[6] += g;
-  st[7] += h;
-}
-
-// finish a hash whose state st already absorbed one 64-byte block: message m of len bytes
-JX_HD void sha256_finish64(uint32_t out[8], const uint32_t st0[8], Msg128& m, int len) {
-  m_byte(m, len, 0x80);
-  const int nblk = (len + 9 + 63) / 64;  // 1 or 2
-  const uint64_t bits = 8ull * (64 + len);
-  m.w[nblk * 16 - 2] = (uint32_t)(bits >> 32);
-  m.w[nblk * 16 - 1] = (uint32_t)bits;
-#pragma unroll
-  for (int i = 0; i < 8; i++) out[i] = st0[i];
-  sha256_compress(out, m.w);
-  if (nblk == 2) sha256_compress(out, m.w + 16);
-}
-
-// HMAC-SHA256 key pads for a 32-byte key given as 8 big-endian words (RFC 2104)
-JX_HD void hmac_pads(const uint32_t key[8], uint32_t ist[8], uint32_t ost[8]) {
-  uint32_t bi[16], bo[16];
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const uint32_t k = i < 8 ? key[i] : 0u;
-    bi[i] = k ^ 0x36363636u;
-    bo[i] = k ^ 0x5c5c5c5cu;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    ist[i] = SHA256_IV[i];
-    ost[i] = SHA256_IV[i];
-  }
-  sha256_compress(ist, bi);
-  sha256_compress(ost, bo);
-}
-// HMAC outer hash over an inner digest
-JX_HD void hmac_outer(uint32_t out[8], const uint32_t ost[8], const uint32_t inner[8]) {
-  Msg128 m;
-  m_zero(m);
-  m_be32(m, 0, inner);
-  sha256_finish64(out, ost, m, 32);
-}
-
-// ============================================================================ AES-128 / GCM
-
-// round keys: 44 words, word = 4 bytes little-endian (byte 0 in bits 0..7)
-JX_HD uint32_t sub_word(const uint8_t* sbox, uint32_t w) {
-  return (uint32_t)sbox[w & 0xff] | ((uint32_t)sbox[(w >> 8) & 0xff] << 8) | ((uint32_t)sbox[(w >> 16) & 0xff] << 16) |
-         ((uint32_t)sbox[w >> 24] << 24);
-}
-JX_HD void aes128_expand_key(const uint8_t* sbox, const uint32_t key[4], uint32_t rk[44]) {
-#pragma unroll
-  for (int i = 0; i < 4; i++) rk[i] = key[i];
-  uint32_t rcon = 1;
-#pragma unroll
-  for (int i = 4; i < 44; i++) {
-    uint32_t t = rk[i - 1];
-    if (i % 4 == 0) {
-      t = sub_word(sbox, (t >> 8) | (t << 24)) ^ rcon;
-      rcon = (rcon << 1) ^ ((rcon >> 7) * 0x11bu);
-    }
-    rk[i] = rk[i - 4] ^ t;
-  }
-}
-JX_HD uint32_t xtime4(uint32_t x) { return ((x & 0x7f7f7f7fu) << 1) ^ (((x >> 7) & 0x01010101u) * 0x1bu); }
-// one 16-byte block as 4 little-endian column words
-JX_HD void aes128_encrypt(const uint8_t* sbox, const uint32_t rk[44], const uint32_t in[4], uint32_t out[4]) {
-  uint32_t s0 = in[0] ^ rk[0], s1 = in[1] ^ rk[1], s2 = in[2] ^ rk[2], s3 = in[3] ^ rk[3];
-#pragma unroll
-  for (int r = 1; r <= 10; r++) {
-    // SubBytes + ShiftRows: row i of column c comes from column (c + i) mod 4
-    uint32_t t0 = (uint32_t)sbox[s0 & 0xff] | ((uint32_t)sbox[(s1 >> 8) & 0xff] << 8) |
-                  ((uint32_t)sbox[(s2 >> 16) & 0xff] << 16) | ((uint32_t)sbox[s3 >> 24] << 24);
-    uint32_t t1 = (uint32_t)sbox[s1 & 0xff] | ((uint32_t)sbox[(s2 >> 8) & 0xff] << 8) |
-                  ((uint32_t)sbox[(s3 >> 16) & 0xff] << 16) | ((uint32_t)sbox[s0 >> 24] << 24);
-    uint32_t t2 = (uint32_t)sbox[s2 & 0xff] | ((uint32_t)sbox[(s3 >> 8) & 0xff] << 8) |
-                  ((uint32_t)sbox[(s0 >> 16) & 0xff] << 16) | ((uint32_t)sbox[s1 >> 24] << 24);
-    uint32_t t3 = (uint32_t)sbox[s3 & 0xff] | ((uint32_t)sbox[(s0 >> 8) & 0xff] << 8) |
-                  ((uint32_t)sbox[(s1 >> 16) & 0xff] << 16) | ((uint32_t)sbox[s2 >> 24] << 24);
-    if (r != 10) {  // MixColumns: b_i = 2(a_i ^ a_{i+1}) ^ a_{i+1} ^ a_{i+2} ^ a_{i+3}
-      uint32_t c[4] = {t0, t1, t2, t3};
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const uint32_t w = c[q];
-        const uint32_t r1 = (w >> 8) | (w << 24), r2 = (w >> 16) | (w << 16), r3 = (w >> 24) | (w << 8);
-        c[q] = xtime4(w ^ r1) ^ r1 ^ r2 ^ r3;
-      }
-      t0 = c[0];
-      t1 = c[1];
-      t2 = c[2];
-      t3 = c[3];
-    }
-    s0 = t0 ^ rk[4 * r];
-    s1 = t1 ^ rk[4 * r + 1];
-    s2 = t2 ^ rk[4 * r + 2];
-    s3 = t3 ^ rk[4 * r + 3];
-  }
-  out[0] = s0;
-  out[1] = s1;
-  out[2] = s2;
-  out[3] = s3;
 }
 
 // GF(2^128) multiply in GCM's bit order; operands as 4 big-endian words (x[0] = bytes 0..3)

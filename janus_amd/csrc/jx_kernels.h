@@ -6,7 +6,16 @@
 
 namespace jx {
 
-enum Algo : uint32_t { ALGO_COUNT = 0, ALGO_SUM = 1, ALGO_SUMVEC = 2, ALGO_HISTOGRAM = 3 };
+enum Algo : uint32_t {
+  ALGO_COUNT = 0,
+  ALGO_SUM = 1,
+  ALGO_SUMVEC = 2,
+  ALGO_HISTOGRAM = 3,
+  // Prio3SumVecField64MultiproofHmacSha256Aes128 (core/src/vdaf.rs:173-199): Field64, num_proofs
+  // >= 2, XofHmacSha256Aes128 with 32-byte seeds (kernels: jx_mp64.hip)
+  ALGO_SUMVEC_F64_MULTIPROOF = 4,
+};
+constexpr uint32_t MP_MAX_PROOFS = 8;  // num_proofs supported by the multiproof kernels
 
 // per-report flag bits written by the XOF stage, consumed by the FLP stage
 enum : uint32_t {
@@ -32,6 +41,14 @@ struct Cfg {
   uint32_t vk[4];
   // constant table offsets (uint4 units) in Bufs::consts
   uint32_t c_omega, c_S, c_misc;
+  uint32_t fb;      // field element bytes (8: Field64, 16: Field128)
+  uint32_t seed;    // XOF SEED_SIZE (16 TurboSHAKE128, 32 HmacSha256Aes128) = prep message bytes
+  uint32_t np;      // num_proofs
+  uint32_t dst_id;  // algorithm id in the XOF domain-separation tags
+  uint32_t nco;     // multiproof: coefficient slots per proof
+  // multiproof: HMAC-SHA256 inner/outer states after the key block, for the 32-byte verify key
+  // (query randomness) and the all-zero key (joint-rand seed derivations)
+  uint32_t vk_ist[8], vk_ost[8], zero_ist[8], zero_ost[8];
 };
 
 // coefficient slots (Montgomery form unless noted) for the ParallelSum / Sum FLP
@@ -59,7 +76,7 @@ struct Bufs {
   uint4* outs;
   uint4* coef;
   uint32_t* flags;
-  uint4* part;  // ParallelSum FLP partial sums [blk][group][4][lane]
+  uint4* part;  // ParallelSum FLP partial sums [blk][group][4][lane] (multiproof: uint2 [blk][proof][group][3][lane])
   uint8_t* verdicts;
   uint8_t* msgs;
   const uint4* consts;
@@ -82,6 +99,9 @@ struct AccArgs {
   unsigned long long* count;
 };
 
+// multiproof coefficient slots (canonical Field64), per proof
+enum : uint32_t { MCOEF_L = 0, MCOEF_C0 = 1, MCOEF_HALFSUM = 2, MCOEF_T = 3, MCOEF_R = 4, MCOEF_K = 5 };
+
 // launchers (jx_kernels.hip)
 hipError_t launch_count(const Cfg& c, const Bufs& b, hipStream_t s);
 hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s);
@@ -95,5 +115,9 @@ hipError_t launch_record_export(const Cfg& c, const uint4* agg, const unsigned l
 hipError_t launch_record_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, hipStream_t s);
 hipError_t launch_transpose_out(const Cfg& c, const uint4* outs, uint64_t n, uint8_t* dst, hipStream_t s);
 hipError_t launch_agg_encode(const Cfg& c, const uint4* agg, uint8_t* dst, hipStream_t s);
+// multiproof Field64 SumVec (jx_mp64.hip)
+hipError_t launch_mp_xof(const Cfg& c, const Bufs& b, hipStream_t s);
+hipError_t launch_mp_slow(const Cfg& c, const Bufs& b, hipStream_t s);
+hipError_t launch_mp_flp(const Cfg& c, const Bufs& b, hipStream_t s);
 
 }  // namespace jx

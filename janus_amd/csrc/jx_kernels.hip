@@ -1129,9 +1129,11 @@ __global__ __launch_bounds__(256) void leader_finish_kernel(Cfg c, Bufs b, const
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= b.n) return;
   if (b.verdicts[r] != 0 || c.jr_len == 0) return;
-  const uint4 m = *reinterpret_cast<const uint4*>(prep_msgs + 16 * r);
-  const uint4 k = *reinterpret_cast<const uint4*>(b.msgs + 16 * r);
-  if (m.x != k.x || m.y != k.y || m.z != k.z || m.w != k.w) b.verdicts[r] = 4;
+  for (uint32_t o = 0; o < c.seed; o += 16) {
+    const uint4 m = *reinterpret_cast<const uint4*>(prep_msgs + c.seed * r + o);
+    const uint4 k = *reinterpret_cast<const uint4*>(b.msgs + c.seed * r + o);
+    if (m.x != k.x || m.y != k.y || m.z != k.z || m.w != k.w) b.verdicts[r] = 4;
+  }
 }
 
 // ---------------------------------------------------------------------------- K4: accumulate
@@ -1195,14 +1197,6 @@ __global__ __launch_bounds__(256) void accumulate_kernel(AccArgs a, const uint8_
   }
 }
 
-__device__ uint64_t reduce192_p64(uint64_t w0, uint64_t w1, uint64_t w2) {
-  const uint64_t c64 = 0xFFFFFFFFull;  // 2^64 mod p
-  const uint64_t c128 = mul64(c64, c64);
-  uint64_t a = w0 >= P64 ? w0 - P64 : w0;
-  uint64_t b = w1 >= P64 ? w1 - P64 : w1;
-  uint64_t d = w2 >= P64 ? w2 - P64 : w2;
-  return add64(add64(a, mul64(b, c64)), mul64(d, c128));
-}
 
 __global__ void reduce_partials_kernel(Cfg c, const uint64_t* partials, uint32_t nchunks, uint4* agg) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1217,7 +1211,7 @@ __global__ void reduce_partials_kernel(Cfg c, const uint64_t* partials, uint32_t
     acc.w2 = acc.w2 + p[2] + cc;
   }
   acc_add128(acc, u4_to_f(agg[i]));
-  if (c.algo == ALGO_COUNT) {
+  if (c.fb == 8) {
     uint64_t v = reduce192_p64(acc.w0, acc.w1, acc.w2);
     agg[i] = make_uint4(lo32(v), hi32(v), 0, 0);
   } else {
@@ -1229,7 +1223,7 @@ __global__ void reduce_partials_kernel(Cfg c, const uint64_t* partials, uint32_t
 __global__ void combine_kernel(Cfg c, const uint8_t* parts, uint32_t nparts, uint8_t* out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= c.out_len) return;
-  const uint32_t fb = c.algo == ALGO_COUNT ? 8 : 16;
+  const uint32_t fb = c.fb;
   const uint64_t stride = (uint64_t)c.out_len * fb;
   if (fb == 8) {
     uint64_t s = 0;
@@ -1259,7 +1253,7 @@ __global__ void combine_kernel(Cfg c, const uint8_t* parts, uint32_t nparts, uin
 __global__ void record_export_kernel(Cfg c, const uint4* agg, const unsigned long long* count,
                                      const uint32_t* checksum, uint8_t* dst) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t fb = c.algo == ALGO_COUNT ? 8 : 16;
+  const uint32_t fb = c.fb;
   if (i < c.out_len) {
     uint4 v = agg[i];
     for (uint32_t k = 0; k < fb; k++) {
@@ -1278,7 +1272,7 @@ __global__ void record_export_kernel(Cfg c, const uint4* agg, const unsigned lon
 // mod-p sum of the aggregate shares, sum of the counts, XOR of the checksums.
 __global__ void record_combine_kernel(Cfg c, const uint8_t* parts, uint32_t nparts, uint8_t* out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t fb = c.algo == ALGO_COUNT ? 8 : 16;
+  const uint32_t fb = c.fb;
   const uint64_t stride = (uint64_t)c.out_len * fb + 40;
   if (i < c.out_len) {
     if (fb == 8) {
@@ -1328,7 +1322,7 @@ __global__ void transpose_out_kernel(Cfg c, const uint4* outs, uint64_t n, uint8
   const uint32_t i = t % c.out_len;
   if (r >= n) return;
   uint4 v = outs[il_idx(r / 64, c.out_len, i, r % 64)];
-  if (c.algo == ALGO_COUNT) {
+  if (c.fb == 8) {
     *reinterpret_cast<uint2*>(dst + t * 8) = make_uint2(v.x, v.y);
   } else {
     *reinterpret_cast<uint4*>(dst + t * 16) = v;
@@ -1339,7 +1333,7 @@ __global__ void agg_encode_kernel(Cfg c, const uint4* agg, uint8_t* dst) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= c.out_len) return;
   uint4 v = agg[i];
-  if (c.algo == ALGO_COUNT)
+  if (c.fb == 8)
     *reinterpret_cast<uint2*>(dst + (uint64_t)i * 8) = make_uint2(v.x, v.y);
   else
     *reinterpret_cast<uint4*>(dst + (uint64_t)i * 16) = v;

@@ -82,16 +82,18 @@ class HelperEngine:
     _leader_n = 0
 
     def __init__(self, vdaf: Prio3, verify_key: bytes, device: int = 0):
-        if len(verify_key) != 16:
-            raise ValueError("verify key must be 16 bytes (VERIFY_KEY_LENGTH)")
+        if len(verify_key) != vdaf.verify_key_len:
+            raise ValueError(f"verify key must be {vdaf.verify_key_len} bytes for {vdaf.name()} "
+                             "(VERIFY_KEY_LENGTH / VERIFY_KEY_LENGTH_HMACSHA256_AES128, core/src/vdaf.rs:16,24)")
         self.vdaf = vdaf
         self.device = device
         L = _lib.load()
         self._L = L
         p = JxParams(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length, vdaf.num_proofs)
         h = ctypes.c_void_p()
-        vk = (ctypes.c_uint8 * 16).from_buffer_copy(verify_key)
-        st = L.jx_engine_create(ctypes.byref(p), ctypes.cast(vk, ctypes.c_void_p), device, ctypes.byref(h))
+        vk = (ctypes.c_uint8 * len(verify_key)).from_buffer_copy(verify_key)
+        st = L.jx_engine_create_ex(ctypes.byref(p), ctypes.cast(vk, ctypes.c_void_p), len(verify_key), device,
+                                   ctypes.byref(h))
         check(st, None, f"jx_engine_create({vdaf.name()})")
         self._h = h
         sizes = [ctypes.c_uint32() for _ in range(6)]
@@ -194,7 +196,7 @@ class HelperEngine:
         his = _u8(helper_input_shares, n, self.helper_input_share_len, "helper_input_shares")
         lps = _u8(leader_prep_shares, n, self.prep_share_len, "leader_prep_shares")
         verdicts = np.zeros(max(n, 1), np.uint8) if want_results else None
-        msgs = np.zeros((max(n, 1), 16), np.uint8) if (want_results and self.prep_msg_len) else None
+        msgs = np.zeros((max(n, 1), self.prep_msg_len), np.uint8) if (want_results and self.prep_msg_len) else None
         st = self._L.jx_helper_prep_aggregate(self._h, n, _ptr(nn), _ptr(ps) if self.public_share_len else None,
                                               _ptr(his), _ptr(lps), segment, _ptr(msgs), _ptr(verdicts))
         check(st, self._h, "jx_helper_prep_aggregate")

@@ -10,9 +10,13 @@ from __future__ import annotations
 from dataclasses import dataclass
 
 VERIFY_KEY_LENGTH = 16  # core/src/vdaf.rs:16
+VERIFY_KEY_LENGTH_HMACSHA256_AES128 = 32  # core/src/vdaf.rs:24
 
-# Prio3 algorithm ids (== taskprov VDAF type codes, messages/src/taskprov.rs:358-363)
+# Prio3 algorithm ids (== taskprov VDAF type codes, messages/src/taskprov.rs:358-363), plus the
+# engine's id for Prio3SumVecField64MultiproofHmacSha256Aes128 (core/src/vdaf.rs:173-199, whose
+# private-use DST algorithm id is 0xFFFF1003)
 PRIO3_COUNT, PRIO3_SUM, PRIO3_SUMVEC, PRIO3_HISTOGRAM = 0, 1, 2, 3
+PRIO3_SUMVEC_F64_MULTIPROOF = 4
 
 
 def _next_pow2(v: int) -> int:
@@ -24,7 +28,8 @@ def _next_pow2(v: int) -> int:
 
 @dataclass(frozen=True)
 class Prio3:
-    """One Prio3 instance (2 aggregators, 1 proof, XofTurboShake128)."""
+    """One Prio3 instance (2 aggregators). XofTurboShake128 and one proof, except
+    Prio3SumVecField64MultiproofHmacSha256Aes128 (Field64, num_proofs >= 2, XofHmacSha256Aes128)."""
 
     algo_id: int
     bits: int = 0
@@ -49,14 +54,33 @@ class Prio3:
     def histogram(length: int, chunk_length: int) -> "Prio3":
         return Prio3(PRIO3_HISTOGRAM, length=length, chunk_length=chunk_length)
 
+    @staticmethod
+    def sum_vec_field64_multiproof_hmacsha256_aes128(proofs: int, bits: int, length: int,
+                                                     chunk_length: int) -> "Prio3":
+        """new_prio3_sum_vec_field64_multiproof_hmacsha256_aes128 (core/src/vdaf.rs:176-199)."""
+        if proofs < 2:
+            raise ValueError("Must use at least two proofs with Field64")
+        return Prio3(PRIO3_SUMVEC_F64_MULTIPROOF, bits=bits, length=length, chunk_length=chunk_length,
+                     num_proofs=proofs)
+
     # -- derived sizes
     @property
+    def seed_size(self) -> int:
+        return 32 if self.algo_id == PRIO3_SUMVEC_F64_MULTIPROOF else 16
+
+    @property
+    def verify_key_len(self) -> int:
+        return VERIFY_KEY_LENGTH_HMACSHA256_AES128 if self.algo_id == PRIO3_SUMVEC_F64_MULTIPROOF \
+            else VERIFY_KEY_LENGTH
+
+    @property
     def field_bytes(self) -> int:
-        return 8 if self.algo_id == PRIO3_COUNT else 16
+        return 8 if self.algo_id in (PRIO3_COUNT, PRIO3_SUMVEC_F64_MULTIPROOF) else 16
 
     @property
     def meas_len(self) -> int:
         return {PRIO3_COUNT: 1, PRIO3_SUM: self.bits, PRIO3_SUMVEC: self.bits * self.length,
+                PRIO3_SUMVEC_F64_MULTIPROOF: self.bits * self.length,
                 PRIO3_HISTOGRAM: self.length}[self.algo_id]
 
     @property
@@ -65,7 +89,8 @@ class Prio3:
 
     @property
     def joint_rand_len(self) -> int:
-        return {PRIO3_COUNT: 0, PRIO3_SUM: 1, PRIO3_SUMVEC: 1, PRIO3_HISTOGRAM: 2}[self.algo_id]
+        return {PRIO3_COUNT: 0, PRIO3_SUM: 1, PRIO3_SUMVEC: 1, PRIO3_SUMVEC_F64_MULTIPROOF: 1,
+                PRIO3_HISTOGRAM: 2}[self.algo_id]
 
     @property
     def arity(self) -> int:
@@ -93,22 +118,29 @@ class Prio3:
 
     @property
     def public_share_len(self) -> int:
-        return 32 if self.joint_rand_len else 0
+        return 2 * self.seed_size if self.joint_rand_len else 0
 
     @property
     def helper_input_share_len(self) -> int:
-        return 48 if self.joint_rand_len else 32
+        return (3 if self.joint_rand_len else 2) * self.seed_size
 
     @property
     def prep_share_len(self) -> int:
-        return self.verifier_len * self.field_bytes + (16 if self.joint_rand_len else 0)
+        return self.num_proofs * self.verifier_len * self.field_bytes + (self.seed_size if self.joint_rand_len else 0)
+
+    @property
+    def leader_input_share_len(self) -> int:
+        return (self.meas_len + self.num_proofs * self.proof_len) * self.field_bytes + \
+            (self.seed_size if self.joint_rand_len else 0)
 
     @property
     def prep_msg_len(self) -> int:
-        return 16 if self.joint_rand_len else 0
+        return self.seed_size if self.joint_rand_len else 0
 
     def name(self) -> str:
         return {PRIO3_COUNT: "Prio3Count", PRIO3_SUM: f"Prio3Sum{{bits={self.bits}}}",
                 PRIO3_SUMVEC: f"Prio3SumVec{{bits={self.bits},length={self.length},chunk_length={self.chunk_length}}}",
                 PRIO3_HISTOGRAM: f"Prio3Histogram{{length={self.length},chunk_length={self.chunk_length}}}",
+                PRIO3_SUMVEC_F64_MULTIPROOF: "Prio3SumVecField64MultiproofHmacSha256Aes128"
+                f"{{proofs={self.num_proofs},bits={self.bits},length={self.length},chunk_length={self.chunk_length}}}",
                 }[self.algo_id]

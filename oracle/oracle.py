@@ -19,6 +19,8 @@ _LIB_PATH = os.path.join(_HERE, "build", "libprio3_oracle.so")
 _lib = None
 
 COUNT, SUM, SUMVEC, HISTOGRAM = 0, 1, 2, 3
+# Prio3SumVecField64MultiproofHmacSha256Aes128 (core/src/vdaf.rs:173-199)
+SUMVEC_F64_MULTIPROOF = 4
 VERDICT_NAMES = {
     0: "finished",
     1: "prepare_init_failure",
@@ -55,6 +57,8 @@ def lib():
             getattr(L, name).restype = ctypes.c_int
         L.jo_turboshake128.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint8, u8p, ctypes.c_size_t]
         L.jo_xof_expand.argtypes = [u8p, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t]
+        L.jo_xof_hmac_aes.argtypes = [u8p, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t]
+        L.jo_aes128_encrypt.argtypes = [u8p, u8p, u8p]
         L.jo_keccak_p1600.argtypes = [u8p, ctypes.c_int]
         L.jo_field_op.argtypes = [ctypes.c_int, ctypes.c_int, u8p, u8p, u8p]
         L.jo_sha256.argtypes = [u8p, ctypes.c_size_t, u8p]
@@ -87,6 +91,18 @@ def keccak_p1600(state: list[int], rounds: int) -> list[int]:
 def xof_expand(seed: bytes, dst: bytes, binder: bytes, outlen: int) -> bytes:
     out = bytearray(outlen)
     lib().jo_xof_expand(_buf(seed), _buf(dst), len(dst), _buf(binder), len(binder), _buf(out), outlen)
+    return bytes(out)
+
+
+def xof_hmac_aes(seed: bytes, dst: bytes, binder: bytes, outlen: int) -> bytes:
+    out = bytearray(outlen)
+    lib().jo_xof_hmac_aes(_buf(seed), _buf(dst), len(dst), _buf(binder), len(binder), _buf(out), outlen)
+    return bytes(out)
+
+
+def aes128_encrypt(key: bytes, block: bytes) -> bytes:
+    out = bytearray(16)
+    lib().jo_aes128_encrypt(_buf(key), _buf(block), _buf(out))
     return bytes(out)
 
 
@@ -126,6 +142,8 @@ class Sizes:
     arity: int
     calls: int
     P: int
+    seed: int
+    verify_key: int
 
 
 class Prio3Oracle:
@@ -133,7 +151,7 @@ class Prio3Oracle:
 
     def __init__(self, algo: int, bits: int = 0, length: int = 0, chunk: int = 0, proofs: int = 1):
         self.params = (algo, bits, length, chunk, proofs)
-        out = (ctypes.c_uint32 * 15)()
+        out = (ctypes.c_uint32 * 17)()
         if lib().jo_sizes(*self.params, ctypes.cast(out, ctypes.c_void_p)) != 0:
             raise ValueError(f"bad Prio3 params {self.params}")
         self.sizes = Sizes(*list(out))
@@ -141,7 +159,7 @@ class Prio3Oracle:
 
     @property
     def meas_stride(self) -> int:
-        return self.params[2] if self.algo == SUMVEC else 1
+        return self.params[2] if self.algo in (SUMVEC, SUMVEC_F64_MULTIPROOF) else 1
 
     def shard(self, measurement, nonce: bytes, rand: bytes):
         s = self.sizes
@@ -154,13 +172,13 @@ class Prio3Oracle:
 
     def prep_init(self, vk: bytes, agg_id: int, nonce: bytes, public_share: bytes, input_share: bytes):
         s = self.sizes
-        prep_share, out, corr = bytearray(s.prep_share), bytearray(s.output_len * s.field_bytes), bytearray(16)
+        prep_share, out, corr = bytearray(s.prep_share), bytearray(s.output_len * s.field_bytes), bytearray(s.seed)
         rc = lib().jo_prep_init(*self.params, _buf(vk), agg_id, _buf(nonce), _buf(public_share),
                                 _buf(input_share), _buf(prep_share), _buf(out), _buf(corr))
         return rc, bytes(prep_share), bytes(out), bytes(corr)
 
     def prep_shares_to_prep(self, leader_share: bytes, helper_share: bytes):
-        msg = bytearray(16)
+        msg = bytearray(self.sizes.seed)
         rc = lib().jo_prep_shares_to_prep(*self.params, _buf(leader_share), len(leader_share),
                                           _buf(helper_share), len(helper_share), _buf(msg))
         return rc, bytes(msg[: self.sizes.prep_msg])
@@ -168,7 +186,7 @@ class Prio3Oracle:
     def helper_prep(self, vk: bytes, nonce: bytes, public_share: bytes, helper_input_share: bytes,
                     leader_prep_share: bytes):
         s = self.sizes
-        msg, out = bytearray(16), bytearray(s.output_len * s.field_bytes)
+        msg, out = bytearray(s.seed), bytearray(s.output_len * s.field_bytes)
         v = lib().jo_helper_prep(*self.params, _buf(vk), _buf(nonce), _buf(public_share),
                                  _buf(helper_input_share), _buf(leader_prep_share), len(leader_prep_share),
                                  _buf(msg), _buf(out))

@@ -122,6 +122,283 @@ void jo_xof_expand(const uint8_t seed[16], const uint8_t *dst, size_t dst_len, c
 }
 
 /* ------------------------------------------------------------------------- */
+/* SHA-256 (FIPS 180-4): ReportIdChecksum (core/src/report_id.rs:19-42) and the HMAC of
+ * XofHmacSha256Aes128.                                                        */
+
+static const uint32_t SHA_K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+static inline uint32_t ror32(uint32_t v, int n) { return (v >> n) | (v << (32 - n)); }
+
+static void sha256_block(uint32_t h[8], const uint8_t *blk) {
+  uint32_t w[64];
+  for (int i = 0; i < 16; i++)
+    w[i] = (uint32_t)blk[4 * i] << 24 | (uint32_t)blk[4 * i + 1] << 16 | (uint32_t)blk[4 * i + 2] << 8 | blk[4 * i + 3];
+  for (int i = 16; i < 64; i++) {
+    uint32_t s0 = ror32(w[i - 15], 7) ^ ror32(w[i - 15], 18) ^ (w[i - 15] >> 3);
+    uint32_t s1 = ror32(w[i - 2], 17) ^ ror32(w[i - 2], 19) ^ (w[i - 2] >> 10);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  for (int i = 0; i < 64; i++) {
+    uint32_t S1 = ror32(e, 6) ^ ror32(e, 11) ^ ror32(e, 25);
+    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t t1 = hh + S1 + ch + SHA_K[i] + w[i];
+    uint32_t S0 = ror32(a, 2) ^ ror32(a, 13) ^ ror32(a, 22);
+    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint32_t t2 = S0 + mj;
+    hh = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+  }
+  h[0] += a;
+  h[1] += b;
+  h[2] += c;
+  h[3] += d;
+  h[4] += e;
+  h[5] += f;
+  h[6] += g;
+  h[7] += hh;
+}
+
+typedef struct {
+  uint32_t h[8];
+  uint8_t buf[64];
+  size_t blen;
+  uint64_t total;
+} sha_t;
+
+static void sha_init(sha_t *s) {
+  static const uint32_t H0[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  memcpy(s->h, H0, sizeof H0);
+  s->blen = 0;
+  s->total = 0;
+}
+static void sha_update(sha_t *s, const uint8_t *m, size_t len) {
+  s->total += len;
+  for (size_t i = 0; i < len; i++) {
+    s->buf[s->blen++] = m[i];
+    if (s->blen == 64) {
+      sha256_block(s->h, s->buf);
+      s->blen = 0;
+    }
+  }
+}
+static void sha_final(sha_t *s, uint8_t out[32]) {
+  uint64_t bits = s->total * 8;
+  uint8_t pad = 0x80, z = 0;
+  sha_update(s, &pad, 1);
+  while (s->blen != 56) sha_update(s, &z, 1);
+  uint8_t L[8];
+  for (int k = 0; k < 8; k++) L[k] = (uint8_t)(bits >> (56 - 8 * k));
+  sha_update(s, L, 8);
+  for (int k = 0; k < 8; k++) {
+    out[4 * k] = (uint8_t)(s->h[k] >> 24);
+    out[4 * k + 1] = (uint8_t)(s->h[k] >> 16);
+    out[4 * k + 2] = (uint8_t)(s->h[k] >> 8);
+    out[4 * k + 3] = (uint8_t)s->h[k];
+  }
+}
+
+void jo_sha256(const uint8_t *msg, size_t len, uint8_t out[32]) {
+  sha_t s;
+  sha_init(&s);
+  sha_update(&s, msg, len);
+  sha_final(&s, out);
+}
+
+/* HMAC-SHA256 (RFC 2104) with a key of at most 64 bytes (the XOF's 32-byte seeds). */
+typedef struct {
+  sha_t inner;
+  uint8_t okey[64];
+} hmac_t;
+
+static void hmac_init(hmac_t *m, const uint8_t *key, size_t klen) {
+  uint8_t ik[64];
+  memset(ik, 0, 64);
+  memcpy(ik, key, klen);
+  for (int i = 0; i < 64; i++) {
+    m->okey[i] = ik[i] ^ 0x5c;
+    ik[i] ^= 0x36;
+  }
+  sha_init(&m->inner);
+  sha_update(&m->inner, ik, 64);
+}
+static void hmac_final(hmac_t *m, uint8_t tag[32]) {
+  uint8_t ih[32];
+  sha_final(&m->inner, ih);
+  sha_t o;
+  sha_init(&o);
+  sha_update(&o, m->okey, 64);
+  sha_update(&o, ih, 32);
+  sha_final(&o, tag);
+}
+
+/* ------------------------------------------------------------------------- */
+/* AES-128 (FIPS 197), byte-oriented, S-box derived from the GF(2^8) inverse.  */
+
+static uint8_t AES_SBOX[256];
+static pthread_once_t aes_once = PTHREAD_ONCE_INIT;
+
+static uint8_t gf_mul(uint8_t a, uint8_t b) {
+  uint8_t r = 0;
+  while (b) {
+    if (b & 1) r ^= a;
+    a = (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+    b >>= 1;
+  }
+  return r;
+}
+static void aes_init_sbox(void) {
+  for (int x = 0; x < 256; x++) {
+    uint8_t inv = 0;
+    for (int y = 1; y < 256 && x; y++)
+      if (gf_mul((uint8_t)x, (uint8_t)y) == 1) {
+        inv = (uint8_t)y;
+        break;
+      }
+    uint8_t s = inv;
+    for (int i = 1; i <= 4; i++) s ^= (uint8_t)((inv << i) | (inv >> (8 - i)));
+    AES_SBOX[x] = s ^ 0x63;
+  }
+}
+static void aes128_expand(const uint8_t key[16], uint8_t rk[176]) {
+  pthread_once(&aes_once, aes_init_sbox);
+  memcpy(rk, key, 16);
+  uint8_t rcon = 1;
+  for (int i = 4; i < 44; i++) {
+    uint8_t t[4];
+    memcpy(t, rk + 4 * (i - 1), 4);
+    if (i % 4 == 0) {
+      uint8_t t0 = t[0];
+      t[0] = AES_SBOX[t[1]] ^ rcon;
+      t[1] = AES_SBOX[t[2]];
+      t[2] = AES_SBOX[t[3]];
+      t[3] = AES_SBOX[t0];
+      rcon = gf_mul(rcon, 2);
+    }
+    for (int j = 0; j < 4; j++) rk[4 * i + j] = rk[4 * (i - 4) + j] ^ t[j];
+  }
+}
+static void aes128_block(const uint8_t rk[176], const uint8_t in[16], uint8_t out[16]) {
+  uint8_t s[16], t[16];
+  for (int i = 0; i < 16; i++) s[i] = in[i] ^ rk[i];
+  for (int r = 1; r <= 10; r++) {
+    for (int i = 0; i < 16; i++) s[i] = AES_SBOX[s[i]];
+    for (int i = 0; i < 16; i++) t[i] = s[(i + 4 * (i % 4)) % 16]; /* ShiftRows, column-major s[4c+r] */
+    if (r < 10) {
+      for (int c = 0; c < 4; c++) {
+        const uint8_t *a = t + 4 * c;
+        uint8_t m0 = gf_mul(a[0], 2) ^ gf_mul(a[1], 3) ^ a[2] ^ a[3];
+        uint8_t m1 = a[0] ^ gf_mul(a[1], 2) ^ gf_mul(a[2], 3) ^ a[3];
+        uint8_t m2 = a[0] ^ a[1] ^ gf_mul(a[2], 2) ^ gf_mul(a[3], 3);
+        uint8_t m3 = gf_mul(a[0], 3) ^ a[1] ^ a[2] ^ gf_mul(a[3], 2);
+        s[4 * c] = m0;
+        s[4 * c + 1] = m1;
+        s[4 * c + 2] = m2;
+        s[4 * c + 3] = m3;
+      }
+    } else {
+      memcpy(s, t, 16);
+    }
+    for (int i = 0; i < 16; i++) s[i] ^= rk[16 * r + i];
+  }
+  memcpy(out, s, 16);
+}
+
+void jo_aes128_encrypt(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]) {
+  uint8_t rk[176];
+  aes128_expand(key, rk);
+  aes128_block(rk, in, out);
+}
+
+/* ------------------------------------------------------------------------- */
+/* The Prio3 XOF, two instantiations:
+ *  - XofTurboShake128 (VDAF-08 §6.2.1), SEED_SIZE 16: TurboSHAKE128(byte(len(dst)) || dst ||
+ *    seed || binder, D = 1);
+ *  - XofHmacSha256Aes128 (prio 0.16.1 vdaf::xof, "experimental"; Janus
+ *    core/src/vdaf.rs:8,173-199), SEED_SIZE 32: tag = HMAC-SHA256(key = seed,
+ *    byte(len(dst)) || dst || binder); the stream is AES-128-CTR keystream with key tag[0:16]
+ *    and initial counter block tag[16:32], the low 64 bits a big-endian counter
+ *    (ctr 0.9.2 Ctr64BE; aes 0.8.4 / hmac 0.12.1 per Cargo.lock:41,979,1781).      */
+
+enum { XOF_TURBOSHAKE = 0, XOF_HMAC_AES = 1 };
+
+typedef struct {
+  int kind;
+  int squeezing;
+  ts_t ts;
+  hmac_t mac;
+  uint8_t rk[176];
+  uint8_t ctr[16];
+  uint8_t ks[16];
+  unsigned kpos;
+} xof_t;
+
+static void xof_start(xof_t *x, int kind, const uint8_t *seed, const uint8_t *dst, size_t dst_len) {
+  uint8_t l = (uint8_t)dst_len;
+  x->kind = kind;
+  x->squeezing = 0;
+  if (kind == XOF_TURBOSHAKE) {
+    xof_init(&x->ts, seed, dst, dst_len);
+  } else {
+    hmac_init(&x->mac, seed, 32);
+    sha_update(&x->mac.inner, &l, 1);
+    sha_update(&x->mac.inner, dst, dst_len);
+  }
+}
+static void xof_update(xof_t *x, const uint8_t *m, size_t len) {
+  if (x->kind == XOF_TURBOSHAKE)
+    ts_absorb(&x->ts, m, len);
+  else
+    sha_update(&x->mac.inner, m, len);
+}
+static void xof_read(xof_t *x, uint8_t *out, size_t len) {
+  if (x->kind == XOF_TURBOSHAKE) {
+    ts_squeeze(&x->ts, out, len);
+    return;
+  }
+  if (!x->squeezing) {
+    uint8_t tag[32];
+    hmac_final(&x->mac, tag);
+    aes128_expand(tag, x->rk);
+    memcpy(x->ctr, tag + 16, 16);
+    x->kpos = 16;
+    x->squeezing = 1;
+  }
+  for (size_t i = 0; i < len; i++) {
+    if (x->kpos == 16) {
+      aes128_block(x->rk, x->ctr, x->ks);
+      for (int k = 15; k >= 8; k--) /* Ctr64BE: increment the low 64 bits, wrapping */
+        if (++x->ctr[k] != 0) break;
+      x->kpos = 0;
+    }
+    out[i] = x->ks[x->kpos++];
+  }
+}
+
+void jo_xof_hmac_aes(const uint8_t seed[32], const uint8_t *dst, size_t dst_len, const uint8_t *binder,
+                     size_t binder_len, uint8_t *out, size_t outlen) {
+  xof_t x;
+  xof_start(&x, XOF_HMAC_AES, seed, dst, dst_len);
+  xof_update(&x, binder, binder_len);
+  xof_read(&x, out, outlen);
+}
+
+/* ------------------------------------------------------------------------- */
 /* Fields (VDAF-08 §6.1.2): Field64 p = 2^64-2^32+1, Field128 p = 2^128-28*2^64+1.
  * GEN = 7^((p-1)/2^GEN_LOG2). LE encoding; decode rejects values >= p.       */
 
@@ -238,11 +515,11 @@ static int f_decode(const field_t *F, const uint8_t *in, fe *v) {
 
 /* XOF.next_vec (VDAF-08 §6.2): read ENC bytes LE, mask to next_pow2(p)-1 (a no-op
  * for both fields), reject if >= p, continue the stream. */
-static void xof_next_vec(const field_t *F, ts_t *x, fe *out, size_t n) {
+static void xof_next_vec(const field_t *F, xof_t *x, fe *out, size_t n) {
   uint8_t buf[16];
   size_t i = 0;
   while (i < n) {
-    ts_squeeze(x, buf, F->enc);
+    xof_read(x, buf, (size_t)F->enc);
     fe v;
     if (f_decode(F, buf, &v) == 0) out[i++] = v;
   }
@@ -253,6 +530,9 @@ static void xof_next_vec(const field_t *F, ts_t *x, fe *out, size_t n) {
  * constructors core/src/vdaf.rs:203-262).                                     */
 
 enum { G_MUL = 0, G_RANGE2 = 1, G_PSUM_MUL = 2 };
+#define SEED_MAX 32
+/* Private-use algorithm id of Prio3SumVecField64MultiproofHmacSha256Aes128 (core/src/vdaf.rs:18-20). */
+#define ALGO_ID_SUMVEC_F64_MULTIPROOF 0xFFFF1003u
 enum {
   USAGE_MEAS_SHARE = 1,
   USAGE_PROOF_SHARE = 2,
@@ -265,6 +545,9 @@ enum {
 
 typedef struct {
   int algo, bits, length, chunk, proofs;
+  uint32_t algo_id; /* the DST's algorithm id */
+  int xof;          /* XOF_TURBOSHAKE or XOF_HMAC_AES */
+  int seed;         /* SEED_SIZE (= verify key length): 16 or 32 */
   const field_t *F;
   int meas_len, out_len, jr_len, qr_len;
   int gadget, arity, degree, calls, P;
@@ -285,6 +568,9 @@ static int cfg_make(cfg_t *c, int algo, int bits, int length, int chunk, int pro
   c->length = length;
   c->chunk = chunk;
   c->proofs = proofs;
+  c->algo_id = (uint32_t)algo;
+  c->xof = XOF_TURBOSHAKE;
+  c->seed = 16;
   if (proofs < 1 || proofs > 255) return -1;
   c->qr_len = 1;
   c->degree = 2;
@@ -308,9 +594,16 @@ static int cfg_make(cfg_t *c, int algo, int bits, int length, int chunk, int pro
       c->arity = 1;
       c->calls = bits;
       break;
+    case JO_SUMVEC_F64_MULTIPROOF: /* new_prio3_sum_vec_field64_multiproof_hmacsha256_aes128, core/src/vdaf.rs:176-199 */
+      if (proofs < 2) return -1;
+      c->algo_id = ALGO_ID_SUMVEC_F64_MULTIPROOF;
+      c->xof = XOF_HMAC_AES;
+      c->seed = 32;
+      /* SumVec<Field64, ParallelSum<Field64, Mul<Field64>>> */
+      __attribute__((fallthrough));
     case JO_SUMVEC:
       if (bits < 1 || bits > 64 || length < 1 || chunk < 1) return -1;
-      c->F = &F128;
+      c->F = algo == JO_SUMVEC ? &F128 : &F64;
       c->meas_len = bits * length;
       c->out_len = length;
       c->jr_len = 1;
@@ -342,28 +635,30 @@ static int cfg_make(cfg_t *c, int algo, int bits, int length, int chunk, int pro
 int jo_sizes(int algo, int bits, int length, int chunk, int proofs, uint32_t out[JO_NSIZES]) {
   cfg_t c;
   if (cfg_make(&c, algo, bits, length, chunk, proofs)) return -1;
-  int E = c.F->enc, jr = c.jr_len > 0;
+  int E = c.F->enc, jr = c.jr_len > 0, S = c.seed;
   out[0] = c.meas_len;
   out[1] = c.out_len;
   out[2] = c.jr_len;
   out[3] = c.proof_len;
   out[4] = c.verifier_len;
-  out[5] = jr ? 32 : 0;
-  out[6] = (c.meas_len + c.proof_len * proofs) * E + (jr ? 16 : 0);
-  out[7] = 32 + (jr ? 16 : 0);
-  out[8] = c.verifier_len * proofs * E + (jr ? 16 : 0);
-  out[9] = jr ? 16 : 0;
+  out[5] = jr ? 2 * S : 0;
+  out[6] = (c.meas_len + c.proof_len * proofs) * E + (jr ? S : 0);
+  out[7] = 2 * S + (jr ? S : 0);
+  out[8] = c.verifier_len * proofs * E + (jr ? S : 0);
+  out[9] = jr ? S : 0;
   out[10] = E;
-  out[11] = 16 * (3 + (jr ? 2 : 0));
+  out[11] = S * (3 + (jr ? 2 : 0));
   out[12] = c.arity;
   out[13] = c.calls;
   out[14] = c.P;
+  out[15] = S;
+  out[16] = S;
   return 0;
 }
 
 static void dst_make(const cfg_t *c, int usage, uint8_t dst[8]) {
   /* VDAF-08 §7.2.x domain_separation_tag = format_dst(0, ID, usage): VERSION=8 */
-  uint32_t id = (uint32_t)c->algo;
+  uint32_t id = c->algo_id;
   dst[0] = 8;
   dst[1] = 0;
   dst[2] = (uint8_t)(id >> 24);
@@ -374,13 +669,13 @@ static void dst_make(const cfg_t *c, int usage, uint8_t dst[8]) {
   dst[7] = (uint8_t)usage;
 }
 
-static void expand_into_vec(const cfg_t *c, const uint8_t seed[16], int usage, const uint8_t *binder,
-                            size_t blen, fe *out, size_t n) {
+static void expand_into_vec(const cfg_t *c, const uint8_t *seed, int usage, const uint8_t *binder, size_t blen,
+                            fe *out, size_t n) {
   uint8_t dst[8];
-  ts_t x;
+  xof_t x;
   dst_make(c, usage, dst);
-  xof_init(&x, seed, dst, 8);
-  ts_absorb(&x, binder, blen);
+  xof_start(&x, c->xof, seed, dst, 8);
+  xof_update(&x, binder, blen);
   xof_next_vec(c->F, &x, out, n);
 }
 
@@ -499,7 +794,8 @@ static fe valid_eval(const cfg_t *c, grec_t *g, const fe *meas, const fe *jr, in
       }
       return out;
     }
-    case JO_SUMVEC: {
+    case JO_SUMVEC:
+    case JO_SUMVEC_F64_MULTIPROOF: {
       fe *buf = calloc((size_t)c->arity, sizeof(fe));
       fe out = psum_range_checks(c, g, meas, jr[0], num_shares, buf);
       free(buf);
@@ -526,6 +822,7 @@ static void flp_encode(const cfg_t *c, uint64_t m, const uint64_t *vec, fe *meas
       for (int i = 0; i < c->bits; i++) meas[i] = (m >> i) & 1;
       break;
     case JO_SUMVEC:
+    case JO_SUMVEC_F64_MULTIPROOF:
       for (int i = 0; i < c->length; i++)
         for (int j = 0; j < c->bits; j++) meas[i * c->bits + j] = (vec[i] >> j) & 1;
       break;
@@ -631,56 +928,57 @@ static int flp_decide(const cfg_t *c, const fe *verifier) {
 /* ------------------------------------------------------------------------- */
 /* Prio3 (VDAF-08 §7.2).                                                       */
 
-static void derive_seed(const cfg_t *c, const uint8_t seed[16], int usage, const uint8_t *binder, size_t blen,
-                        uint8_t out[16]) {
+/* Xof::derive_seed: the first SEED_SIZE bytes of the stream */
+static void derive_seed(const cfg_t *c, const uint8_t *seed, int usage, const uint8_t *binder, size_t blen,
+                        uint8_t *out) {
   uint8_t dst[8];
-  ts_t x;
+  xof_t x;
   dst_make(c, usage, dst);
-  xof_init(&x, seed, dst, 8);
-  ts_absorb(&x, binder, blen);
-  ts_squeeze(&x, out, 16);
+  xof_start(&x, c->xof, seed, dst, 8);
+  xof_update(&x, binder, blen);
+  xof_read(&x, out, (size_t)c->seed);
 }
 
-static void joint_rand_part(const cfg_t *c, int agg_id, const uint8_t blind[16], const fe *meas_share,
-                            const uint8_t nonce[16], uint8_t out[16]) {
+static void joint_rand_part(const cfg_t *c, int agg_id, const uint8_t *blind, const fe *meas_share,
+                            const uint8_t nonce[16], uint8_t *out) {
   uint8_t dst[8], b = (uint8_t)agg_id, enc[16];
-  ts_t x;
+  xof_t x;
   dst_make(c, USAGE_JOINT_RAND_PART, dst);
-  xof_init(&x, blind, dst, 8);
-  ts_absorb(&x, &b, 1);
-  ts_absorb(&x, nonce, 16);
+  xof_start(&x, c->xof, blind, dst, 8);
+  xof_update(&x, &b, 1);
+  xof_update(&x, nonce, 16);
   for (int i = 0; i < c->meas_len; i++) {
     f_encode(c->F, meas_share[i], enc);
-    ts_absorb(&x, enc, (size_t)c->F->enc);
+    xof_update(&x, enc, (size_t)c->F->enc);
   }
-  ts_squeeze(&x, out, 16);
+  xof_read(&x, out, (size_t)c->seed);
 }
 
-static void joint_rand_seed(const cfg_t *c, const uint8_t part0[16], const uint8_t part1[16], uint8_t out[16]) {
-  uint8_t zero[16] = {0}, parts[32];
-  memcpy(parts, part0, 16);
-  memcpy(parts + 16, part1, 16);
-  derive_seed(c, zero, USAGE_JOINT_RAND_SEED, parts, 32, out);
+static void joint_rand_seed(const cfg_t *c, const uint8_t *part0, const uint8_t *part1, uint8_t *out) {
+  uint8_t zero[SEED_MAX] = {0}, parts[2 * SEED_MAX];
+  memcpy(parts, part0, (size_t)c->seed);
+  memcpy(parts + c->seed, part1, (size_t)c->seed);
+  derive_seed(c, zero, USAGE_JOINT_RAND_SEED, parts, 2 * (size_t)c->seed, out);
 }
 
-static void joint_rands(const cfg_t *c, const uint8_t seed[16], fe *out) {
+static void joint_rands(const cfg_t *c, const uint8_t *seed, fe *out) {
   uint8_t binder = (uint8_t)c->proofs;
   expand_into_vec(c, seed, USAGE_JOINT_RANDOMNESS, &binder, 1, out, (size_t)c->jr_len * c->proofs);
 }
 
-static void query_rands(const cfg_t *c, const uint8_t vk[16], const uint8_t nonce[16], fe *out) {
+static void query_rands(const cfg_t *c, const uint8_t *vk, const uint8_t nonce[16], fe *out) {
   uint8_t binder[17];
   binder[0] = (uint8_t)c->proofs;
   memcpy(binder + 1, nonce, 16);
   expand_into_vec(c, vk, USAGE_QUERY_RANDOMNESS, binder, 17, out, (size_t)c->qr_len * c->proofs);
 }
 
-static void helper_meas_share(const cfg_t *c, int agg_id, const uint8_t seed[16], fe *out) {
+static void helper_meas_share(const cfg_t *c, int agg_id, const uint8_t *seed, fe *out) {
   uint8_t binder = (uint8_t)agg_id;
   expand_into_vec(c, seed, USAGE_MEAS_SHARE, &binder, 1, out, (size_t)c->meas_len);
 }
 
-static void helper_proofs_share(const cfg_t *c, int agg_id, const uint8_t seed[16], fe *out) {
+static void helper_proofs_share(const cfg_t *c, int agg_id, const uint8_t *seed, fe *out) {
   uint8_t binder[2] = {(uint8_t)c->proofs, (uint8_t)agg_id};
   expand_into_vec(c, seed, USAGE_PROOF_SHARE, binder, 2, out, (size_t)c->proof_len * c->proofs);
 }
@@ -694,10 +992,10 @@ int jo_shard(int algo, int bits, int length, int chunk, int proofs, const uint64
              uint8_t *helper_input_share) {
   CFG_OR_FAIL(c);
   const field_t *F = c.F;
-  int E = F->enc, JR = c.jr_len > 0;
-  /* rand = k_helper_meas || k_helper_proofs || k_prove || [blind_L || blind_H] */
-  const uint8_t *k_hmeas = rand, *k_hproofs = rand + 16, *k_prove = rand + 32;
-  const uint8_t *blind_l = rand + 48, *blind_h = rand + 64;
+  int E = F->enc, JR = c.jr_len > 0, S = c.seed;
+  /* rand = k_helper_meas || k_helper_proofs || k_prove || [blind_L || blind_H], SEED_SIZE each */
+  const uint8_t *k_hmeas = rand, *k_hproofs = rand + S, *k_prove = rand + 2 * S;
+  const uint8_t *blind_l = rand + 3 * S, *blind_h = rand + 4 * S;
   fe *meas = calloc((size_t)c.meas_len, sizeof(fe)), *hmeas = calloc((size_t)c.meas_len, sizeof(fe));
   fe *proofs_v = calloc((size_t)c.proof_len * proofs, sizeof(fe));
   fe *hproofs = calloc((size_t)c.proof_len * proofs, sizeof(fe));
@@ -706,11 +1004,11 @@ int jo_shard(int algo, int bits, int length, int chunk, int proofs, const uint64
   flp_encode(&c, measurement[0], measurement, meas);
   helper_meas_share(&c, 1, k_hmeas, hmeas);
   for (int i = 0; i < c.meas_len; i++) meas[i] = f_sub(F, meas[i], hmeas[i]); /* leader share */
-  uint8_t part_l[16], part_h[16];
+  uint8_t part_l[SEED_MAX], part_h[SEED_MAX];
   if (JR) {
     joint_rand_part(&c, 0, blind_l, meas, nonce, part_l);
     joint_rand_part(&c, 1, blind_h, hmeas, nonce, part_h);
-    uint8_t seed[16];
+    uint8_t seed[SEED_MAX];
     joint_rand_seed(&c, part_l, part_h, seed);
     joint_rands(&c, seed, jr);
   }
@@ -728,16 +1026,16 @@ int jo_shard(int algo, int bits, int length, int chunk, int proofs, const uint64
   for (int i = 0; i < c.proof_len * proofs; i++) proofs_v[i] = f_sub(F, proofs_v[i], hproofs[i]);
   /* encodings */
   if (JR) {
-    memcpy(public_share, part_l, 16);
-    memcpy(public_share + 16, part_h, 16);
+    memcpy(public_share, part_l, (size_t)S);
+    memcpy(public_share + S, part_h, (size_t)S);
   }
   uint8_t *o = leader_input_share;
   for (int i = 0; i < c.meas_len; i++, o += E) f_encode(F, meas[i], o);
   for (int i = 0; i < c.proof_len * proofs; i++, o += E) f_encode(F, proofs_v[i], o);
-  if (JR) memcpy(o, blind_l, 16);
-  memcpy(helper_input_share, k_hmeas, 16);
-  memcpy(helper_input_share + 16, k_hproofs, 16);
-  if (JR) memcpy(helper_input_share + 32, blind_h, 16);
+  if (JR) memcpy(o, blind_l, (size_t)S);
+  memcpy(helper_input_share, k_hmeas, (size_t)S);
+  memcpy(helper_input_share + S, k_hproofs, (size_t)S);
+  if (JR) memcpy(helper_input_share + 2 * S, blind_h, (size_t)S);
   free(meas);
   free(hmeas);
   free(proofs_v);
@@ -747,11 +1045,11 @@ int jo_shard(int algo, int bits, int length, int chunk, int proofs, const uint64
   return 0;
 }
 
-static int prep_init_cfg(const cfg_t *c, const uint8_t vk[16], int agg_id, const uint8_t nonce[16],
+static int prep_init_cfg(const cfg_t *c, const uint8_t *vk, int agg_id, const uint8_t nonce[16],
                          const uint8_t *public_share, const uint8_t *input_share, uint8_t *prep_share,
-                         fe *out_share, uint8_t corrected[16]) {
+                         fe *out_share, uint8_t *corrected) {
   const field_t *F = c->F;
-  int E = F->enc, JR = c->jr_len > 0, np = c->proofs;
+  int E = F->enc, JR = c->jr_len > 0, np = c->proofs, S = c->seed;
   fe *meas = calloc((size_t)c->meas_len, sizeof(fe));
   fe *proofs_v = calloc((size_t)c->proof_len * np, sizeof(fe));
   const uint8_t *blind = NULL;
@@ -765,19 +1063,19 @@ static int prep_init_cfg(const cfg_t *c, const uint8_t vk[16], int agg_id, const
     blind = p;
   } else {
     helper_meas_share(c, agg_id, input_share, meas);
-    helper_proofs_share(c, agg_id, input_share + 16, proofs_v);
-    blind = input_share + 32;
+    helper_proofs_share(c, agg_id, input_share + S, proofs_v);
+    blind = input_share + 2 * S;
   }
   if (!rc) {
     flp_truncate(c, meas, out_share);
     fe jr[2 * 256] = {0}, qr[256];
-    uint8_t own_part[16];
+    uint8_t own_part[SEED_MAX];
     if (JR) {
-      uint8_t parts[2][16];
+      uint8_t parts[2][SEED_MAX];
       joint_rand_part(c, agg_id, blind, meas, nonce, own_part);
-      memcpy(parts[0], public_share, 16);
-      memcpy(parts[1], public_share + 16, 16);
-      memcpy(parts[agg_id], own_part, 16);
+      memcpy(parts[0], public_share, (size_t)S);
+      memcpy(parts[1], public_share + S, (size_t)S);
+      memcpy(parts[agg_id], own_part, (size_t)S);
       joint_rand_seed(c, parts[0], parts[1], corrected);
       joint_rands(c, corrected, jr);
     }
@@ -790,7 +1088,7 @@ static int prep_init_cfg(const cfg_t *c, const uint8_t vk[16], int agg_id, const
     if (!rc) {
       uint8_t *o = prep_share;
       for (int i = 0; i < c->verifier_len * np; i++, o += E) f_encode(F, ver[i], o);
-      if (JR) memcpy(o, own_part, 16);
+      if (JR) memcpy(o, own_part, (size_t)S);
     }
     free(ver);
   }
@@ -799,37 +1097,37 @@ static int prep_init_cfg(const cfg_t *c, const uint8_t vk[16], int agg_id, const
   return rc;
 }
 
-int jo_prep_init(int algo, int bits, int length, int chunk, int proofs, const uint8_t verify_key[16], int agg_id,
+int jo_prep_init(int algo, int bits, int length, int chunk, int proofs, const uint8_t *verify_key, int agg_id,
                  const uint8_t nonce[16], const uint8_t *public_share, const uint8_t *input_share,
                  uint8_t *prep_share, uint8_t *out_share, uint8_t *corrected_seed) {
   CFG_OR_FAIL(c);
   fe *out = calloc((size_t)c.out_len, sizeof(fe));
-  uint8_t corr[16] = {0};
+  uint8_t corr[SEED_MAX] = {0};
   int rc = prep_init_cfg(&c, verify_key, agg_id, nonce, public_share, input_share, prep_share, out, corr);
   if (!rc) {
     for (int i = 0; i < c.out_len; i++) f_encode(c.F, out[i], out_share + (size_t)i * c.F->enc);
-    if (corrected_seed) memcpy(corrected_seed, corr, 16);
+    if (corrected_seed) memcpy(corrected_seed, corr, (size_t)c.seed);
   }
   free(out);
   return rc;
 }
 
 /* decode a prep share (Prio3PrepareShare): verifiers || [joint_rand_part] */
-static int decode_prep_share(const cfg_t *c, const uint8_t *b, size_t len, fe *ver, uint8_t part[16]) {
+static int decode_prep_share(const cfg_t *c, const uint8_t *b, size_t len, fe *ver, uint8_t *part) {
   int E = c->F->enc, n = c->verifier_len * c->proofs;
-  size_t want = (size_t)n * E + (c->jr_len ? 16 : 0);
+  size_t want = (size_t)n * E + (c->jr_len ? (size_t)c->seed : 0);
   if (len != want) return -1;
   for (int i = 0; i < n; i++)
     if (f_decode(c->F, b + (size_t)i * E, &ver[i])) return -1;
-  if (c->jr_len) memcpy(part, b + (size_t)n * E, 16);
+  if (c->jr_len) memcpy(part, b + (size_t)n * E, (size_t)c->seed);
   return 0;
 }
 
 static int prep_shares_to_prep_cfg(const cfg_t *c, const uint8_t *ls, size_t llen, const uint8_t *hs, size_t hlen,
-                                   uint8_t msg[16]) {
+                                   uint8_t *msg) {
   int n = c->verifier_len * c->proofs;
   fe *lv = calloc((size_t)n, sizeof(fe)), *hv = calloc((size_t)n, sizeof(fe));
-  uint8_t lp[16], hp[16];
+  uint8_t lp[SEED_MAX], hp[SEED_MAX];
   int rc = 0;
   if (decode_prep_share(c, ls, llen, lv, lp) || decode_prep_share(c, hs, hlen, hv, hp)) {
     rc = JO_PREP_SHARE_DECODE_FAILURE;
@@ -853,24 +1151,24 @@ int jo_prep_shares_to_prep(int algo, int bits, int length, int chunk, int proofs
 
 /* prio ping-pong helper_initialized + evaluate (topology::ping_pong), as called at
  * aggregator/src/aggregator.rs:1947-1956; error mapping error.rs:379-424. */
-static int helper_prep_cfg(const cfg_t *c, const uint8_t vk[16], const uint8_t nonce[16], const uint8_t *ps,
+static int helper_prep_cfg(const cfg_t *c, const uint8_t *vk, const uint8_t nonce[16], const uint8_t *ps,
                            const uint8_t *his, const uint8_t *lps, size_t llen, uint8_t *msg, fe *out) {
   uint32_t sz[JO_NSIZES];
   jo_sizes(c->algo, c->bits, c->length, c->chunk, c->proofs, sz);
   uint8_t *hshare = malloc(sz[8]);
-  uint8_t corrected[16] = {0}, m[16] = {0};
+  uint8_t corrected[SEED_MAX] = {0}, m[SEED_MAX] = {0};
   int rc = prep_init_cfg(c, vk, 1, nonce, ps, his, hshare, out, corrected);
   if (!rc) {
     rc = prep_shares_to_prep_cfg(c, lps, llen, hshare, sz[8], m);
     /* prepare_next: prep_msg must equal the corrected joint-rand seed */
-    if (!rc && c->jr_len && memcmp(m, corrected, 16) != 0) rc = JO_PREPARE_NEXT_FAILURE;
-    if (!rc && msg && c->jr_len) memcpy(msg, m, 16);
+    if (!rc && c->jr_len && memcmp(m, corrected, (size_t)c->seed) != 0) rc = JO_PREPARE_NEXT_FAILURE;
+    if (!rc && msg && c->jr_len) memcpy(msg, m, (size_t)c->seed);
   }
   free(hshare);
   return rc;
 }
 
-int jo_helper_prep(int algo, int bits, int length, int chunk, int proofs, const uint8_t verify_key[16],
+int jo_helper_prep(int algo, int bits, int length, int chunk, int proofs, const uint8_t *verify_key,
                    const uint8_t nonce[16], const uint8_t *public_share, const uint8_t *helper_input_share,
                    const uint8_t *leader_prep_share, size_t leader_len, uint8_t *prep_msg, uint8_t *out_share) {
   CFG_OR_FAIL(c);
@@ -881,78 +1179,6 @@ int jo_helper_prep(int algo, int bits, int length, int chunk, int proofs, const 
     for (int i = 0; i < c.out_len; i++) f_encode(c.F, out[i], out_share + (size_t)i * c.F->enc);
   free(out);
   return rc;
-}
-
-/* ------------------------------------------------------------------------- */
-/* SHA-256 (FIPS 180-4), for ReportIdChecksum core/src/report_id.rs:19-42.      */
-
-static const uint32_t SHA_K[64] = {
-    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
-    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
-    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
-    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
-    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
-    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
-    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
-    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
-
-static inline uint32_t ror32(uint32_t v, int n) { return (v >> n) | (v << (32 - n)); }
-
-static void sha256_block(uint32_t h[8], const uint8_t *blk) {
-  uint32_t w[64];
-  for (int i = 0; i < 16; i++)
-    w[i] = (uint32_t)blk[4 * i] << 24 | (uint32_t)blk[4 * i + 1] << 16 | (uint32_t)blk[4 * i + 2] << 8 | blk[4 * i + 3];
-  for (int i = 16; i < 64; i++) {
-    uint32_t s0 = ror32(w[i - 15], 7) ^ ror32(w[i - 15], 18) ^ (w[i - 15] >> 3);
-    uint32_t s1 = ror32(w[i - 2], 17) ^ ror32(w[i - 2], 19) ^ (w[i - 2] >> 10);
-    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
-  }
-  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-  for (int i = 0; i < 64; i++) {
-    uint32_t S1 = ror32(e, 6) ^ ror32(e, 11) ^ ror32(e, 25);
-    uint32_t ch = (e & f) ^ (~e & g);
-    uint32_t t1 = hh + S1 + ch + SHA_K[i] + w[i];
-    uint32_t S0 = ror32(a, 2) ^ ror32(a, 13) ^ ror32(a, 22);
-    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
-    uint32_t t2 = S0 + mj;
-    hh = g;
-    g = f;
-    f = e;
-    e = d + t1;
-    d = c;
-    c = b;
-    b = a;
-    a = t1 + t2;
-  }
-  h[0] += a;
-  h[1] += b;
-  h[2] += c;
-  h[3] += d;
-  h[4] += e;
-  h[5] += f;
-  h[6] += g;
-  h[7] += hh;
-}
-
-void jo_sha256(const uint8_t *msg, size_t len, uint8_t out[32]) {
-  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
-  size_t i = 0;
-  for (; i + 64 <= len; i += 64) sha256_block(h, msg + i);
-  uint8_t blk[128] = {0};
-  size_t rem = len - i;
-  memcpy(blk, msg + i, rem);
-  blk[rem] = 0x80;
-  size_t tot = (rem + 9 <= 64) ? 64 : 128;
-  uint64_t bits = (uint64_t)len * 8;
-  for (int k = 0; k < 8; k++) blk[tot - 1 - k] = (uint8_t)(bits >> (8 * k));
-  sha256_block(h, blk);
-  if (tot == 128) sha256_block(h, blk + 64);
-  for (int k = 0; k < 8; k++) {
-    out[4 * k] = (uint8_t)(h[k] >> 24);
-    out[4 * k + 1] = (uint8_t)(h[k] >> 16);
-    out[4 * k + 2] = (uint8_t)(h[k] >> 8);
-    out[4 * k + 3] = (uint8_t)h[k];
-  }
 }
 
 /* ------------------------------------------------------------------------- */
@@ -980,7 +1206,7 @@ static void *helper_worker(void *arg) {
   jo_sizes(c->algo, c->bits, c->length, c->chunk, c->proofs, sz);
   fe *out = calloc((size_t)c->out_len, sizeof(fe));
   for (uint64_t r = j->lo; r < j->hi; r++) {
-    uint8_t msg[16] = {0};
+    uint8_t msg[SEED_MAX] = {0};
     int v = helper_prep_cfg(c, j->vk, j->nonces + 16 * r, j->ps + sz[5] * r, j->his + sz[7] * r,
                             j->lps + sz[8] * r, sz[8], msg, out);
     if (j->verdicts) j->verdicts[r] = (uint8_t)v;
@@ -1000,7 +1226,7 @@ static void *helper_worker(void *arg) {
   return NULL;
 }
 
-int jo_helper_prep_batch(int algo, int bits, int length, int chunk, int proofs, const uint8_t verify_key[16],
+int jo_helper_prep_batch(int algo, int bits, int length, int chunk, int proofs, const uint8_t *verify_key,
                          uint64_t n, const uint8_t *nonces, const uint8_t *public_shares,
                          const uint8_t *helper_input_shares, const uint8_t *leader_prep_shares, uint8_t *prep_msgs,
                          uint8_t *verdicts, uint8_t *out_shares, uint8_t *agg_out, uint64_t *count_out,
@@ -1053,9 +1279,9 @@ static void *client_worker(void *arg) {
   const cfg_t *c = j->c;
   uint32_t sz[JO_NSIZES];
   jo_sizes(c->algo, c->bits, c->length, c->chunk, c->proofs, sz);
-  int mstride = c->algo == JO_SUMVEC ? c->length : 1;
+  int mstride = (c->algo == JO_SUMVEC || c->algo == JO_SUMVEC_F64_MULTIPROOF) ? c->length : 1;
   uint8_t *lin = malloc(sz[6]);
-  uint8_t corr[16];
+  uint8_t corr[SEED_MAX];
   for (uint64_t r = j->lo; r < j->hi; r++) {
     jo_shard(c->algo, c->bits, c->length, c->chunk, c->proofs, j->meas + (size_t)mstride * r, j->nonces + 16 * r,
              j->rands + (size_t)sz[11] * r, j->ps_out + (size_t)sz[5] * r, lin, j->his_out + (size_t)sz[7] * r);
@@ -1071,7 +1297,7 @@ static void *client_worker(void *arg) {
   return NULL;
 }
 
-int jo_client_leader_batch(int algo, int bits, int length, int chunk, int proofs, const uint8_t verify_key[16],
+int jo_client_leader_batch(int algo, int bits, int length, int chunk, int proofs, const uint8_t *verify_key,
                            uint64_t n, const uint64_t *measurements, const uint8_t *nonces, const uint8_t *rands,
                            uint8_t *public_shares, uint8_t *helper_input_shares, uint8_t *leader_prep_shares,
                            uint8_t *leader_out_shares, int nthreads) {

@@ -28,8 +28,11 @@
 extern "C" {
 #endif
 
-/* Prio3 algorithm ids == taskprov VDAF type codes, messages/src/taskprov.rs:358-363 */
-enum { JO_COUNT = 0, JO_SUM = 1, JO_SUMVEC = 2, JO_HISTOGRAM = 3 };
+/* Prio3 algorithm ids == taskprov VDAF type codes, messages/src/taskprov.rs:358-363.
+ * JO_SUMVEC_F64_MULTIPROOF selects Prio3SumVecField64MultiproofHmacSha256Aes128
+ * (core/src/vdaf.rs:173-199: Field64, proofs >= 2, XofHmacSha256Aes128, 32-byte seeds and
+ * verify key, DST algorithm id 0xFFFF1003). */
+enum { JO_COUNT = 0, JO_SUM = 1, JO_SUMVEC = 2, JO_HISTOGRAM = 3, JO_SUMVEC_F64_MULTIPROOF = 4 };
 
 /* Verdicts, mirroring the PingPongError labels of aggregator/src/aggregator/error.rs:379-424 */
 enum {
@@ -44,8 +47,9 @@ enum {
  *  0 meas_len  1 output_len  2 joint_rand_len  3 proof_len  4 verifier_len
  *  5 public_share_bytes  6 leader_input_share_bytes  7 helper_input_share_bytes
  *  8 prep_share_bytes  9 prep_msg_bytes  10 field_bytes  11 client_rand_bytes
- *  12 gadget_arity  13 gadget_calls  14 P (wire poly length)            */
-#define JO_NSIZES 15
+ *  12 gadget_arity  13 gadget_calls  14 P (wire poly length)  15 seed_size
+ *  16 verify_key_size                                                    */
+#define JO_NSIZES 17
 int jo_sizes(int algo, int bits, int length, int chunk, int proofs, uint32_t out[JO_NSIZES]);
 
 /* Client: shard one measurement. measurement: Count {0,1}; Sum integer;
@@ -55,9 +59,10 @@ int jo_shard(int algo, int bits, int length, int chunk, int proofs,
              uint8_t *public_share, uint8_t *leader_input_share, uint8_t *helper_input_share);
 
 /* Prio3 prepare_init for one aggregator. Returns 0 or JO_PREPARE_INIT_FAILURE.
- * out_share: output_len*field_bytes; corrected_seed: 16 bytes (unused w/o joint rand). */
+ * out_share: output_len*field_bytes; corrected_seed: seed_size bytes (unused w/o joint rand).
+ * verify_key: verify_key_size bytes (16, or 32 for JO_SUMVEC_F64_MULTIPROOF). */
 int jo_prep_init(int algo, int bits, int length, int chunk, int proofs,
-                 const uint8_t verify_key[16], int agg_id, const uint8_t nonce[16],
+                 const uint8_t *verify_key, int agg_id, const uint8_t nonce[16],
                  const uint8_t *public_share, const uint8_t *input_share,
                  uint8_t *prep_share, uint8_t *out_share, uint8_t *corrected_seed);
 
@@ -71,7 +76,7 @@ int jo_prep_shares_to_prep(int algo, int bits, int length, int chunk, int proofs
 /* Ping-pong helper step: helper_initialized(...).evaluate(). Returns the verdict;
  * on JO_FINISHED writes prep_msg (prep_msg_bytes) and out_share. */
 int jo_helper_prep(int algo, int bits, int length, int chunk, int proofs,
-                   const uint8_t verify_key[16], const uint8_t nonce[16],
+                   const uint8_t *verify_key, const uint8_t nonce[16],
                    const uint8_t *public_share, const uint8_t *helper_input_share,
                    const uint8_t *leader_prep_share, size_t leader_len,
                    uint8_t *prep_msg, uint8_t *out_share);
@@ -81,7 +86,7 @@ int jo_helper_prep(int algo, int bits, int length, int chunk, int proofs,
  * shares; count_out (nullable) the accepted count; checksum_out (nullable) the XOR
  * of SHA-256(report id = nonce) over accepted reports. out_shares nullable. */
 int jo_helper_prep_batch(int algo, int bits, int length, int chunk, int proofs,
-                         const uint8_t verify_key[16], uint64_t n, const uint8_t *nonces,
+                         const uint8_t *verify_key, uint64_t n, const uint8_t *nonces,
                          const uint8_t *public_shares, const uint8_t *helper_input_shares,
                          const uint8_t *leader_prep_shares, uint8_t *prep_msgs, uint8_t *verdicts,
                          uint8_t *out_shares, uint8_t *agg_out, uint64_t *count_out,
@@ -90,7 +95,7 @@ int jo_helper_prep_batch(int algo, int bits, int length, int chunk, int proofs,
 /* Batched client shard + leader prep_init (input generation for tests/bench).
  * measurements: n * (SumVec: length; else 1) uint64; rands: n*client_rand_bytes. */
 int jo_client_leader_batch(int algo, int bits, int length, int chunk, int proofs,
-                           const uint8_t verify_key[16], uint64_t n, const uint64_t *measurements,
+                           const uint8_t *verify_key, uint64_t n, const uint64_t *measurements,
                            const uint8_t *nonces, const uint8_t *rands, uint8_t *public_shares,
                            uint8_t *helper_input_shares, uint8_t *leader_prep_shares,
                            uint8_t *leader_out_shares, int nthreads);
@@ -104,6 +109,10 @@ void jo_keccak_p1600(uint64_t state[25], int rounds);
 void jo_turboshake128(const uint8_t *msg, size_t len, uint8_t D, uint8_t *out, size_t outlen);
 void jo_xof_expand(const uint8_t seed[16], const uint8_t *dst, size_t dst_len,
                    const uint8_t *binder, size_t binder_len, uint8_t *out, size_t outlen);
+/* XofHmacSha256Aes128 stream: the first outlen bytes for (seed, dst, binder). */
+void jo_xof_hmac_aes(const uint8_t seed[32], const uint8_t *dst, size_t dst_len,
+                     const uint8_t *binder, size_t binder_len, uint8_t *out, size_t outlen);
+void jo_aes128_encrypt(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]);
 int jo_field_op(int field64, int op, const uint8_t *a, const uint8_t *b, uint8_t *out);
 void jo_sha256(const uint8_t *msg, size_t len, uint8_t out[32]);
 

@@ -139,11 +139,36 @@ class XofTurboShake128:
 
     @classmethod
     def derive_seed(cls, seed, dst, binder):
-        return cls(seed, dst, binder).next(16)
+        return cls(seed, dst, binder).next(cls.SEED_SIZE)
 
     @classmethod
     def expand_into_vec(cls, field, seed, dst, binder, length):
         return cls(seed, dst, binder).next_vec(field, length)
+
+
+class XofHmacSha256Aes128(XofTurboShake128):
+    """prio 0.16.1 XofHmacSha256Aes128 (used by Janus core/src/vdaf.rs:8,173-199): tag =
+    HMAC-SHA256(seed, byte(len(dst)) || dst || binder); stream = AES-128-CTR keystream, key
+    tag[:16], initial counter block tag[16:], low 64 bits a big-endian counter (Ctr64BE)."""
+    SEED_SIZE = 32
+
+    def __init__(self, seed: bytes, dst: bytes, binder: bytes):
+        import hashlib
+        import hmac
+
+        from oracle.hpke_oracle import aes128_expand
+        tag = hmac.new(seed, bytes([len(dst)]) + dst + binder, hashlib.sha256).digest()
+        self.rk = aes128_expand(tag[:16])
+        self.iv_hi, self.ctr = tag[16:24], int.from_bytes(tag[24:], "big")
+        self.buf = b""
+
+    def next(self, length):
+        from oracle.hpke_oracle import aes128_encrypt_block
+        while len(self.buf) < length:
+            self.buf += aes128_encrypt_block(self.rk, self.iv_hi + self.ctr.to_bytes(8, "big"))
+            self.ctr = (self.ctr + 1) % (1 << 64)
+        out, self.buf = self.buf[:length], self.buf[length:]
+        return out
 
 
 # --------------------------------------------------------------------------- polynomials
@@ -230,7 +255,7 @@ def next_pow2(n):
 class Valid:
     """Circuits as in VDAF-08 §7.4 (and prio 0.16.1 flp::types)."""
 
-    def __init__(self, kind, bits=0, length=0, chunk=0):
+    def __init__(self, kind, bits=0, length=0, chunk=0, field=None):
         self.kind = kind
         if kind == "count":
             self.Field, self.GADGET, self.CALLS = Field64, Mul(), 1
@@ -239,7 +264,7 @@ class Valid:
             self.Field, self.GADGET, self.CALLS = Field128, Range2(), bits
             self.MEAS_LEN, self.OUTPUT_LEN, self.JOINT_RAND_LEN = bits, 1, 1
         elif kind == "sumvec":
-            self.Field, self.GADGET = Field128, ParallelSumMul(chunk)
+            self.Field, self.GADGET = field or Field128, ParallelSumMul(chunk)
             self.MEAS_LEN, self.OUTPUT_LEN, self.JOINT_RAND_LEN = bits * length, length, 1
             self.CALLS = (self.MEAS_LEN + chunk - 1) // chunk
         elif kind == "histogram":
@@ -358,109 +383,124 @@ class FlpGeneric:
 
 # --------------------------------------------------------------------------- Prio3
 
-ALGO_IDS = {"count": 0, "sum": 1, "sumvec": 2, "histogram": 3}
+ALGO_IDS = {"count": 0, "sum": 1, "sumvec": 2, "histogram": 3, "sumvec_f64_multiproof": 0xFFFF1003}
 USAGE = dict(meas_share=1, proof_share=2, joint_randomness=3, prove_randomness=4, query_randomness=5,
              joint_rand_seed=6, joint_rand_part=7)
 
 
 class Prio3:
     SHARES = 2
-    PROOFS = 1
 
-    def __init__(self, kind, **kw):
+    def __init__(self, kind, proofs=1, **kw):
+        self.ID = ALGO_IDS[kind]
+        self.Xof = XofTurboShake128
+        if kind == "sumvec_f64_multiproof":  # core/src/vdaf.rs:176-199
+            assert proofs >= 2
+            kind, kw["field"], self.Xof = "sumvec", Field64, XofHmacSha256Aes128
+        self.PROOFS = proofs
         self.valid = Valid(kind, **kw)
         self.flp = FlpGeneric(self.valid)
-        self.ID = ALGO_IDS[kind]
         self.F = self.valid.Field
+        self.S = self.Xof.SEED_SIZE
 
     def dst(self, usage):
         return bytes([8, 0]) + self.ID.to_bytes(4, "big") + USAGE[usage].to_bytes(2, "big")
 
     def helper_meas_share(self, agg_id, k):
-        return XofTurboShake128.expand_into_vec(self.F, k, self.dst("meas_share"), bytes([agg_id]),
+        return self.Xof.expand_into_vec(self.F, k, self.dst("meas_share"), bytes([agg_id]),
                                                 self.valid.MEAS_LEN)
 
     def helper_proofs_share(self, agg_id, k):
-        return XofTurboShake128.expand_into_vec(self.F, k, self.dst("proof_share"),
+        return self.Xof.expand_into_vec(self.F, k, self.dst("proof_share"),
                                                 bytes([self.PROOFS, agg_id]), self.valid.PROOF_LEN * self.PROOFS)
 
     def joint_rand_part(self, agg_id, blind, meas_share, nonce):
-        return XofTurboShake128.derive_seed(blind, self.dst("joint_rand_part"),
+        return self.Xof.derive_seed(blind, self.dst("joint_rand_part"),
                                             bytes([agg_id]) + nonce + self.F.encode_vec(meas_share))
 
     def joint_rand_seed(self, parts):
-        return XofTurboShake128.derive_seed(bytes(16), self.dst("joint_rand_seed"), b"".join(parts))
+        return self.Xof.derive_seed(bytes(self.S), self.dst("joint_rand_seed"), b"".join(parts))
 
     def joint_rands(self, seed):
-        return XofTurboShake128.expand_into_vec(self.F, seed, self.dst("joint_randomness"), bytes([self.PROOFS]),
+        return self.Xof.expand_into_vec(self.F, seed, self.dst("joint_randomness"), bytes([self.PROOFS]),
                                                 self.valid.JOINT_RAND_LEN * self.PROOFS)
 
     def query_rands(self, vk, nonce):
-        return XofTurboShake128.expand_into_vec(self.F, vk, self.dst("query_randomness"),
-                                                bytes([self.PROOFS]) + nonce, self.PROOFS)
+        return self.Xof.expand_into_vec(self.F, vk, self.dst("query_randomness"),
+                                        bytes([self.PROOFS]) + nonce, self.valid.QUERY_RAND_LEN * self.PROOFS)
 
     def shard(self, measurement, nonce, rand):
-        """rand = k_helper_meas || k_helper_proofs || k_prove || [blind_L || blind_H] (same as the C oracle)."""
-        p = self.F.p
-        k_hm, k_hp, k_prove = rand[0:16], rand[16:32], rand[32:48]
-        meas = self.valid.encode(measurement)
+        """rand = k_helper_meas || k_helper_proofs || k_prove || [blind_L || blind_H], SEED_SIZE each
+        (same layout as the C oracle)."""
+        p, S, V, NP = self.F.p, self.S, self.valid, self.PROOFS
+        k_hm, k_hp, k_prove = rand[0:S], rand[S:2 * S], rand[2 * S:3 * S]
+        meas = V.encode(measurement)
         hmeas = self.helper_meas_share(1, k_hm)
         lmeas = [(a - b) % p for a, b in zip(meas, hmeas)]
         jr, public = [], b""
-        if self.valid.JOINT_RAND_LEN:
-            bl, bh = rand[48:64], rand[64:80]
+        if V.JOINT_RAND_LEN:
+            bl, bh = rand[3 * S:4 * S], rand[4 * S:5 * S]
             pl = self.joint_rand_part(0, bl, lmeas, nonce)
             ph = self.joint_rand_part(1, bh, hmeas, nonce)
             jr = self.joint_rands(self.joint_rand_seed([pl, ph]))
             public = pl + ph
-        prove_rand = XofTurboShake128.expand_into_vec(self.F, k_prove, self.dst("prove_randomness"),
-                                                      bytes([self.PROOFS]), self.valid.PROVE_RAND_LEN)
-        proof = self.flp.prove(meas, prove_rand, jr)
+        prove_rands = self.Xof.expand_into_vec(self.F, k_prove, self.dst("prove_randomness"), bytes([NP]),
+                                               V.PROVE_RAND_LEN * NP)
+        proofs = []
+        for i in range(NP):
+            proofs += self.flp.prove(meas, prove_rands[i * V.PROVE_RAND_LEN:(i + 1) * V.PROVE_RAND_LEN],
+                                     jr[i * V.JOINT_RAND_LEN:(i + 1) * V.JOINT_RAND_LEN])
         hproof = self.helper_proofs_share(1, k_hp)
-        lproof = [(a - b) % p for a, b in zip(proof, hproof)]
+        lproof = [(a - b) % p for a, b in zip(proofs, hproof)]
         leader = self.F.encode_vec(lmeas) + self.F.encode_vec(lproof)
         helper = k_hm + k_hp
-        if self.valid.JOINT_RAND_LEN:
-            leader += rand[48:64]
-            helper += rand[64:80]
+        if V.JOINT_RAND_LEN:
+            leader += rand[3 * S:4 * S]
+            helper += rand[4 * S:5 * S]
         return public, leader, helper
 
     def prep_init(self, vk, agg_id, nonce, public_share, input_share):
-        V, F = self.valid, self.F
+        V, F, S, NP = self.valid, self.F, self.S, self.PROOFS
         if agg_id == 0:
             n = V.MEAS_LEN * F.ENCODED_SIZE
+            m = V.PROOF_LEN * NP * F.ENCODED_SIZE
             meas = F.decode_vec(input_share[:n])
-            proof = F.decode_vec(input_share[n:n + V.PROOF_LEN * F.ENCODED_SIZE])
-            blind = input_share[n + V.PROOF_LEN * F.ENCODED_SIZE:]
+            proof = F.decode_vec(input_share[n:n + m])
+            blind = input_share[n + m:]
         else:
-            meas = self.helper_meas_share(agg_id, input_share[:16])
-            proof = self.helper_proofs_share(agg_id, input_share[16:32])
-            blind = input_share[32:48]
+            meas = self.helper_meas_share(agg_id, input_share[:S])
+            proof = self.helper_proofs_share(agg_id, input_share[S:2 * S])
+            blind = input_share[2 * S:3 * S]
         out_share = V.truncate(meas)
         jr, corrected, part = [], None, b""
         if V.JOINT_RAND_LEN:
             part = self.joint_rand_part(agg_id, blind, meas, nonce)
-            parts = [public_share[0:16], public_share[16:32]]
+            parts = [public_share[0:S], public_share[S:2 * S]]
             parts[agg_id] = part
             corrected = self.joint_rand_seed(parts)
             jr = self.joint_rands(corrected)
         qr = self.query_rands(vk, nonce)
-        ver = self.flp.query(meas, proof, qr, jr, self.SHARES)
+        ver = []
+        for i in range(NP):
+            ver += self.flp.query(meas, proof[i * V.PROOF_LEN:(i + 1) * V.PROOF_LEN],
+                                  qr[i * V.QUERY_RAND_LEN:(i + 1) * V.QUERY_RAND_LEN],
+                                  jr[i * V.JOINT_RAND_LEN:(i + 1) * V.JOINT_RAND_LEN], self.SHARES)
         return (out_share, corrected), F.encode_vec(ver) + part
 
     def prep_shares_to_prep(self, shares):
-        V, F = self.valid, self.F
-        n = V.VERIFIER_LEN * F.ENCODED_SIZE
-        ver = [0] * V.VERIFIER_LEN
+        V, F, NP = self.valid, self.F, self.PROOFS
+        n = V.VERIFIER_LEN * NP * F.ENCODED_SIZE
+        ver = [0] * (V.VERIFIER_LEN * NP)
         parts = []
         for s in shares:
-            if len(s) != n + (16 if V.JOINT_RAND_LEN else 0):
+            if len(s) != n + (self.S if V.JOINT_RAND_LEN else 0):
                 raise ValueError("decode")
             v = F.decode_vec(s[:n])
             ver = [(a + b) % F.p for a, b in zip(ver, v)]
             parts.append(s[n:])
-        if not self.flp.decide(ver):
-            raise AssertionError("decide")
+        for i in range(NP):
+            if not self.flp.decide(ver[i * V.VERIFIER_LEN:(i + 1) * V.VERIFIER_LEN]):
+                raise AssertionError("decide")
         return self.joint_rand_seed(parts) if V.JOINT_RAND_LEN else b""
 
     def helper_prep(self, vk, nonce, public_share, helper_input_share, leader_prep_share):

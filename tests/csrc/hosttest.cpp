@@ -8,6 +8,7 @@
 #include "../../janus_amd/csrc/jx_keccak.h"
 #include "../../janus_amd/csrc/jx_sha256.h"
 #include "../../janus_amd/csrc/jx_hpke.h"
+#include "../../janus_amd/csrc/jx_sha_aes.h"
 
 using namespace jx;
 
@@ -182,4 +183,38 @@ void ht_xof_block(uint32_t algo, uint32_t usage, const uint8_t seed[16], const u
   blk_pad(b, pos + blen);
   memcpy(out, b.w, sizeof b.w);
 }
+// T-table AES of the XofHmacSha256Aes128 kernels (jx_sha_aes.h): otf = 0 expands the 44-word
+// schedule first, otf = 1 computes it on the fly
+void ht_aes128_t(int otf, const uint8_t key[16], const uint8_t in[16], uint8_t out[16]) {
+  ht_sbox_init();
+  static uint32_t t0[256];
+  for (int x = 0; x < 256; x++) t0[x] = aes_t0_entry(HT_SBOX[x]);
+  auto T = [&](uint32_t x) { return t0[x]; };
+  uint32_t k[4], rk[44], i4[4], o4[4];
+  memcpy(k, key, 16);
+  memcpy(i4, in, 16);
+  if (otf) {
+    aes128_encrypt_t_otf(T, k, i4, o4);
+  } else {
+    aes128_expand_key_t(T, k, rk);
+    aes128_encrypt_t(T, rk, i4, o4);
+  }
+  memcpy(out, o4, 16);
+}
+uint32_t ht_be_word_shift16(uint32_t lo, uint32_t hi) { return be_word_shift16(lo, hi); }
+// sum_k xs[k] * cs[k] mod p64 through the Field64 limb column accumulator (folding every 1024 terms)
+uint64_t ht_wacc64_dot(const uint64_t* xs, const uint64_t* cs, int n) {
+  wacc64 a;
+  wacc64_zero(a);
+  uint64_t acc = 0;
+  for (int k = 0; k < n; k++) {
+    wacc64_mac(a, xs[k], to_c64limbs(cs[k]));
+    if ((k + 1) % (int)WACC64_MAX_TERMS == 0) {
+      acc = add64(acc, wacc64_reduce(a));
+      wacc64_zero(a);
+    }
+  }
+  return add64(acc, wacc64_reduce(a));
+}
+uint64_t ht_reduce192_p64(const uint64_t w[3]) { return reduce192_p64(w[0], w[1], w[2]); }
 }

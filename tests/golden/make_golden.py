@@ -20,6 +20,7 @@ sys.path.insert(0, ROOT)
 from oracle import oracle as O  # noqa: E402
 
 VK = bytes(range(16))
+VK32 = bytes(range(32))  # VERIFY_KEY_LENGTH_HMACSHA256_AES128, core/src/vdaf.rs:24
 
 CONFIGS = {
     "count": dict(algo=O.COUNT, bits=0, length=0, chunk=0, n=12),
@@ -29,6 +30,14 @@ CONFIGS = {
     "sumvec_8x1000_88": dict(algo=O.SUMVEC, bits=8, length=1000, chunk=88, n=6),
     "histogram_16_4": dict(algo=O.HISTOGRAM, bits=0, length=16, chunk=4, n=12),
     "histogram_256_16": dict(algo=O.HISTOGRAM, bits=0, length=256, chunk=16, n=8),
+    # Prio3SumVecField64MultiproofHmacSha256Aes128: the parameter sets of Janus's own tests
+    # (integration_tests/tests/integration/janus.rs:369-374, taskprov_tests.rs:1266) and the
+    # headline SumVec shape with two and three proofs
+    "sumvec_f64mp_2_16x15_16": dict(algo=O.SUMVEC_F64_MULTIPROOF, bits=16, length=15, chunk=16, proofs=2, n=12),
+    "sumvec_f64mp_2_8x12_14": dict(algo=O.SUMVEC_F64_MULTIPROOF, bits=8, length=12, chunk=14, proofs=2, n=12),
+    "sumvec_f64mp_3_1x7_3": dict(algo=O.SUMVEC_F64_MULTIPROOF, bits=1, length=7, chunk=3, proofs=3, n=12),
+    "sumvec_f64mp_2_8x1000_88": dict(algo=O.SUMVEC_F64_MULTIPROOF, bits=8, length=1000, chunk=88, proofs=2, n=6),
+    "sumvec_f64mp_3_8x1000_88": dict(algo=O.SUMVEC_F64_MULTIPROOF, bits=8, length=1000, chunk=88, proofs=3, n=6),
 }
 
 
@@ -65,8 +74,10 @@ def tamper(lps: np.ndarray, sizes: O.Sizes, rng) -> list[str]:
 
 def make(name, cfg):
     rng = np.random.default_rng(sum(map(ord, name)) * 7919)
-    orc = O.Prio3Oracle(cfg["algo"], cfg["bits"], cfg["length"], cfg["chunk"])
+    proofs = cfg.get("proofs", 1)
+    orc = O.Prio3Oracle(cfg["algo"], cfg["bits"], cfg["length"], cfg["chunk"], proofs)
     s = orc.sizes
+    VK = VK32 if s.verify_key == 32 else bytes(range(16))
     n = cfg["n"]
     meas = measurements(cfg, rng, n)
     nonces = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
@@ -98,7 +109,7 @@ def make(name, cfg):
         "generator": "tests/golden/make_golden.py (C oracle oracle/prio3_oracle.c)",
         "parity": "pins GPU == C oracle == pyref; parity with prio 0.16.1 unpinned (SURVEY.md 8c)",
         "vdaf": {"algo_id": cfg["algo"], "bits": cfg["bits"], "length": cfg["length"],
-                 "chunk_length": cfg["chunk"], "num_proofs": 1},
+                 "chunk_length": cfg["chunk"], "num_proofs": proofs},
         "verify_key": VK.hex(),
         "sizes": s.__dict__,
         "reports": reports,

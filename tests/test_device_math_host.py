@@ -21,7 +21,7 @@ def ht():
     src = os.path.join(HERE, "csrc", "hosttest.cpp")
     so = os.path.join(HERE, "csrc", "libjx_hosttest.so")
     hdrs = [os.path.join(HERE, "..", "janus_amd", "csrc", h) for h in ("jx_field.h", "jx_keccak.h", "jx_sha256.h",
-                                                                         "jx_hpke.h")]
+                                                                         "jx_hpke.h", "jx_sha_aes.h")]
     if not os.path.exists(so) or any(os.path.getmtime(h) > os.path.getmtime(so) for h in hdrs + [src]):
         subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", so, src], check=True)
     L = ctypes.CDLL(so)
@@ -40,6 +40,13 @@ def ht():
     L.ht_keccak_p12.argtypes = [vp]
     L.ht_sha256_16.argtypes = [vp, vp]
     L.ht_xof_block.argtypes = [ctypes.c_uint32, ctypes.c_uint32, vp, vp, ctypes.c_int, vp]
+    L.ht_aes128_t.argtypes = [ctypes.c_int, vp, vp, vp]
+    L.ht_be_word_shift16.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    L.ht_be_word_shift16.restype = ctypes.c_uint32
+    L.ht_wacc64_dot.argtypes = [vp, vp, ctypes.c_int]
+    L.ht_wacc64_dot.restype = ctypes.c_uint64
+    L.ht_reduce192_p64.argtypes = [vp]
+    L.ht_reduce192_p64.restype = ctypes.c_uint64
     return L
 
 
@@ -219,3 +226,52 @@ def test_aes_ghash_hmac_vs_oracle(ht):
         key, msg = rnd.randbytes(32), rnd.randbytes(n)
         ht.ht_hmac32(key, msg, n, out)
         assert out.raw == hm.new(key, msg, hashlib.sha256).digest(), n
+
+
+# ---- XofHmacSha256Aes128 / Field64 multiproof building blocks (jx_sha_aes.h, jx_field.h)
+
+def test_aes128_ttable_fips197(ht):
+    """T-table AES (both key-schedule forms) against the FIPS 197 Appendix C.1 vector and the oracle."""
+    from oracle import oracle as O
+    key, pt = bytes.fromhex("000102030405060708090a0b0c0d0e0f"), bytes.fromhex("00112233445566778899aabbccddeeff")
+    rnd = random.Random(9)
+    cases = [(key, pt, bytes.fromhex("69c4e0d86a7b0430d8cdb78070b4c55a"))]
+    for _ in range(20):
+        k, m = rnd.randbytes(16), rnd.randbytes(16)
+        cases.append((k, m, O.aes128_encrypt(k, m)))
+    for k, m, want in cases:
+        for otf in (0, 1):
+            out = ctypes.create_string_buffer(16)
+            ht.ht_aes128_t(otf, k, m, out)
+            assert out.raw == want, (otf, k.hex())
+
+
+def test_be_word_shift16(ht):
+    rnd = random.Random(3)
+    for _ in range(100):
+        lo, hi = rnd.getrandbits(32), rnd.getrandbits(32)
+        b = lo.to_bytes(4, "little") + hi.to_bytes(4, "little")
+        assert ht.ht_be_word_shift16(lo, hi) == int.from_bytes(b[2:6], "big")
+
+
+@pytest.mark.parametrize("n", [1, 91, 1023, 1024, 1025, 3000])
+def test_wacc64_dot(ht, n):
+    rnd = random.Random(n)
+    edge = [0, 1, P64 - 1, P64 - 2, 2**63, 2**32, 2**32 - 1]
+    xs = [rnd.choice(edge) if rnd.random() < 0.3 else rnd.randrange(P64) for _ in range(n)]
+    cs = [rnd.choice(edge) if rnd.random() < 0.3 else rnd.randrange(P64) for _ in range(n)]
+    if n == 1024:  # worst case for the column bound
+        xs, cs = [P64 - 1] * n, [P64 - 1] * n
+    ax = (ctypes.c_uint64 * n)(*xs)
+    ac = (ctypes.c_uint64 * n)(*cs)
+    assert ht.ht_wacc64_dot(ax, ac, n) == sum(x * c for x, c in zip(xs, cs)) % P64
+
+
+def test_reduce192_p64(ht):
+    rnd = random.Random(5)
+    for _ in range(200):
+        w = [rnd.getrandbits(64) for _ in range(3)]
+        if rnd.random() < 0.2:
+            w = [2**64 - 1] * 3
+        a = (ctypes.c_uint64 * 3)(*w)
+        assert ht.ht_reduce192_p64(a) == (w[0] + (w[1] << 64) + (w[2] << 128)) % P64

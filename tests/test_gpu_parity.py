@@ -19,12 +19,13 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.json")))
+GOLDEN = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.json"))
+                if not os.path.basename(p).startswith("hpke"))
 
 
 def _vdaf(doc) -> Prio3:
     v = doc["vdaf"]
-    return Prio3(v["algo_id"], v["bits"], v["length"], v["chunk_length"])
+    return Prio3(v["algo_id"], v["bits"], v["length"], v["chunk_length"], v.get("num_proofs", 1))
 
 
 def _arrays(doc):
@@ -63,7 +64,7 @@ def test_golden(path, slow):
 def _random_batch(orc: O.Prio3Oracle, vk, n, seed, tamper_every=7):
     rng = np.random.default_rng(seed)
     a, (algo, bits, length, chunk, _) = orc.algo, orc.params
-    if a == O.SUMVEC:
+    if a in (O.SUMVEC, O.SUMVEC_F64_MULTIPROOF):
         meas = rng.integers(0, 1 << bits, size=(n, length), dtype=np.uint64)
     elif a == O.SUM:
         meas = rng.integers(0, 1 << bits, size=(n, 1), dtype=np.uint64)

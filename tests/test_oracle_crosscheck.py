@@ -78,3 +78,57 @@ def test_invalid_measurement_rejected():
     _, lshare = Py.prep_init(vk, 0, nonce, ps, bad_lin)
     assert Py.helper_prep(vk, nonce, ps, hin, lshare)[0] in (3, 4)
     assert C.helper_prep(vk, nonce, ps, hin, lshare)[0] == Py.helper_prep(vk, nonce, ps, hin, lshare)[0]
+
+
+# ---- Prio3SumVecField64MultiproofHmacSha256Aes128 (core/src/vdaf.rs:173-199)
+
+MP_CFGS = [(2, 16, 15, 16), (2, 8, 12, 14), (3, 1, 7, 3), (2, 2, 5, 3)]
+
+
+def test_xof_hmac_sha256_aes128_c_equals_python():
+    """The two restatements of XofHmacSha256Aes128 agree (C: own SHA-256/HMAC/AES; Python:
+    hashlib/hmac + the AES of oracle/hpke_oracle.py, itself pinned by RFC 9180's AES-GCM vector),
+    including a counter that wraps its low 64 bits (Ctr64BE)."""
+    rng = random.Random(4)
+    for n in (0, 1, 16, 17, 100, 1000):
+        seed, dst, binder = rng.randbytes(32), rng.randbytes(8), rng.randbytes(rng.randrange(40))
+        assert O.xof_hmac_aes(seed, dst, binder, n) == pyref.XofHmacSha256Aes128(seed, dst, binder).next(n)
+    # Ctr64BE: the low 64 bits of the counter block wrap without carrying into the high half
+    x = pyref.XofHmacSha256Aes128(bytes(32), b"d", b"")
+    x.ctr = 2**64 - 1
+    hi = x.iv_hi
+    a = x.next(32)
+    assert x.ctr == 1 and x.iv_hi == hi and len(a) == 32
+
+
+@pytest.mark.parametrize("cfg", MP_CFGS, ids=[f"p{c[0]}_{c[1]}x{c[2]}_{c[3]}" for c in MP_CFGS])
+def test_multiproof_c_oracle_equals_pyref(cfg):
+    proofs, bits, length, chunk = cfg
+    rng = random.Random(sum(cfg))
+    C = O.Prio3Oracle(O.SUMVEC_F64_MULTIPROOF, bits, length, chunk, proofs)
+    Py = pyref.Prio3("sumvec_f64_multiproof", proofs=proofs, bits=bits, length=length, chunk=chunk)
+    assert (C.sizes.seed, C.sizes.verify_key, C.sizes.field_bytes) == (32, 32, 8)
+    vk = rng.randbytes(32)
+    for _ in range(2):
+        nonce = rng.randbytes(16)
+        rand = rng.randbytes(C.sizes.client_rand)
+        m = [rng.randrange(1 << bits) for _ in range(length)]
+        shard = C.shard(m, nonce, rand)
+        assert shard == Py.shard(m, nonce, rand)
+        ps, lin, hin = shard
+        rc, lshare, lout, _ = C.prep_init(vk, 0, nonce, ps, lin)
+        assert rc == 0 and lshare == Py.prep_init(vk, 0, nonce, ps, lin)[1]
+        got = C.helper_prep(vk, nonce, ps, hin, lshare)
+        assert got == Py.helper_prep(vk, nonce, ps, hin, lshare) and got[0] == 0
+        agg = C.aggregate([lout, got[2]])
+        assert [int.from_bytes(agg[i:i + 8], "little") for i in range(0, len(agg), 8)] == m
+        for byte in range(0, len(lshare), max(1, len(lshare) // 7)):
+            t = bytearray(lshare)
+            t[byte] ^= 1 << rng.randrange(8)
+            v = C.helper_prep(vk, nonce, ps, hin, bytes(t))[0]
+            assert v == Py.helper_prep(vk, nonce, ps, hin, bytes(t))[0] and v in (2, 3, 4)
+
+
+def test_multiproof_rejects_single_proof():
+    with pytest.raises(ValueError):
+        O.Prio3Oracle(O.SUMVEC_F64_MULTIPROOF, 8, 12, 14, 1)
