@@ -13,6 +13,9 @@ SOURCES = [os.path.join(_HERE, "csrc", f) for f in ("jx_kernels.hip", "jx_engine
 HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("jx_field.h", "jx_keccak.h", "jx_sha256.h", "jx_kernels.h",
                                                   "jx_hpke.h", "jx_sha_aes.h")]
 OUT = os.path.join(_HERE, "lib", "libjanus_prio3.so")
+# jx_mp64.hip: keep the LDS for the AES table (the AMDGPU backend would otherwise move a small private
+# array of the out-of-line helpers into LDS, +16 KiB per workgroup, one workgroup less per CU)
+EXTRA_FLAGS = {"jx_mp64.hip": ["-mllvm", "-disable-promote-alloca-to-lds"]}
 ARCH = os.environ.get("JX_OFFLOAD_ARCH", "gfx950")
 
 
@@ -35,6 +38,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     for src in SOURCES:
         obj = os.path.join(os.path.dirname(OUT), os.path.basename(src) + ".o")
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-x", "hip", "-c", src, "-o", obj]
+        cmd += EXTRA_FLAGS.get(os.path.basename(src), [])
         procs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), cmd))
         objs.append(obj)
     for p, cmd in procs:

@@ -33,6 +33,14 @@ struct f128 {
   uint64_t lo, hi;
 };
 
+// 3-input XOR and majority: one v_bitop3_b32 each on gfx950 (the compiler does not always fuse them)
+#if defined(__HIP_DEVICE_COMPILE__)
+JX_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+JX_HD uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8); }
+#else
+JX_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return a ^ b ^ c; }
+JX_HD uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) { return (a & b) ^ (a & c) ^ (b & c); }
+#endif
 JX_HD uint32_t lo32(uint64_t v) { return (uint32_t)v; }
 JX_HD uint32_t hi32(uint64_t v) { return (uint32_t)(v >> 32); }
 

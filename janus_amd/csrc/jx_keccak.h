@@ -89,11 +89,6 @@ JX_HD void rho_pi_all(const uint32_t* A, uint32_t* B, IndexSeq<Is...>) {
   (rho_pi_one<Is>(A, B), ...);
 }
 
-#if defined(__HIP_DEVICE_COMPILE__)
-JX_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
-#else
-JX_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return a ^ b ^ c; }
-#endif
 
 // One round of Keccak-f[1600] on a state of 25 (lo, hi) lanes: theta's 5-way column parity
 // is two 3-input XORs (v_bitop3_b32 0x96) per word, rho is two v_alignbit_b32 per lane,

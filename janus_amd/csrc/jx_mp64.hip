@@ -28,17 +28,70 @@ namespace jx {
 
 namespace {
 
-constexpr uint32_t TT_COPIES = 32;
 constexpr uint32_t USAGE_MEAS = 1, USAGE_PROOF = 2, USAGE_JR = 3, USAGE_QR = 5, USAGE_JR_SEED = 6,
                    USAGE_JR_PART = 7;
 
+// AES tables in LDS (128 KiB): T_t[x] = rotl(T0[x], 8t), T0[x] = (2s, s, s, 3s), t = 0..3, each in 32
+// copies; lane l reads copy l mod 32, which sits in bank l mod 32, so every ds_read_b32 of a wave is
+// conflict-free. Lane l's copy of T_t[x] is at byte (t >> 1) << 16 | x << 8 | (t & 1) << 7 | 4 (l mod
+// 32): one v_perm_b32 merges the state byte (-> bits 8..15) with the lane's per-table address word
+// a_t. A MixColumns column is four lookups (four perms) and two 3-input XORs.
+constexpr uint32_t TT_WORDS = 4 * 256 * 32;
 struct TTab {
-  const uint32_t* p;  // this lane's copy of T0
-  __device__ __forceinline__ uint32_t operator()(uint32_t x) const { return p[x * TT_COPIES]; }
+  const uint8_t* base;  // the tables (LDS)
+  uint32_t a0;          // 4 (lane mod 32)
+  // T0[x] (key schedule, one-off blocks)
+  __device__ __forceinline__ uint32_t operator()(uint32_t x) const {
+    return *reinterpret_cast<const uint32_t*>(base + ((x << 8) | a0));
+  }
 };
+__device__ __forceinline__ TTab ttab(const uint32_t* tt, uint32_t lane) {
+  return TTab{reinterpret_cast<const uint8_t*>(tt), 4u * (lane & 31u)};
+}
 
 __device__ __forceinline__ void tt_fill(uint32_t* tt) {
-  for (uint32_t i = threadIdx.x; i < 256 * TT_COPIES; i += blockDim.x) tt[i] = aes_t0_entry(AES_SBOX[i / TT_COPIES]);
+  for (uint32_t i = threadIdx.x; i < TT_WORDS; i += blockDim.x) {
+    const uint32_t t = 2 * (i >> 14) + ((i >> 5) & 1u);
+    const uint32_t t0 = aes_t0_entry(AES_SBOX[(i >> 6) & 255u]);
+    tt[i] = t ? rotl32(t0, 8 * t) : t0;
+  }
+}
+// T_t of byte K of s
+template <int t, int K>
+__device__ __forceinline__ uint32_t lt(const TTab& T, uint32_t s) {
+  const uint32_t a = T.a0 | ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) << 7);
+  return *reinterpret_cast<const uint32_t*>(T.base + __builtin_amdgcn_perm(s, a, 0x0C020000u | ((4u + K) << 8)));
+}
+// one MixColumns output column from state columns (a, b, c, d) = (c, c+1, c+2, c+3)
+__device__ __forceinline__ uint32_t aes_col(const TTab& T, uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                                            uint32_t k) {
+  return xor3(xor3(lt<0, 0>(T, a), lt<1, 1>(T, b), lt<2, 2>(T, c)), lt<3, 3>(T, d), k);
+}
+// last round: S[x] is byte 1 and byte 2 of T0[x] and byte 3 of T1[x]
+__device__ __forceinline__ uint32_t aes_col_last(const TTab& T, uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                                                 uint32_t k) {
+  const uint32_t lo = __builtin_amdgcn_perm(lt<0, 1>(T, b), lt<0, 0>(T, a), 0x0C0C0501u);
+  const uint32_t hi = __builtin_amdgcn_perm(lt<1, 3>(T, d), lt<0, 2>(T, c), 0x07020C0Cu);
+  return (lo | hi) ^ k;
+}
+__device__ __forceinline__ void aes_enc_fast(const TTab& T, const uint32_t rk[44], const uint32_t in[4],
+                                             uint32_t out[4]) {
+  uint32_t s0 = in[0] ^ rk[0], s1 = in[1] ^ rk[1], s2 = in[2] ^ rk[2], s3 = in[3] ^ rk[3];
+#pragma unroll
+  for (int r = 1; r < 10; r++) {
+    const uint32_t t0 = aes_col(T, s0, s1, s2, s3, rk[4 * r]);
+    const uint32_t t1 = aes_col(T, s1, s2, s3, s0, rk[4 * r + 1]);
+    const uint32_t t2 = aes_col(T, s2, s3, s0, s1, rk[4 * r + 2]);
+    const uint32_t t3 = aes_col(T, s3, s0, s1, s2, rk[4 * r + 3]);
+    s0 = t0;
+    s1 = t1;
+    s2 = t2;
+    s3 = t3;
+  }
+  out[0] = aes_col_last(T, s0, s1, s2, s3, rk[40]);
+  out[1] = aes_col_last(T, s1, s2, s3, s0, rk[41]);
+  out[2] = aes_col_last(T, s2, s3, s0, s1, rk[42]);
+  out[3] = aes_col_last(T, s3, s0, s1, s2, rk[43]);
 }
 
 __device__ __forceinline__ uint64_t u2v(uint2 v) { return (uint64_t)v.x | ((uint64_t)v.y << 32); }
@@ -111,8 +164,8 @@ __device__ __forceinline__ void sha_blk(uint32_t st[8], const uint32_t* w) {
 #pragma unroll
   for (int i = 0; i < 8; i++) st[i] = x.s[i];
 }
-__device__ __noinline__ uint4 aes_call(const uint32_t* tp, uint4 key, uint4 in) {
-  const TTab T{tp};
+__device__ __noinline__ uint4 aes_call(const uint8_t* base, uint32_t a0, uint4 key, uint4 in) {
+  const TTab T{base, a0};
   const uint32_t k[4] = {key.x, key.y, key.z, key.w}, x[4] = {in.x, in.y, in.z, in.w};
   uint32_t o[4];
   aes128_encrypt_t_otf(T, k, x, o);
@@ -178,13 +231,13 @@ __device__ __forceinline__ void ctr_init(Ctr& s, const TTab& T, const uint32_t t
 }
 __device__ __forceinline__ void ctr_next(Ctr& s, const TTab& T, uint32_t out[4]) {
   const uint32_t in[4] = {s.iv0, s.iv1, bswap32(hi32(s.ctr)), bswap32(lo32(s.ctr))};
-  aes128_encrypt_t(T, s.rk, in, out);
+  aes_enc_fast(T, s.rk, in, out);
   s.ctr++;
 }
 // block j of the stream of tag, one-off
 __device__ __forceinline__ uint4 ctr_block_c(const TTab& T, const uint32_t tag[8], uint64_t j) {
   const uint64_t ctr = (((uint64_t)tag[6] << 32) | tag[7]) + j;
-  return aes_call(T.p, make_uint4(bswap32(tag[0]), bswap32(tag[1]), bswap32(tag[2]), bswap32(tag[3])),
+  return aes_call(T.base, T.a0, make_uint4(bswap32(tag[0]), bswap32(tag[1]), bswap32(tag[2]), bswap32(tag[3])),
                   make_uint4(bswap32(tag[4]), bswap32(tag[5]), bswap32(hi32(ctr)), bswap32(lo32(ctr))));
 }
 // the first 32 bytes of the stream (Xof::into_seed), as 8 little-endian words
@@ -257,44 +310,60 @@ __device__ __forceinline__ void jr_part_header(const Cfg& c, uint32_t agg_id, co
   hv[6] = nonce[3];
 }
 
-// Runs the inner SHA-256 of the joint_rand_part HMAC over the share; chunk(q, K) supplies the 16
-// little-endian words of share bytes [64q, 64q + 64) (any side effects: storing, truncating).
-// J: inner state after the key block on entry, the inner digest on return.
-template <class ChunkFn>
-__device__ __forceinline__ void jr_part_inner(const Cfg& c, uint32_t J[8], const uint32_t hv[7], ChunkFn&& chunk) {
+// Runs the inner SHA-256 of the joint_rand_part HMAC over the share. gen(q, K) supplies the 16
+// little-endian words of share bytes [64q, 64q + 64); emit(q, K) does the side effects on them
+// (store, truncate, screen). J: inner state after the key block on entry, the digest on return.
+// Software-pipelined: chunk q + 1 is generated in the same basic block as the compression of
+// block q, so the AES lookups in LDS fill the SHA-256 dependency chains.
+template <class GenFn, class EmitFn>
+__device__ __forceinline__ void jr_part_inner(const Cfg& c, uint32_t J[8], const uint32_t hv[7], GenFn&& gen,
+                                              EmitFn&& emit) {
   const uint32_t M = c.meas_len;
   const uint32_t NC = (M + 7) / 8;
   const uint32_t Lmsg = 26 + 8 * M;
+  const uint32_t nfull = Lmsg / 64;  // blocks made only of message bytes (NC - 1 or NC)
   uint32_t prev[7], cur[16];
 #pragma unroll
   for (int i = 0; i < 7; i++) prev[i] = hv[i];
+  gen(0, cur);
+  const uint32_t qs = NC - 1;  // nfull is NC - 1 or NC
+  uint32_t q = 0;
 #pragma unroll 1
-  for (uint32_t q = 0; q < NC; q++) {
-    if (q > 0) {
+  for (; q < qs; q++) {
+    emit(q, cur);  // branchy (uniform) side effects first; generation and hashing share a block
+    uint32_t nxt[16];
+    gen(q + 1, nxt);
+    uint32_t W[16];
 #pragma unroll
-      for (int i = 0; i < 7; i++) prev[i] = cur[9 + i];
+    for (int i = 0; i < 16; i++) {
+      const uint32_t lo = i < 7 ? prev[i] : cur[i - 7];
+      const uint32_t hi = i < 6 ? prev[i + 1] : cur[i - 6];
+      W[i] = be_word_shift16(lo, hi);
     }
-    chunk(q, cur);
-    if (64 * q + 64 <= Lmsg) {
-      uint32_t W[16];
+    sha256_compress(J, W);
 #pragma unroll
-      for (int i = 0; i < 16; i++) {
-        const uint32_t lo = i < 7 ? prev[i] : cur[i - 7];
-        const uint32_t hi = i < 6 ? prev[i + 1] : cur[i - 6];
-        W[i] = be_word_shift16(lo, hi);
-      }
-      sha256_compress(J, W);
-    }
+    for (int i = 0; i < 7; i++) prev[i] = cur[9 + i];
+#pragma unroll
+    for (int i = 0; i < 16; i++) cur[i] = nxt[i];
   }
-  // the first block that is not all message bytes, then padding and the bit length of
-  // (key block || message)
-  const uint32_t mstar = (64 * NC <= Lmsg) ? NC : NC - 1;
-  if (mstar == NC) {
+  emit(q, cur);
+  if (q < nfull) {  // the last chunk's block is full too
+    uint32_t W[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const uint32_t lo = i < 7 ? prev[i] : cur[i - 7];
+      const uint32_t hi = i < 6 ? prev[i + 1] : cur[i - 6];
+      W[i] = be_word_shift16(lo, hi);
+    }
+    sha_blk(J, W);
 #pragma unroll
     for (int i = 0; i < 7; i++) prev[i] = cur[9 + i];
 #pragma unroll
     for (int i = 0; i < 16; i++) cur[i] = 0;
   }
+  // block mstar (the first that is not all message bytes): the tail, padding, and the bit length
+  // of (key block || message)
+  const uint32_t mstar = nfull;
   const int rem = (int)(Lmsg - 64 * mstar);  // message bytes in block mstar, 0..63
   uint32_t W[16];
 #pragma unroll
@@ -467,18 +536,20 @@ __device__ uint32_t mp_tail(const Cfg& c, const Bufs& b, const TTab& T, uint64_t
 // HELPER (agg_id 1, aggregator.rs:1947): shares expanded from the 32-byte seeds of the helper input
 // share (k_meas || k_proofs || k_blind). LEADER (agg_id 0, aggregation_job_driver.rs:345): explicit
 // shares (meas || proofs || k_blind), decoded here (elements >= p fail prepare_init).
+// MP_XOF_WAVES waves per workgroup share the 128 KiB of tables; one workgroup per CU
+constexpr uint32_t MP_XOF_WAVES = 8;
 template <bool LEADER>
-__global__ __launch_bounds__(256) void mp_xof_kernel(Cfg c, Bufs b) {
-  __shared__ uint32_t tt[256 * TT_COPIES];
+__global__ __launch_bounds__(64 * MP_XOF_WAVES) void mp_xof_kernel(Cfg c, Bufs b) {
+  __shared__ uint32_t tt[TT_WORDS];
   tt_fill(tt);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t blk = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t blk = (uint64_t)blockIdx.x * MP_XOF_WAVES + (threadIdx.x >> 6);
   const uint64_t nblk = (b.n + 63) / 64;
   if (blk >= nblk) return;
   const uint64_t r0 = blk * 64 + lane;
   const uint64_t r = r0 < b.n ? r0 : b.n - 1;
-  const TTab T{tt + (lane & 31)};
+  const TTab T = ttab(tt, lane);
   const uint32_t M = c.meas_len, MB = 8 * M, NPL = c.np * c.proof_len;
   const uint8_t* hs = LEADER ? nullptr : b.his + (uint64_t)c.his_bytes * r;
   const uint8_t* ls = LEADER ? b.lis + (uint64_t)c.lis_bytes * r : nullptr;
@@ -508,33 +579,44 @@ __global__ __launch_bounds__(256) void mp_xof_kernel(Cfg c, Bufs b) {
     hmac_tag(tag, ist, ost, m, pos + 1);
     Ctr sm;
     ctr_init(sm, T, tag);
-    jr_part_inner(c, J, hv, [&](uint32_t q, uint32_t K[16]) {
+    jr_part_inner(
+        c, J, hv,
+        [&](uint32_t, uint32_t K[16]) {
 #pragma unroll
-      for (int a = 0; a < 4; a++) ctr_next(sm, T, K + 4 * a);
+          for (int a = 0; a < 4; a++) ctr_next(sm, T, K + 4 * a);
+        },
+        [&](uint32_t q, const uint32_t K[16]) {
 #pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const uint32_t e = 8 * q + i;
-        if (e < M) {
-          bad |= ge_p64(K[2 * i], K[2 * i + 1]);
-          emit64(c, mp, op, e, K[2 * i], K[2 * i + 1], tr);
-        }
-      }
-    });
+          for (int i = 0; i < 8; i++) {
+            const uint32_t e = 8 * q + i;
+            if (e < M) {
+              bad |= ge_p64(K[2 * i], K[2 * i + 1]);
+              emit64(c, mp, op, e, K[2 * i], K[2 * i + 1], tr);
+            }
+          }
+        });
   } else {
-    jr_part_inner(c, J, hv, [&](uint32_t q, uint32_t K[16]) {
+    jr_part_inner(
+        c, J, hv,
+        [&](uint32_t q, uint32_t K[16]) {
 #pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const uint32_t e = 8 * q + i;
-        uint2 v = make_uint2(0, 0);
-        if (e < M) {
-          v = *reinterpret_cast<const uint2*>(ls + 8ull * e);
-          bad |= ge_p64(v.x, v.y);
-          emit64(c, mp, op, e, v.x, v.y, tr);
-        }
-        K[2 * i] = v.x;
-        K[2 * i + 1] = v.y;
-      }
-    });
+          for (int i = 0; i < 8; i++) {
+            const uint32_t e = 8 * q + i;
+            const uint2 v = e < M ? *reinterpret_cast<const uint2*>(ls + 8ull * e) : make_uint2(0, 0);
+            K[2 * i] = v.x;
+            K[2 * i + 1] = v.y;
+          }
+        },
+        [&](uint32_t q, const uint32_t K[16]) {
+#pragma unroll
+          for (int i = 0; i < 8; i++) {
+            const uint32_t e = 8 * q + i;
+            if (e < M) {
+              bad |= ge_p64(K[2 * i], K[2 * i + 1]);
+              emit64(c, mp, op, e, K[2 * i], K[2 * i + 1], tr);
+            }
+          }
+        });
   }
   uint32_t own[8];
   {
@@ -592,7 +674,7 @@ __global__ __launch_bounds__(256) void mp_xof_kernel(Cfg c, Bufs b) {
 // ---------------------------------------------------------------------------- K1' (helper)
 // Exact recomputation with rejection sampling for the reports K1 flagged (or all, force_slow).
 __global__ __launch_bounds__(64) void mp_slow_kernel(Cfg c, Bufs b) {
-  __shared__ uint32_t tt[256 * TT_COPIES];
+  __shared__ uint32_t tt[TT_WORDS];
   const uint32_t lane = threadIdx.x;
   const uint64_t blk = blockIdx.x;
   const uint64_t r = blk * 64 + lane;
@@ -601,7 +683,7 @@ __global__ __launch_bounds__(64) void mp_slow_kernel(Cfg c, Bufs b) {
   tt_fill(tt);
   __syncthreads();
   if (!mine) return;
-  const TTab T{tt + (lane & 31)};
+  const TTab T = ttab(tt, lane);
   const uint32_t M = c.meas_len, NPL = c.np * c.proof_len;
   const uint8_t* hs = b.his + (uint64_t)c.his_bytes * r;
   uint2* const mp = reinterpret_cast<uint2*>(b.meas) + (blk * M) * IL + lane;
@@ -652,15 +734,18 @@ __global__ __launch_bounds__(64) void mp_slow_kernel(Cfg c, Bufs b) {
   load32(hs + 64, kb);
   hmac_key_le(kb, J, Jo);
   jr_part_header(c, 1, nonce, hv);
-  jr_part_inner(c, J, hv, [&](uint32_t q, uint32_t K[16]) {
+  jr_part_inner(
+      c, J, hv,
+      [&](uint32_t q, uint32_t K[16]) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const uint32_t e = 8 * q + i;
-      const uint2 v = e < M ? mp[(uint64_t)e * IL] : make_uint2(0, 0);
-      K[2 * i] = v.x;
-      K[2 * i + 1] = v.y;
-    }
-  });
+        for (int i = 0; i < 8; i++) {
+          const uint32_t e = 8 * q + i;
+          const uint2 v = e < M ? mp[(uint64_t)e * IL] : make_uint2(0, 0);
+          K[2 * i] = v.x;
+          K[2 * i + 1] = v.y;
+        }
+      },
+      [](uint32_t, const uint32_t*) {});
   uint32_t own[8];
   {
     uint32_t tag[8];
@@ -677,140 +762,175 @@ __device__ __forceinline__ uint64_t ld_lead64(const Bufs& b, const Cfg& c, uint6
   return u2v(v);
 }
 
-// One wave per (64-report block, group of PPW chunk slots, proof). For its slots it forms the
-// wire sums E_i = sum_k d_k x_{k,i} and O_i = sum_k c_k x_{k,i} as limb column sums, the wires at
-// t (leader: written into its prep share), sum_i Ve_i Vo_i over the slots with the leader's shares
-// added (helper), and its share of v = sum_m g_m S_m and of G(t).
+// One wave per (64-report block, group of PPW chunk slots, pair of proofs): the measurement
+// elements are read once for both proofs (the share is the kernel's dominant HBM stream). For its
+// slots and proofs it forms the wire sums E = sum_k d_k x_{k,i} and O = sum_k c_k x_{k,i} as limb
+// column sums, the wires at t (leader: written into its prep share), sum_i Ve_i Vo_i over the slots
+// with the leader's shares added (helper), and its share of v = sum_m g_m S_m and of G(t).
 template <int PPW, bool LEADER>
-__global__ __launch_bounds__(64, 4) void mp_flp_part_kernel(Cfg c, Bufs b) {
-  const uint32_t NG = c.ngroups, NP = c.np, U = NG * NP;
+__global__ __launch_bounds__(64, 3) void mp_flp_part_kernel(Cfg c, Bufs b) {
+  constexpr int NPW = 2;
+  const uint32_t NG = c.ngroups, NP = c.np, NPG = (NP + NPW - 1) / NPW, U = NG * NPG;
   // XCD-aware: the U waves of one block run back to back on one XCD (shared L2 for the
-  // measurement share and the leader's share)
+  // coefficients and the leader's share)
   const uint32_t bid = blockIdx.x;
   const uint32_t xcd = bid & 7u, q = bid >> 3;
   const uint32_t u = q % U;
   const uint64_t blk = (uint64_t)(q / U) * 8 + xcd;
   const uint64_t nblk = (b.n + 63) / 64;
   if (blk >= nblk) return;
-  const uint32_t g = u % NG, p = u / NG;
+  const uint32_t g = u % NG, p0 = (u / NG) * NPW;
+  const bool two = p0 + 1 < NP;  // wave-uniform
   const uint32_t lane = threadIdx.x;
   const uint64_t r0 = blk * 64 + lane;
   const uint64_t r = r0 < b.n ? r0 : b.n - 1;
   const uint32_t C = c.calls, chunk = c.chunk, M = c.meas_len, A = 2 * chunk, PL = c.proof_len, VL = c.ver_len;
   const uint32_t j0 = g * PPW;
-  const uint2* coefb = reinterpret_cast<const uint2*>(b.coef) + ((blk * NP + p) * c.nco) * IL + lane;
-  const uint2* measb = reinterpret_cast<const uint2*>(b.meas) + (blk * M) * IL + lane;
-  const uint2* proofb = reinterpret_cast<const uint2*>(b.proof) + (blk * NP * PL + (uint64_t)p * PL) * IL + lane;
-
-  wacc64 ae[PPW], ao[PPW];
-  uint64_t E[PPW], O[PPW];
+  const uint2* coefb[NPW];
 #pragma unroll
-  for (int i = 0; i < PPW; i++) {
-    wacc64_zero(ae[i]);
-    wacc64_zero(ao[i]);
-    E[i] = 0;
-    O[i] = 0;
-  }
-  auto fold = [&]() {
+  for (int w = 0; w < NPW; w++)
+    coefb[w] = reinterpret_cast<const uint2*>(b.coef) + ((blk * NP + min(p0 + w, NP - 1)) * c.nco) * IL + lane;
+  const uint2* measb = reinterpret_cast<const uint2*>(b.meas) + (blk * M) * IL + lane;
+
+  wacc64 ae[NPW][PPW], ao[NPW][PPW];
+  uint64_t E[NPW][PPW], O[NPW][PPW];
+#pragma unroll
+  for (int w = 0; w < NPW; w++)
 #pragma unroll
     for (int i = 0; i < PPW; i++) {
-      E[i] = add64(E[i], wacc64_reduce(ae[i]));
-      O[i] = add64(O[i], wacc64_reduce(ao[i]));
-      wacc64_zero(ae[i]);
-      wacc64_zero(ao[i]);
+      wacc64_zero(ae[w][i]);
+      wacc64_zero(ao[w][i]);
+      E[w][i] = 0;
+      O[w][i] = 0;
     }
+  auto fold = [&]() {
+#pragma unroll
+    for (int w = 0; w < NPW; w++)
+#pragma unroll
+      for (int i = 0; i < PPW; i++) {
+        E[w][i] = add64(E[w][i], wacc64_reduce(ae[w][i]));
+        O[w][i] = add64(O[w][i], wacc64_reduce(ao[w][i]));
+        wacc64_zero(ae[w][i]);
+        wacc64_zero(ao[w][i]);
+      }
+  };
+  auto ldc = [&](int w, uint32_t k, bool d) -> uint2 {
+    return coefb[w][(uint64_t)(MCOEF_K + 2 * (k - 1) + (d ? 1 : 0)) * IL];
   };
   // calls whose PPW slots are all real measurement elements run branch-free
   uint32_t kf = 0;
   if (j0 + PPW <= chunk && M >= j0 + PPW) kf = min(C, (M - j0 - PPW) / chunk + 1);
   for (uint32_t k0 = 1; k0 <= kf; k0 += WACC64_MAX_TERMS) {
     const uint32_t k1 = min(kf, k0 + WACC64_MAX_TERMS - 1);
-    uint2 cn = coefb[(uint64_t)(MCOEF_K + 2 * (k0 - 1)) * IL], dn = coefb[(uint64_t)(MCOEF_K + 2 * (k0 - 1) + 1) * IL];
-    uint2 xn[PPW];
+    uint2 cn[NPW], dn[NPW], xn[PPW];
+#pragma unroll
+    for (int w = 0; w < NPW; w++) {
+      cn[w] = ldc(w, k0, false);
+      dn[w] = ldc(w, k0, true);
+    }
 #pragma unroll
     for (int i = 0; i < PPW; i++) xn[i] = measb[(uint64_t)((k0 - 1) * chunk + j0 + i) * IL];
 #pragma unroll 1
     for (uint32_t k = k0; k <= k1; k++) {
-      const c64limbs ck = to_c64limbs(u2v(cn)), dk = to_c64limbs(u2v(dn));
+      c64limbs ck[NPW], dk[NPW];
+#pragma unroll
+      for (int w = 0; w < NPW; w++) {
+        ck[w] = to_c64limbs(u2v(cn[w]));
+        dk[w] = to_c64limbs(u2v(dn[w]));
+      }
       uint64_t x[PPW];
 #pragma unroll
       for (int i = 0; i < PPW; i++) x[i] = u2v(xn[i]);
-      if (k < k1) {
-        cn = coefb[(uint64_t)(MCOEF_K + 2 * k) * IL];
-        dn = coefb[(uint64_t)(MCOEF_K + 2 * k + 1) * IL];
+      if (k < k1) {  // software pipeline: call k + 1's loads in flight during call k's products
+#pragma unroll
+        for (int w = 0; w < NPW; w++) {
+          cn[w] = ldc(w, k + 1, false);
+          dn[w] = ldc(w, k + 1, true);
+        }
 #pragma unroll
         for (int i = 0; i < PPW; i++) xn[i] = measb[(uint64_t)(k * chunk + j0 + i) * IL];
       }
 #pragma unroll
-      for (int i = 0; i < PPW; i++) {
-        wacc64_mac(ae[i], x[i], dk);
-        wacc64_mac(ao[i], x[i], ck);
-      }
+      for (int w = 0; w < NPW; w++)
+#pragma unroll
+        for (int i = 0; i < PPW; i++) {
+          wacc64_mac(ae[w][i], x[i], dk[w]);
+          wacc64_mac(ao[w][i], x[i], ck[w]);
+        }
     }
     fold();
   }
 #pragma unroll 1
   for (uint32_t k = kf + 1; k <= C; k++) {  // the ragged last call(s), or every call of a padded group
-    const c64limbs ck = to_c64limbs(u2v(coefb[(uint64_t)(MCOEF_K + 2 * (k - 1)) * IL]));
-    const c64limbs dk = to_c64limbs(u2v(coefb[(uint64_t)(MCOEF_K + 2 * (k - 1) + 1) * IL]));
     const uint32_t nb = (k - 1) * chunk + j0;
 #pragma unroll
-    for (int i = 0; i < PPW; i++) {
-      if (j0 + i < chunk && nb + i < M) {
-        const uint64_t x = u2v(measb[(uint64_t)(nb + i) * IL]);
-        wacc64_mac(ae[i], x, dk);
-        wacc64_mac(ao[i], x, ck);
+    for (int w = 0; w < NPW; w++) {
+      const c64limbs ck = to_c64limbs(u2v(ldc(w, k, false))), dk = to_c64limbs(u2v(ldc(w, k, true)));
+#pragma unroll
+      for (int i = 0; i < PPW; i++) {
+        if (j0 + i < chunk && nb + i < M) {
+          const uint64_t x = u2v(measb[(uint64_t)(nb + i) * IL]);
+          wacc64_mac(ae[w][i], x, dk);
+          wacc64_mac(ao[w][i], x, ck);
+        }
       }
     }
     if (((k - kf) % WACC64_MAX_TERMS) == 0) fold();
   }
   fold();
-  // ---- wires at t for this group's slots
-  const uint64_t L = u2v(coefb[MCOEF_L * IL]), c0 = u2v(coefb[MCOEF_C0 * IL]);
-  const uint64_t hsum = u2v(coefb[MCOEF_HALFSUM * IL]), t = u2v(coefb[MCOEF_T * IL]);
-  const uint64_t rr = u2v(coefb[MCOEF_R * IL]);
   bool dfail = false;
-  uint64_t prod = 0;
-  uint64_t rpow = pow64_h(rr, j0 + 1);
-#pragma unroll
-  for (int i = 0; i < PPW; i++) {
-    const uint32_t j = j0 + i;
-    if (j < chunk) {
-      const uint64_t se = u2v(proofb[(uint64_t)(2 * j) * IL]), so = u2v(proofb[(uint64_t)(2 * j + 1) * IL]);
-      const uint64_t We = mul64(add64(mul64(se, c0), mul64(E[i], rpow)), L);
-      const uint64_t Wo = mul64(sub64(add64(mul64(so, c0), O[i]), hsum), L);
-      rpow = mul64(rpow, rr);
-      if (LEADER) {
-        if (r0 < b.n) {
-          uint2* o = reinterpret_cast<uint2*>(b.lps_out + (uint64_t)c.lps_bytes * r);
-          o[(uint64_t)p * VL + 1 + 2 * j] = v2u(We);
-          o[(uint64_t)p * VL + 2 + 2 * j] = v2u(Wo);
-        }
-      } else {
-        const uint64_t Ve = add64(We, ld_lead64(b, c, r, p * VL + 1 + 2 * j, dfail));
-        const uint64_t Vo = add64(Wo, ld_lead64(b, c, r, p * VL + 2 + 2 * j, dfail));
-        prod = add64(prod, mul64(Ve, Vo));
-      }
-    }
-  }
-  // ---- gadget polynomial over this group's coefficient range
   const uint32_t GL = c.gpoly_len;
   const uint32_t per = (GL + NG - 1) / NG;
   const uint32_t m0 = g * per, m1 = min(GL, m0 + per);
   const uint4* Sm = b.consts + c.c_S;
-  uint64_t vpart = 0, gpart = 0;
-  if (m0 < m1) {
-    for (uint32_t m = m1; m-- > m0;) {
-      const uint64_t gm = u2v(proofb[(uint64_t)(A + m) * IL]);
-      vpart = add64(vpart, mul64(gm, (uint64_t)Sm[m].x | ((uint64_t)Sm[m].y << 32)));
-      gpart = add64(mul64(gpart, t), gm);
+#pragma unroll
+  for (int w = 0; w < NPW; w++) {
+    if (w == 1 && !two) break;
+    const uint32_t p = p0 + w;
+    const uint2* cb = coefb[w];
+    const uint2* proofb = reinterpret_cast<const uint2*>(b.proof) + (blk * NP * PL + (uint64_t)p * PL) * IL + lane;
+    // ---- wires at t for this group's slots
+    const uint64_t L = u2v(cb[MCOEF_L * IL]), c0 = u2v(cb[MCOEF_C0 * IL]);
+    const uint64_t hsum = u2v(cb[MCOEF_HALFSUM * IL]), t = u2v(cb[MCOEF_T * IL]);
+    const uint64_t rr = u2v(cb[MCOEF_R * IL]);
+    uint64_t prod = 0;
+    uint64_t rpow = pow64_h(rr, j0 + 1);
+#pragma unroll
+    for (int i = 0; i < PPW; i++) {
+      const uint32_t j = j0 + i;
+      if (j < chunk) {
+        const uint64_t se = u2v(proofb[(uint64_t)(2 * j) * IL]), so = u2v(proofb[(uint64_t)(2 * j + 1) * IL]);
+        const uint64_t We = mul64(add64(mul64(se, c0), mul64(E[w][i], rpow)), L);
+        const uint64_t Wo = mul64(sub64(add64(mul64(so, c0), O[w][i]), hsum), L);
+        rpow = mul64(rpow, rr);
+        if (LEADER) {
+          if (r0 < b.n) {
+            uint2* o = reinterpret_cast<uint2*>(b.lps_out + (uint64_t)c.lps_bytes * r);
+            o[(uint64_t)p * VL + 1 + 2 * j] = v2u(We);
+            o[(uint64_t)p * VL + 2 + 2 * j] = v2u(Wo);
+          }
+        } else {
+          const uint64_t Ve = add64(We, ld_lead64(b, c, r, p * VL + 1 + 2 * j, dfail));
+          const uint64_t Vo = add64(Wo, ld_lead64(b, c, r, p * VL + 2 + 2 * j, dfail));
+          prod = add64(prod, mul64(Ve, Vo));
+        }
+      }
     }
-    gpart = mul64(gpart, pow64_h(t, m0));
+    // ---- gadget polynomial over this group's coefficient range
+    uint64_t vpart = 0, gpart = 0;
+    if (m0 < m1) {
+      for (uint32_t m = m1; m-- > m0;) {
+        const uint64_t gm = u2v(proofb[(uint64_t)(A + m) * IL]);
+        vpart = add64(vpart, mul64(gm, (uint64_t)Sm[m].x | ((uint64_t)Sm[m].y << 32)));
+        gpart = add64(mul64(gpart, t), gm);
+      }
+      gpart = mul64(gpart, pow64_h(t, m0));
+    }
+    uint2* pp = reinterpret_cast<uint2*>(b.part) + (((blk * NP + p) * NG + g) * 3) * IL + lane;
+    pp[0] = v2u(prod);
+    pp[IL] = v2u(vpart);
+    pp[2 * IL] = v2u(gpart);
   }
-  uint2* pp = reinterpret_cast<uint2*>(b.part) + (((blk * NP + p) * NG + g) * 3) * IL + lane;
-  pp[0] = v2u(prod);
-  pp[IL] = v2u(vpart);
-  pp[2 * IL] = v2u(gpart);
   if (dfail && r0 < b.n) atomicOr(&b.flags[r0], FLAG_DFAIL);
 }
 
@@ -859,7 +979,7 @@ inline uint32_t nblk_of(uint64_t n) { return (uint32_t)((n + 63) / 64); }
 template <int PPW, bool LEADER>
 void launch_mp_flp_r(const Cfg& c, const Bufs& b, hipStream_t s) {
   const uint32_t nb = nblk_of(b.n);
-  const uint32_t grid = ((nb + 7) / 8) * 8 * c.ngroups * c.np;
+  const uint32_t grid = ((nb + 7) / 8) * 8 * c.ngroups * ((c.np + 1) / 2);
   hipLaunchKernelGGL((mp_flp_part_kernel<PPW, LEADER>), dim3(grid), dim3(64), 0, s, c, b);
   hipLaunchKernelGGL((mp_flp_final_kernel<LEADER>), dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, c, b);
 }
@@ -869,9 +989,11 @@ void launch_mp_flp_r(const Cfg& c, const Bufs& b, hipStream_t s) {
 hipError_t launch_mp_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
   const uint32_t nb = nblk_of(b.n);
   if (b.leader)
-    hipLaunchKernelGGL(mp_xof_kernel<true>, dim3((nb + 3) / 4), dim3(256), 0, s, c, b);
+    hipLaunchKernelGGL(mp_xof_kernel<true>, dim3((nb + MP_XOF_WAVES - 1) / MP_XOF_WAVES), dim3(64 * MP_XOF_WAVES), 0, s,
+                       c, b);
   else
-    hipLaunchKernelGGL(mp_xof_kernel<false>, dim3((nb + 3) / 4), dim3(256), 0, s, c, b);
+    hipLaunchKernelGGL(mp_xof_kernel<false>, dim3((nb + MP_XOF_WAVES - 1) / MP_XOF_WAVES), dim3(64 * MP_XOF_WAVES), 0,
+                       s, c, b);
   return hipGetLastError();
 }
 

@@ -50,16 +50,16 @@ JX_HD void sha256_compress(uint32_t st[8], const uint32_t* blk) {  // 16 big-end
       wi = w[i];
     } else {
       uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      uint32_t s0 = ror32(w15, 7) ^ ror32(w15, 18) ^ (w15 >> 3);
-      uint32_t s1 = ror32(w2, 17) ^ ror32(w2, 19) ^ (w2 >> 10);
+      uint32_t s0 = xor3(ror32(w15, 7), ror32(w15, 18), w15 >> 3);
+      uint32_t s1 = xor3(ror32(w2, 17), ror32(w2, 19), w2 >> 10);
       wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
       w[i & 15] = wi;
     }
-    uint32_t S1 = ror32(e, 6) ^ ror32(e, 11) ^ ror32(e, 25);
+    uint32_t S1 = xor3(ror32(e, 6), ror32(e, 11), ror32(e, 25));
     uint32_t ch = (e & f) ^ (~e & g);
     uint32_t t1 = h + S1 + ch + SHA256_K[i] + wi;
-    uint32_t S0 = ror32(a, 2) ^ ror32(a, 13) ^ ror32(a, 22);
-    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint32_t S0 = xor3(ror32(a, 2), ror32(a, 13), ror32(a, 22));
+    uint32_t mj = maj3(a, b, c);
     h = g;
     g = f;
     f = e;
