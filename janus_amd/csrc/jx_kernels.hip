@@ -1359,6 +1359,20 @@ hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
     hipLaunchKernelGGL(xof_kernel<false>, dim3((nb + 3) / 4), dim3(256), 0, s, c, b);
   return hipGetLastError();
 }
+// Reports that occupy every K1 wave slot of the device exactly once: CUs x resident
+// workgroups per CU (from the kernel's register/LDS footprint) x 64 reports per wave. K1 waves
+// all run the same length, so a launch runs in ceil(reports / this) equal "rounds"; the
+// engine sizes its launches in whole rounds so only the last launch has a partial one.
+uint64_t k1_round_reports(const Cfg& c, int device) {
+  if (c.algo == ALGO_SUMVEC_F64_MULTIPROOF) return mp_k1_round_reports(device);
+  int cus = 0, wgs = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return 0;
+  hipError_t st = c.algo == ALGO_COUNT
+                      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, count_kernel<false>, 256, 0)
+                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_kernel<false>, 256, 0);
+  if (st != hipSuccess || wgs <= 0) return 0;
+  return (uint64_t)cus * (uint64_t)wgs * 256u;
+}
 hipError_t launch_leader_finish(const Cfg& c, const Bufs& b, const uint8_t* prep_msgs, hipStream_t s) {
   hipLaunchKernelGGL(leader_finish_kernel, dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, c, b, prep_msgs);
   return hipGetLastError();

@@ -997,6 +997,15 @@ hipError_t launch_mp_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
   return hipGetLastError();
 }
 
+uint64_t mp_k1_round_reports(int device) {
+  int cus = 0, wgs = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, mp_xof_kernel<false>, 64 * MP_XOF_WAVES, 0) != hipSuccess ||
+      wgs <= 0)
+    return 0;
+  return (uint64_t)cus * (uint64_t)wgs * 64u * MP_XOF_WAVES;
+}
+
 hipError_t launch_mp_slow(const Cfg& c, const Bufs& b, hipStream_t s) {
   hipLaunchKernelGGL(mp_slow_kernel, dim3(nblk_of(b.n)), dim3(64), 0, s, c, b);
   return hipGetLastError();
