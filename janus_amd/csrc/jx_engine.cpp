@@ -50,7 +50,7 @@ struct jx_engine {
   uint8_t *d_verdicts = nullptr, *d_msgs = nullptr;
   // accumulation scratch: partials + selection bytes
   uint64_t* d_partials = nullptr;
-  uint32_t acc_chunks = 16;
+  uint32_t acc_chunks = 0;  // report chunks of the accumulate kernel (0: acc_nchunks picks)
   uint8_t* d_tmp = nullptr;  // output-share transpose / aggregate encode
   size_t tmp_bytes = 0;
   uint8_t* d_mask = nullptr;
@@ -348,6 +348,14 @@ static uint64_t per_report_bytes(const Cfg& c) {
   return b;
 }
 
+// Report chunks of accumulate_kernel: one wave per (output element, chunk), so short outputs
+// (Count, Sum: 1 element) need many chunks to fill the device; >= 16384 waves in total.
+static uint32_t acc_nchunks(const jx_engine* e) {
+  if (e->acc_chunks) return e->acc_chunks;
+  const uint32_t want = (16384u + e->cfg.out_len - 1) / e->cfg.out_len;
+  return want < 16u ? 16u : (want > 4096u ? 4096u : want);
+}
+
 static int32_t ensure_capacity(jx_engine* e, uint64_t n) {
   if (n <= e->cap) return JX_OK;
   free_staging(e);
@@ -369,7 +377,7 @@ static int32_t ensure_capacity(jx_engine* e, uint64_t n) {
   HIPCHK(e, A((void**)&e->d_msgs, cap * c.seed));
   HIPCHK(e, A((void**)&e->d_mask, cap));
   HIPCHK(e, A((void**)&e->d_seg, cap * 4));
-  size_t pbytes = (size_t)e->acc_chunks * c.out_len * 3 * sizeof(uint64_t) + cap;
+  size_t pbytes = (size_t)acc_nchunks(e) * c.out_len * 3 * sizeof(uint64_t) + cap;
   HIPCHK(e, A((void**)&e->d_partials, pbytes));
   HIPCHK(e, hipMemsetAsync(e->d_flags, 0, cap * 4, e->stream));
   e->cap = cap;
@@ -542,7 +550,7 @@ static int32_t accumulate_core(jx_engine* e, uint64_t n, const uint8_t* verdicts
   a.seg = d_seg;
   a.seg_id = seg_id;
   a.partials = e->d_partials;
-  a.nchunks = e->acc_chunks;
+  a.nchunks = acc_nchunks(e);
   uint64_t nblk = (n + 63) / 64;
   a.blocks_per_chunk = (uint32_t)((nblk + a.nchunks - 1) / a.nchunks);
   if (a.blocks_per_chunk == 0) a.blocks_per_chunk = 1;

@@ -879,15 +879,32 @@ __global__ __launch_bounds__(256) void flp_sum_kernel(Cfg c, Bufs b) {
   }
   f128 s0 = ld_il(b.proof, blk, c.proof_len, 0, lane);
   f128 W0 = mont128(add128(mont128(s0, c0R), acc_reduce(ao)), LR);
-  // v = sum_k r^k * gadget_poly(alpha^k);   G(t) by Horner
-  const uint32_t GL = c.gpoly_len;
-  f128 v = make128(0, 0), rk = rR;
-  for (uint32_t k = 1; k <= C; k++) {
-    f128 wk = u4_to_f(omega[k]);
-    f128 h = make128(0, 0);
-    for (uint32_t m = GL; m-- > 0;) h = add128(mont128(h, wk), ld_il(b.proof, blk, c.proof_len, 1 + m, lane));
-    v = add128(v, mont128(h, rk));
-    rk = mont128(rk, rR);
+  // v = sum_{k=1..C} r^k g(w^k). The spec evaluates the gadget polynomial g (GL = 2P - 1
+  // coefficients) at every w^k by Horner: C * GL products and proof-share reads. Since w^P = 1,
+  // g(w^k) = sum_{j<P} g'_j w^{kj} with g'_j = g_j + g_{j+P}, so
+  //   v = sum_{j<P} g'_j S_j,   S_j = sum_{k=1..C} q_j^k,   q_j = r w^j,
+  // and each geometric sum S_j comes from the bits of C by doubling (s_2n = s_n + q^n s_n,
+  // q^2n = (q^n)^2; s_n+1 = s_n + q^n+1): ~2 log2(C) products per j, every coefficient read once.
+  const uint32_t GL = c.gpoly_len, P = c.P;
+  const uint32_t top = 31u - (uint32_t)__builtin_clz(C);  // highest set bit of C >= 1
+  f128 v = make128(0, 0);
+  const f128 w1 = u4_to_f(omega[1 % P]);
+  f128 wj = u4_to_f(omega[0]);  // w^j R
+  for (uint32_t j = 0; j < P; j++) {
+    f128 g = ld_il(b.proof, blk, c.proof_len, 1 + j, lane);
+    if (j + P < GL) g = add128(g, ld_il(b.proof, blk, c.proof_len, 1 + j + P, lane));
+    const f128 q = mont128(rR, wj);  // r w^j, Montgomery form
+    f128 sq = q, pq = q;             // s_n, q^n for n = 1
+    for (int bit = (int)top - 1; bit >= 0; bit--) {
+      sq = add128(sq, mont128(pq, sq));
+      pq = mont128(pq, pq);
+      if ((C >> bit) & 1u) {
+        pq = mont128(pq, q);
+        sq = add128(sq, pq);
+      }
+    }
+    v = add128(v, mont128(g, sq));
+    wj = mont128(wj, w1);
   }
   f128 G = make128(0, 0);
   for (uint32_t m = GL; m-- > 0;) G = add128(mont128(G, tR), ld_il(b.proof, blk, c.proof_len, 1 + m, lane));
@@ -1138,32 +1155,54 @@ __global__ __launch_bounds__(256) void leader_finish_kernel(Cfg c, Bufs b, const
 
 // ---------------------------------------------------------------------------- K4: accumulate
 
-// selection + count + checksum (one report per thread)
+// selection + count + checksum. Grid-stride over reports (grid capped at SELECT_WGS
+// workgroups): each thread folds its reports' SHA-256(id) and selections in registers, the
+// workgroup reduces through LDS, and only one set of atomics per workgroup reaches L2 (one
+// set per wave serialised ~15k atomics on the same 40 bytes for 1M Count reports).
+constexpr uint32_t SELECT_WGS = 1024;
 __global__ __launch_bounds__(256) void select_kernel(AccArgs a, uint8_t* sel) {
-  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool s = false;
-  if (r < a.n)
-    s = a.verdicts[r] == 0 && (!a.mask || a.mask[r]) && (!a.seg || a.seg[r] == a.seg_id);
-  if (r < ((a.n + 63) / 64) * 64) sel[r] = s;
+  const uint64_t padded = ((a.n + 63) / 64) * 64;
   uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (s) {
-    uint32_t id[4];
-    load16(a.nonces + 16 * r, id);
-    sha256_16(id, d);
+  uint32_t cnt = 0;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < padded; r += (uint64_t)gridDim.x * blockDim.x) {
+    bool s = false;
+    if (r < a.n) s = a.verdicts[r] == 0 && (!a.mask || a.mask[r]) && (!a.seg || a.seg[r] == a.seg_id);
+    sel[r] = s;
+    if (s) {
+      uint32_t id[4], h[8];
+      load16(a.nonces + 16 * r, id);
+      sha256_16(id, h);
+#pragma unroll
+      for (int k = 0; k < 8; k++) d[k] ^= h[k];
+      cnt++;
+    }
   }
-  // wave XOR-reduce then one atomic per word per wave
+  // wave XOR / sum reduce, then across the 4 waves of the workgroup in LDS
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     uint32_t v = d[k];
     for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off);
     d[k] = v;
   }
-  unsigned long long cnt = __popcll(__ballot(s));
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  __shared__ uint32_t red[4][9];
+  const uint32_t w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
 #pragma unroll
-    for (int k = 0; k < 8; k++)
-      if (d[k]) atomicXor(&a.checksum[k], d[k]);
-    if (cnt) atomicAdd(a.count, cnt);
+    for (int k = 0; k < 8; k++) red[w][k] = d[k];
+    red[w][8] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x < 9) {
+    const uint32_t k = threadIdx.x;
+    uint32_t v = 0;
+    for (uint32_t q = 0; q < blockDim.x / 64; q++) v = k < 8 ? (v ^ red[q][k]) : (v + red[q][k]);
+    if (v) {
+      if (k < 8)
+        atomicXor(&a.checksum[k], v);
+      else
+        atomicAdd(a.count, (unsigned long long)v);
+    }
   }
 }
 
@@ -1176,7 +1215,21 @@ __global__ __launch_bounds__(256) void accumulate_kernel(AccArgs a, const uint8_
   const uint64_t b1 = (b0 + a.blocks_per_chunk < nblk) ? b0 + a.blocks_per_chunk : nblk;
   acc192 acc;
   acc_zero(acc);
-  for (uint64_t bk = b0; bk < b1; bk++) {
+  // four blocks' loads in flight per iteration (one dependent load per trip left HBM idle)
+  uint64_t bk = b0;
+  for (; bk + 4 <= b1; bk += 4) {
+    uint4 v[4];
+    uint8_t s4[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      s4[u] = sel[(bk + u) * 64 + lane];
+      v[u] = a.outs[il_idx(bk + u, a.out_len, i, lane)];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (s4[u]) acc_add128(acc, u4_to_f(v[u]));
+  }
+  for (; bk < b1; bk++) {
     if (sel[bk * 64 + lane]) acc_add128(acc, u4_to_f(a.outs[il_idx(bk, a.out_len, i, lane)]));
   }
   // wave reduction of the 192-bit accumulators
@@ -1198,18 +1251,32 @@ __global__ __launch_bounds__(256) void accumulate_kernel(AccArgs a, const uint8_
 }
 
 
-__global__ void reduce_partials_kernel(Cfg c, const uint64_t* partials, uint32_t nchunks, uint4* agg) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// one wave per output element: lanes stride over the report chunks' partial sums, then a
+// shuffle reduction (Count / Sum use up to 4096 chunks of a single element)
+__global__ __launch_bounds__(256) void reduce_partials_kernel(Cfg c, const uint64_t* partials, uint32_t nchunks,
+                                                              uint4* agg) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= c.out_len) return;
   acc192 acc;
   acc_zero(acc);
-  for (uint32_t q = 0; q < nchunks; q++) {
+  for (uint32_t q = lane; q < nchunks; q += 64) {
     const uint64_t* p = partials + ((uint64_t)q * c.out_len + i) * 3;
     uint32_t cc = 0;
     acc.w0 = addc64(acc.w0, p[0], cc);
     acc.w1 = addc64(acc.w1, p[1], cc);
     acc.w2 = acc.w2 + p[2] + cc;
   }
+  for (int off = 32; off > 0; off >>= 1) {
+    uint64_t o0 = ((uint64_t)__shfl_xor((uint32_t)(acc.w0 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w0, off);
+    uint64_t o1 = ((uint64_t)__shfl_xor((uint32_t)(acc.w1 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w1, off);
+    uint64_t o2 = ((uint64_t)__shfl_xor((uint32_t)(acc.w2 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w2, off);
+    uint32_t cc = 0;
+    acc.w0 = addc64(acc.w0, o0, cc);
+    acc.w1 = addc64(acc.w1, o1, cc);
+    acc.w2 = acc.w2 + o2 + cc;
+  }
+  if (lane != 0) return;
   acc_add128(acc, u4_to_f(agg[i]));
   if (c.fb == 8) {
     uint64_t v = reduce192_p64(acc.w0, acc.w1, acc.w2);
@@ -1453,10 +1520,12 @@ hipError_t launch_accumulate(const Cfg& c, const AccArgs& a, uint4* agg, hipStre
   // sel lives at the tail of the partials allocation (see engine)
   uint8_t* sel = reinterpret_cast<uint8_t*>(a.partials + (size_t)a.nchunks * c.out_len * 3);
   uint64_t nthreads = ((a.n + 63) / 64) * 64;
-  hipLaunchKernelGGL(select_kernel, dim3((uint32_t)((nthreads + 255) / 256)), dim3(256), 0, s, a, sel);
+  uint64_t swg = (nthreads + 255) / 256;
+  if (swg > SELECT_WGS) swg = SELECT_WGS;
+  hipLaunchKernelGGL(select_kernel, dim3((uint32_t)swg), dim3(256), 0, s, a, sel);
   hipLaunchKernelGGL(accumulate_kernel, dim3((c.out_len + 3) / 4, a.nchunks), dim3(256), 0, s, a,
                      (const uint8_t*)sel);
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3((c.out_len + 255) / 256), dim3(256), 0, s, c,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((c.out_len + 3) / 4), dim3(256), 0, s, c,
                      (const uint64_t*)a.partials, a.nchunks, agg);
   return hipGetLastError();
 }

@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""Helper prep + aggregate throughput for the other BASELINE.json configs on one MI355X.
+
+bench.py measures the headline config (Prio3SumVec 8x1000/88). This tool runs the same
+measurement for configs[0..2] — Prio3Count, Prio3Sum{bits=32}, Prio3Histogram{256, 16} — at
+the report counts BASELINE.json names (Count: 100k, the reference's CPU case, also run at 1M
+here; Sum32 / Histogram: 1M reports). Per config: a pool of K distinct client reports (C-oracle
+client + leader prep_init, 1 % tampered) tiled on the device, inputs resident in HBM; `steps`
+fused jx_helper_prep_aggregate_device calls are timed between torch.cuda.synchronize(); the
+aggregate share and count are verified against multiplicity x the oracle's output shares, and
+every verdict against the oracle. The C oracle on the host's cores is timed beside it on a
+bounded sample (kind "port"). One JSON line per config.
+
+    python tools/bench_configs.py [--only count,sum32,hist] [--cpu-seconds 3]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+P64 = 2**64 - 2**32 + 1
+P128 = 2**128 - 28 * 2**64 + 1
+
+
+def run(name, vdaf, meas_fn, R, K, steps, warmup, cpu_seconds, threads):
+    import torch
+
+    from janus_amd.engine import HelperEngine
+    from oracle import oracle as O  # input generation and the checker only
+
+    orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
+    vk = bytes(range(16))
+    rng = np.random.default_rng(0x5EED)
+    meas = meas_fn(rng, K)
+    nonces = rng.integers(0, 256, size=(K, 16), dtype=np.uint8)
+    rands = rng.integers(0, 256, size=(K, orc.sizes.client_rand), dtype=np.uint8)
+    ps, his, lps, _ = orc.client_leader_batch(vk, meas, nonces, rands, nthreads=threads)
+    for i in range(0, K, 100):  # 1 % invalid: one flipped bit in the leader prep share
+        j = int(rng.integers(0, lps.shape[1]))
+        lps[i, j] ^= 1 << int(rng.integers(0, 8))
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=threads, want_out_shares=True)
+
+    reps = -(-R // K)
+    dev = torch.device("cuda", 0)
+
+    def tile(x):
+        return torch.from_numpy(np.ascontiguousarray(x)).to(dev).repeat(reps, 1)[:R].contiguous()
+
+    d_n, d_his, d_lps = tile(nonces), tile(his), tile(lps)
+    d_ps = tile(ps) if ps.shape[1] else None
+    d_v = torch.empty(R, dtype=torch.uint8, device=dev)
+    d_m = torch.empty((R, 16), dtype=torch.uint8, device=dev)
+    with HelperEngine(vdaf, vk) as eng:
+        def step():
+            eng.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr() if d_ps is not None else 0,
+                                          d_his.data_ptr(), d_lps.data_ptr(), R, 0, d_m.data_ptr(), d_v.data_ptr())
+            eng.sync()
+
+        for _ in range(warmup):
+            step()
+        eng.timing(True)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        kt = eng.timing_read()
+        agg, count, _ = eng.aggregate_share(0)
+
+    total = steps + warmup
+    fb, OL = vdaf.field_bytes, vdaf.output_len
+    p = P64 if fb == 8 else P128
+    mult = np.bincount(np.arange(R) % K, minlength=K)
+    fin = want["verdicts"] == 0
+    outs = want["out_shares"].reshape(K, OL, fb)
+    acc = [0] * OL
+    for i in np.nonzero(fin)[0]:
+        m = int(mult[i]) * total
+        for j in range(OL):
+            acc[j] += m * int.from_bytes(outs[i, j].tobytes(), "little")
+    exp = b"".join((x % p).to_bytes(fb, "little") for x in acc)
+    verified = agg == exp and count == total * int(mult[fin].sum()) and \
+        bool(np.array_equal(d_v.cpu().numpy(), np.tile(want["verdicts"], reps)[:R]))
+
+    # CPU baseline: the C oracle on this host's cores, ~cpu_seconds of work
+    t = time.perf_counter()
+    orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=threads)
+    rate0 = K / (time.perf_counter() - t)
+    creps = max(1, int(cpu_seconds * rate0 / K))
+    ct = lambda a: np.ascontiguousarray(np.tile(a, (creps, 1)))  # noqa: E731
+    t = time.perf_counter()
+    orc.helper_prep_batch(vk, ct(nonces), ct(ps), ct(his), ct(lps), nthreads=threads)
+    cdt = time.perf_counter() - t
+
+    def per_launch(stage):
+        return round(kt[stage]["ms"] / max(1, kt[stage]["launches"]), 3)
+
+    return {
+        "metric": f"helper reports/sec (prep_init+aggregate), {name}",
+        "value": round(R * steps / dt, 1), "unit": "reports/s", "n_gpus": 1, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(dt / steps * 1e3, 3), "higher_is_better": True,
+        "config": {"workload": name, "reports": R, "pool": K},
+        "kernels": {"k1_ms_per_launch": per_launch("xof"), "k3_ms_per_launch": per_launch("flp"),
+                    "k4_ms_per_launch": per_launch("accumulate"), "launches_per_step": kt["xof"]["launches"] // steps},
+        "verified": verified,
+        "cpu_baseline": {"value": round(creps * K / cdt, 1), "unit": "reports/s", "cores": threads, "kind": "port",
+                         "sample": f"{creps * K} reports ({K} distinct x {creps}), C oracle, {threads} threads, "
+                                   f"{cdt:.1f} s"},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="count100k,count,sum32,hist")
+    ap.add_argument("--pool", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=3.0)
+    a = ap.parse_args()
+    from janus_amd.vdaf import Prio3
+
+    threads = min(16, os.cpu_count() or 1)
+    cfgs = {
+        "count100k": ("Prio3Count (configs[0]: 100k reports)", Prio3.count(),
+                      lambda rng, K: rng.integers(0, 2, size=(K, 1), dtype=np.uint64), 100_000),
+        "count": ("Prio3Count", Prio3.count(),
+                  lambda rng, K: rng.integers(0, 2, size=(K, 1), dtype=np.uint64), 1_000_000),
+        "sum32": ("Prio3Sum bits=32 (configs[1])", Prio3.sum(32),
+                  lambda rng, K: rng.integers(0, 1 << 32, size=(K, 1), dtype=np.uint64), 1_000_000),
+        "hist": ("Prio3Histogram length=256 chunk_length=16 (configs[2])", Prio3.histogram(256, 16),
+                 lambda rng, K: rng.integers(0, 256, size=(K, 1), dtype=np.uint64), 1_000_000),
+    }
+    for key in a.only.split(","):
+        name, vdaf, fn, R = cfgs[key]
+        print(json.dumps(run(name, vdaf, fn, R, a.pool, a.steps, a.warmup, a.cpu_seconds, threads)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
