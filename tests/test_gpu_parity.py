@@ -84,6 +84,11 @@ def _random_batch(orc: O.Prio3Oracle, vk, n, seed, tamper_every=7):
 CASES = {
     "count": Prio3.count(),
     "sum32": Prio3.sum(32),
+    # Sum's v uses geometric sums over the bits of C = bits: one call, odd and non-power-of-2 counts
+    "sum1": Prio3.sum(1),
+    "sum5": Prio3.sum(5),
+    "sum17": Prio3.sum(17),
+    "sum31": Prio3.sum(31),
     "sumvec_small": Prio3.sum_vec(3, 37, 5),
     "sumvec_8x1000_88": Prio3.sum_vec(8, 1000, 88),
     "histogram_256_16": Prio3.histogram(256, 16),
@@ -114,6 +119,22 @@ def test_random_batches_vs_oracle(name):
         np.testing.assert_array_equal(v2, want["verdicts"])
         agg7, count7, cs7 = eng.aggregate_share(7)
         assert agg7 == want["agg"] and count7 == want["count"] and cs7 == want["checksum"]
+
+
+def test_count_grid_stride_select():
+    """300k Count reports: more than the select kernel's 1024 x 256 threads, so every thread folds
+    several reports' SHA-256 into the checksum; 4096 accumulate chunks of the single element."""
+    vdaf = Prio3.count()
+    vk = bytes(range(16))
+    orc = O.Prio3Oracle(vdaf.algo_id)
+    n = 300_000
+    nonces, ps, his, lps = _random_batch(orc, vk, n, seed=0xC0)
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16)
+    with HelperEngine(vdaf, vk) as eng:
+        v, _ = eng.prep_and_aggregate(nonces, ps, his, lps, segment=0)
+        np.testing.assert_array_equal(v, want["verdicts"])
+        agg, count, cs = eng.aggregate_share(0)
+    assert agg == want["agg"] and count == want["count"] and cs == want["checksum"]
 
 
 def test_mask_and_segments():
