@@ -467,10 +467,11 @@ __device__ __forceinline__ bool ge_exact(uint4 v) {
 // LEADER (agg_id 0, leader_initialized, aggregation_job_driver.rs:345): the shares are explicit in
 // the leader input share (meas || proofs || k_blind, decoded here: elements >= p fail) and only the
 // joint_rand_part absorb runs through Keccak.
+constexpr uint32_t K1_WAVES = 4;  // waves (64-report blocks) per K1 workgroup
 template <bool LEADER>
-__global__ __launch_bounds__(256) void xof_kernel(Cfg c, Bufs b) {
+__global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t blk = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t blk = (uint64_t)blockIdx.x * K1_WAVES + (threadIdx.x >> 6);
   const uint64_t nblk = (b.n + 63) / 64;
   if (blk >= nblk) return;
   const uint64_t r0 = blk * 64 + lane;
@@ -1421,9 +1422,9 @@ hipError_t launch_count(const Cfg& c, const Bufs& b, hipStream_t s) {
 hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
   uint32_t nb = nblk_of(b.n);
   if (b.leader)
-    hipLaunchKernelGGL(xof_kernel<true>, dim3((nb + 3) / 4), dim3(256), 0, s, c, b);
+    hipLaunchKernelGGL(xof_kernel<true>, dim3((nb + K1_WAVES - 1) / K1_WAVES), dim3(64 * K1_WAVES), 0, s, c, b);
   else
-    hipLaunchKernelGGL(xof_kernel<false>, dim3((nb + 3) / 4), dim3(256), 0, s, c, b);
+    hipLaunchKernelGGL(xof_kernel<false>, dim3((nb + K1_WAVES - 1) / K1_WAVES), dim3(64 * K1_WAVES), 0, s, c, b);
   return hipGetLastError();
 }
 // Reports that occupy every K1 wave slot of the device exactly once: CUs x resident
@@ -1434,11 +1435,12 @@ uint64_t k1_round_reports(const Cfg& c, int device) {
   if (c.algo == ALGO_SUMVEC_F64_MULTIPROOF) return mp_k1_round_reports(device);
   int cus = 0, wgs = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return 0;
+  const uint32_t threads = c.algo == ALGO_COUNT ? 256u : 64u * K1_WAVES;
   hipError_t st = c.algo == ALGO_COUNT
-                      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, count_kernel<false>, 256, 0)
-                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_kernel<false>, 256, 0);
+                      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, count_kernel<false>, threads, 0)
+                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_kernel<false>, threads, 0);
   if (st != hipSuccess || wgs <= 0) return 0;
-  return (uint64_t)cus * (uint64_t)wgs * 256u;
+  return (uint64_t)cus * (uint64_t)wgs * threads;
 }
 hipError_t launch_leader_finish(const Cfg& c, const Bufs& b, const uint8_t* prep_msgs, hipStream_t s) {
   hipLaunchKernelGGL(leader_finish_kernel, dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, c, b, prep_msgs);
