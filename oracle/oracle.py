@@ -21,6 +21,9 @@ _lib = None
 COUNT, SUM, SUMVEC, HISTOGRAM = 0, 1, 2, 3
 # Prio3SumVecField64MultiproofHmacSha256Aes128 (core/src/vdaf.rs:173-199)
 SUMVEC_F64_MULTIPROOF = 4
+# Prio3FixedPointBoundedL2VecSum{bitsize, length} (core/src/vdaf.rs:86-91; bits = 16 or 32)
+FIXEDPOINT_L2 = 5
+NSIZES = 21
 VERDICT_NAMES = {
     0: "finished",
     1: "prepare_init_failure",
@@ -144,6 +147,10 @@ class Sizes:
     P: int
     seed: int
     verify_key: int
+    chunk: int          # first gadget's chunk length
+    arity1: int         # second gadget (FixedPoint norm): arity, calls, P; 0 if none
+    calls1: int
+    P1: int
 
 
 class Prio3Oracle:
@@ -151,7 +158,7 @@ class Prio3Oracle:
 
     def __init__(self, algo: int, bits: int = 0, length: int = 0, chunk: int = 0, proofs: int = 1):
         self.params = (algo, bits, length, chunk, proofs)
-        out = (ctypes.c_uint32 * 17)()
+        out = (ctypes.c_uint32 * NSIZES)()
         if lib().jo_sizes(*self.params, ctypes.cast(out, ctypes.c_void_p)) != 0:
             raise ValueError(f"bad Prio3 params {self.params}")
         self.sizes = Sizes(*list(out))
@@ -159,7 +166,7 @@ class Prio3Oracle:
 
     @property
     def meas_stride(self) -> int:
-        return self.params[2] if self.algo in (SUMVEC, SUMVEC_F64_MULTIPROOF) else 1
+        return self.params[2] if self.algo in (SUMVEC, SUMVEC_F64_MULTIPROOF, FIXEDPOINT_L2) else 1
 
     def shard(self, measurement, nonce: bytes, rand: bytes):
         s = self.sizes

@@ -529,10 +529,15 @@ static void xof_next_vec(const field_t *F, xof_t *x, fe *out, size_t n) {
 /* Prio3 configuration (VDAF-08 §7; Janus VdafInstance core/src/vdaf.rs:65-108,
  * constructors core/src/vdaf.rs:203-262).                                     */
 
-enum { G_MUL = 0, G_RANGE2 = 1, G_PSUM_MUL = 2 };
+enum { G_MUL = 0, G_RANGE2 = 1, G_PSUM_MUL = 2, G_PSUM_POLY = 3 };
 #define SEED_MAX 32
+#define MAX_GADGETS 2
 /* Private-use algorithm id of Prio3SumVecField64MultiproofHmacSha256Aes128 (core/src/vdaf.rs:18-20). */
 #define ALGO_ID_SUMVEC_F64_MULTIPROOF 0xFFFF1003u
+/* Algorithm id prio 0.16.1 gives Prio3FixedPointBoundedL2VecSum (Prio3::new(.., 0xFFFF0000, ..) in
+ * new_fixedpoint_boundedl2_vec_sum[_multithreaded]; the constructor Janus calls at
+ * core/src/vdaf.rs:315-333 and aggregator/src/aggregator.rs:916-932). [M] */
+#define ALGO_ID_FIXEDPOINT_L2 0xFFFF0000u
 enum {
   USAGE_MEAS_SHARE = 1,
   USAGE_PROOF_SHARE = 2,
@@ -543,6 +548,16 @@ enum {
   USAGE_JOINT_RAND_PART = 7,
 };
 
+/* One FLP gadget (VDAF-08 §7.3.2): Mul, PolyEval(x^2 - x) ("Range2"), ParallelSum(Mul, chunk) or
+ * ParallelSum(PolyEval(poly), chunk). Every gadget here has degree 2. */
+typedef struct {
+  int kind;       /* G_* */
+  int arity, degree, calls, chunk, P;
+  int gpoly_len;  /* degree * (P - 1) + 1 */
+  int proof_off;  /* offset of [wire seeds || gadget poly] in one proof */
+  fe poly[3];     /* G_PSUM_POLY: the inner PolyEval polynomial, low degree first */
+} gadget_t;
+
 typedef struct {
   int algo, bits, length, chunk, proofs;
   uint32_t algo_id; /* the DST's algorithm id */
@@ -550,14 +565,33 @@ typedef struct {
   int seed;         /* SEED_SIZE (= verify key length): 16 or 32 */
   const field_t *F;
   int meas_len, out_len, jr_len, qr_len;
-  int gadget, arity, degree, calls, P;
-  int gpoly_len, proof_len, verifier_len, prove_rand_len;
+  int ng;           /* gadgets */
+  gadget_t gd[MAX_GADGETS];
+  int proof_len, verifier_len, prove_rand_len;
+  int norm_bits;    /* FixedPointBoundedL2VecSum: bits of the claimed squared norm (2n - 2) */
 } cfg_t;
 
 static int next_pow2(int v) {
   int p = 1;
   while (p < v) p <<= 1;
   return p;
+}
+
+static int isqrt_floor(int v) {
+  int r = 0;
+  while ((long long)(r + 1) * (r + 1) <= v) r++;
+  return r;
+}
+
+static void gadget_init(gadget_t *g, int kind, int arity, int calls, int chunk) {
+  memset(g, 0, sizeof *g);
+  g->kind = kind;
+  g->arity = arity;
+  g->degree = 2;
+  g->calls = calls;
+  g->chunk = chunk;
+  g->P = next_pow2(1 + calls);
+  g->gpoly_len = g->degree * (g->P - 1) + 1;
 }
 
 static int cfg_make(cfg_t *c, int algo, int bits, int length, int chunk, int proofs) {
@@ -571,18 +605,15 @@ static int cfg_make(cfg_t *c, int algo, int bits, int length, int chunk, int pro
   c->algo_id = (uint32_t)algo;
   c->xof = XOF_TURBOSHAKE;
   c->seed = 16;
+  c->ng = 1;
   if (proofs < 1 || proofs > 255) return -1;
-  c->qr_len = 1;
-  c->degree = 2;
   switch (algo) {
     case JO_COUNT:
       c->F = &F64;
       c->meas_len = 1;
       c->out_len = 1;
       c->jr_len = 0;
-      c->gadget = G_MUL;
-      c->arity = 2;
-      c->calls = 1;
+      gadget_init(&c->gd[0], G_MUL, 2, 1, 1);
       break;
     case JO_SUM:
       if (bits < 1 || bits > 64) return -1;
@@ -590,9 +621,7 @@ static int cfg_make(cfg_t *c, int algo, int bits, int length, int chunk, int pro
       c->meas_len = bits;
       c->out_len = 1;
       c->jr_len = 1;
-      c->gadget = G_RANGE2;
-      c->arity = 1;
-      c->calls = bits;
+      gadget_init(&c->gd[0], G_RANGE2, 1, bits, 1);
       break;
     case JO_SUMVEC_F64_MULTIPROOF: /* new_prio3_sum_vec_field64_multiproof_hmacsha256_aes128, core/src/vdaf.rs:176-199 */
       if (proofs < 2) return -1;
@@ -607,9 +636,7 @@ static int cfg_make(cfg_t *c, int algo, int bits, int length, int chunk, int pro
       c->meas_len = bits * length;
       c->out_len = length;
       c->jr_len = 1;
-      c->gadget = G_PSUM_MUL;
-      c->arity = 2 * chunk;
-      c->calls = (c->meas_len + chunk - 1) / chunk;
+      gadget_init(&c->gd[0], G_PSUM_MUL, 2 * chunk, (c->meas_len + chunk - 1) / chunk, chunk);
       break;
     case JO_HISTOGRAM:
       if (length < 1 || chunk < 1) return -1;
@@ -617,18 +644,55 @@ static int cfg_make(cfg_t *c, int algo, int bits, int length, int chunk, int pro
       c->meas_len = length;
       c->out_len = length;
       c->jr_len = 2;
-      c->gadget = G_PSUM_MUL;
-      c->arity = 2 * chunk;
-      c->calls = (length + chunk - 1) / chunk;
+      gadget_init(&c->gd[0], G_PSUM_MUL, 2 * chunk, (length + chunk - 1) / chunk, chunk);
       break;
+    case JO_FIXEDPOINT_L2: {
+      /* FixedPointBoundedL2VecSum<FixedI{n}<U{n-1}>, ParallelSum<PolyEval>, ParallelSum<Mul>>
+       * (prio 0.16.1 flp::types::fixedpoint_l2::FixedPointBoundedL2VecSum::new(entries); Janus builds it
+       * for BitSize16 / BitSize32 at aggregator/src/aggregator.rs:916-932, gadget bounds core/src/dp.rs:
+       * 127-143). [M] items, restated from memory of prio 0.16.1:
+       *  - input = n bits per entry (entry + 2^(n-1), LE) || 2n-2 bits of the claimed squared norm;
+       *  - gadget 0 = ParallelSum(Mul, chunk0) range check of every input bit (parallel_sum_range_checks),
+       *    chunk0 = max(1, floor(sqrt(n*entries + 2n-2)));
+       *  - gadget 1 = ParallelSum(PolyEval(2^(2n-2) - 2^n y + y^2), chunk1) over the decoded entries y,
+       *    chunk1 = max(1, floor(sqrt(entries))), short chunks padded with 2^(n-1)/num_shares;
+       *  - v = jr[1] * range_check + jr[1]^2 * (computed_norm - claimed_norm); JOINT_RAND_LEN 2;
+       *  - output = the decoded entries (OUTPUT_LEN = entries).
+       * bits == chunk unused; entries * 2^(2n+2) must stay below p (FixedPointBoundedL2VecSum::new). */
+      if ((bits != 16 && bits != 32) || length < 1) return -1;
+      c->F = &F128;
+      c->algo_id = ALGO_ID_FIXEDPOINT_L2;
+      c->norm_bits = 2 * bits - 2;
+      if ((u128)length >= (P128 >> (c->norm_bits + 4))) return -1;
+      c->meas_len = bits * length + c->norm_bits;
+      c->out_len = length;
+      c->jr_len = 2;
+      c->ng = 2;
+      int ch0 = isqrt_floor(c->meas_len), ch1 = isqrt_floor(length);
+      if (ch0 < 1) ch0 = 1;
+      if (ch1 < 1) ch1 = 1;
+      c->chunk = ch0;
+      gadget_init(&c->gd[0], G_PSUM_MUL, 2 * ch0, (c->meas_len + ch0 - 1) / ch0, ch0);
+      gadget_init(&c->gd[1], G_PSUM_POLY, ch1, (length + ch1 - 1) / ch1, ch1);
+      /* norm_summand_poly = [2^(2n-2), -2^n, 1] */
+      c->gd[1].poly[0] = ((fe)1) << (2 * bits - 2);
+      c->gd[1].poly[1] = f_neg(c->F, ((fe)1) << bits);
+      c->gd[1].poly[2] = 1;
+      break;
+    }
     default:
       return -1;
   }
-  c->P = next_pow2(1 + c->calls);
-  c->gpoly_len = c->degree * (c->P - 1) + 1;
-  c->proof_len = c->arity + c->gpoly_len;
-  c->verifier_len = 1 + c->arity + 1;
-  c->prove_rand_len = c->arity;
+  c->qr_len = c->ng; /* FlpGeneric::query_rand_len = number of gadgets */
+  int off = 0;
+  c->verifier_len = 1;
+  for (int g = 0; g < c->ng; g++) {
+    c->gd[g].proof_off = off;
+    off += c->gd[g].arity + c->gd[g].gpoly_len;
+    c->verifier_len += c->gd[g].arity + 1;
+    c->prove_rand_len += c->gd[g].arity;
+  }
+  c->proof_len = off;
   return 0;
 }
 
@@ -648,11 +712,15 @@ int jo_sizes(int algo, int bits, int length, int chunk, int proofs, uint32_t out
   out[9] = jr ? S : 0;
   out[10] = E;
   out[11] = S * (3 + (jr ? 2 : 0));
-  out[12] = c.arity;
-  out[13] = c.calls;
-  out[14] = c.P;
+  out[12] = c.gd[0].arity;
+  out[13] = c.gd[0].calls;
+  out[14] = c.gd[0].P;
   out[15] = S;
   out[16] = S;
+  out[17] = c.gd[0].chunk;
+  out[18] = c.ng > 1 ? c.gd[1].arity : 0;
+  out[19] = c.ng > 1 ? c.gd[1].calls : 0;
+  out[20] = c.ng > 1 ? c.gd[1].P : 0;
   return 0;
 }
 
@@ -723,24 +791,31 @@ static void poly_interp_roots(const field_t *F, const fe *vals, fe *coef, int n,
 }
 
 /* ------------------------------------------------------------------------- */
-/* FLP (VDAF-08 §7.3 FlpGeneric) with gadgets Mul, PolyEval(x^2-x), ParallelSum(Mul). */
+/* FLP (VDAF-08 §7.3 FlpGeneric) with gadgets Mul, PolyEval(x^2-x), ParallelSum(Mul),
+ * ParallelSum(PolyEval(p)). */
 
-static fe gadget_eval(const cfg_t *c, const fe *x) {
+static fe gadget_eval(const cfg_t *c, const gadget_t *gd, const fe *x) {
   const field_t *F = c->F;
-  switch (c->gadget) {
+  switch (gd->kind) {
     case G_MUL:
       return f_mul(F, x[0], x[1]);
     case G_RANGE2: /* PolyEval([0,-1,1]) : x^2 - x */
       return f_sub(F, f_mul(F, x[0], x[0]), x[0]);
-    default: {
+    case G_PSUM_MUL: {
       fe s = 0;
-      for (int j = 0; j < c->chunk; j++) s = f_add(F, s, f_mul(F, x[2 * j], x[2 * j + 1]));
+      for (int j = 0; j < gd->chunk; j++) s = f_add(F, s, f_mul(F, x[2 * j], x[2 * j + 1]));
+      return s;
+    }
+    default: { /* G_PSUM_POLY: sum_j p(x_j) */
+      fe s = 0;
+      for (int j = 0; j < gd->chunk; j++) s = f_add(F, s, poly_eval(F, gd->poly, 3, x[j]));
       return s;
     }
   }
 }
 
 typedef struct {
+  const gadget_t *gd;
   fe *wire; /* arity x P, row-major */
   int k;
   int query;
@@ -749,23 +824,25 @@ typedef struct {
 } grec_t;
 
 static fe gadget_call(const cfg_t *c, grec_t *g, const fe *inp) {
+  const gadget_t *gd = g->gd;
   g->k++;
-  for (int j = 0; j < c->arity; j++) g->wire[j * c->P + g->k] = inp[j];
-  if (!g->query) return gadget_eval(c, inp); /* ProveGadget */
+  for (int j = 0; j < gd->arity; j++) g->wire[j * gd->P + g->k] = inp[j];
+  if (!g->query) return gadget_eval(c, gd, inp); /* ProveGadget */
   /* QueryGadget: gadget_poly(alpha^k) */
-  return poly_eval(c->F, g->gpoly, c->gpoly_len, f_pow(c->F, g->alpha, (u128)g->k));
+  return poly_eval(c->F, g->gpoly, gd->gpoly_len, f_pow(c->F, g->alpha, (u128)g->k));
 }
 
 /* ParallelSum range checks as in prio's parallel_sum_range_checks (padding with
- * (0, -1/num_shares) and no r_power update for padded slots). */
-static fe psum_range_checks(const cfg_t *c, grec_t *g, const fe *meas, fe r, int num_shares, fe *buf) {
+ * (0, -1/num_shares) and no r_power update for padded slots) over input[0..len). */
+static fe psum_range_checks(const cfg_t *c, grec_t *g, const fe *meas, int len, fe r, int num_shares, fe *buf) {
   const field_t *F = c->F;
+  const int chunk = g->gd->chunk;
   fe shares_inv = f_inv(F, f_from_u64(F, (uint64_t)num_shares));
   fe out = 0, r_power = r;
-  for (int call = 0; call < c->calls; call++) {
-    for (int j = 0; j < c->chunk; j++) {
-      int idx = call * c->chunk + j;
-      if (idx < c->meas_len) {
+  for (int call = 0; call < g->gd->calls; call++) {
+    for (int j = 0; j < chunk; j++) {
+      int idx = call * chunk + j;
+      if (idx < len) {
         buf[2 * j] = f_mul(F, r_power, meas[idx]);
         buf[2 * j + 1] = f_sub(F, meas[idx], shares_inv);
         r_power = f_mul(F, r_power, r);
@@ -779,35 +856,70 @@ static fe psum_range_checks(const cfg_t *c, grec_t *g, const fe *meas, fe r, int
   return out;
 }
 
+/* Field::decode_bitvector: sum_b 2^b x_b */
+static fe decode_bits(const field_t *F, const fe *x, int nbits) {
+  fe acc = 0, pw = 1;
+  for (int b = 0; b < nbits; b++) {
+    acc = f_add(F, acc, f_mul(F, pw, x[b]));
+    pw = f_add(F, pw, pw);
+  }
+  return acc;
+}
+
 static fe valid_eval(const cfg_t *c, grec_t *g, const fe *meas, const fe *jr, int num_shares) {
   const field_t *F = c->F;
   switch (c->algo) {
     case JO_COUNT: { /* Mul(x, x) - x */
       fe in[2] = {meas[0], meas[0]};
-      return f_sub(F, gadget_call(c, g, in), meas[0]);
+      return f_sub(F, gadget_call(c, &g[0], in), meas[0]);
     }
     case JO_SUM: { /* sum_i r^(i+1) * Range2(bit_i) */
       fe out = 0, r = jr[0];
       for (int i = 0; i < c->meas_len; i++) {
-        out = f_add(F, out, f_mul(F, r, gadget_call(c, g, &meas[i])));
+        out = f_add(F, out, f_mul(F, r, gadget_call(c, &g[0], &meas[i])));
         r = f_mul(F, r, jr[0]);
       }
       return out;
     }
     case JO_SUMVEC:
     case JO_SUMVEC_F64_MULTIPROOF: {
-      fe *buf = calloc((size_t)c->arity, sizeof(fe));
-      fe out = psum_range_checks(c, g, meas, jr[0], num_shares, buf);
+      fe *buf = calloc((size_t)c->gd[0].arity, sizeof(fe));
+      fe out = psum_range_checks(c, &g[0], meas, c->meas_len, jr[0], num_shares, buf);
       free(buf);
       return out;
     }
-    default: { /* Histogram */
-      fe *buf = calloc((size_t)c->arity, sizeof(fe));
-      fe rc = psum_range_checks(c, g, meas, jr[0], num_shares, buf);
+    case JO_HISTOGRAM: {
+      fe *buf = calloc((size_t)c->gd[0].arity, sizeof(fe));
+      fe rc = psum_range_checks(c, &g[0], meas, c->meas_len, jr[0], num_shares, buf);
       free(buf);
       fe sc = f_neg(F, f_inv(F, f_from_u64(F, (uint64_t)num_shares)));
       for (int i = 0; i < c->meas_len; i++) sc = f_add(F, sc, meas[i]);
       return f_add(F, f_mul(F, jr[1], rc), f_mul(F, f_mul(F, jr[1], jr[1]), sc));
+    }
+    default: { /* FixedPointBoundedL2VecSum::valid */
+      const int n = c->bits, E = c->length;
+      fe *buf = calloc((size_t)c->gd[0].arity, sizeof(fe));
+      /* (I) every input bit (entries and claimed norm) is 0 or 1 */
+      fe range = psum_range_checks(c, &g[0], meas, c->meas_len, jr[0], num_shares, buf);
+      free(buf);
+      /* (II) computed squared norm: sum over the decoded entries y of 2^(2n-2) - 2^n y + y^2,
+       * chunks of chunk1 entries through ParallelSum(PolyEval); a short chunk is padded with a share
+       * of the encoding of 0.0, 2^(n-1) / num_shares */
+      const gadget_t *g1 = &c->gd[1];
+      fe zero_share = f_mul(F, ((fe)1) << (n - 1), f_inv(F, f_from_u64(F, (uint64_t)num_shares)));
+      fe *in = calloc((size_t)g1->chunk, sizeof(fe));
+      fe computed = 0;
+      for (int k = 0; k < g1->calls; k++) {
+        for (int j = 0; j < g1->chunk; j++) {
+          int idx = k * g1->chunk + j;
+          in[j] = idx < E ? decode_bits(F, meas + (size_t)idx * n, n) : zero_share;
+        }
+        computed = f_add(F, computed, gadget_call(c, &g[1], in));
+      }
+      free(in);
+      fe claimed = decode_bits(F, meas + (size_t)E * n, c->norm_bits);
+      fe norm_check = f_sub(F, computed, claimed);
+      return f_add(F, f_mul(F, jr[1], range), f_mul(F, f_mul(F, jr[1], jr[1]), norm_check));
     }
   }
 }
@@ -826,8 +938,25 @@ static void flp_encode(const cfg_t *c, uint64_t m, const uint64_t *vec, fe *meas
       for (int i = 0; i < c->length; i++)
         for (int j = 0; j < c->bits; j++) meas[i * c->bits + j] = (vec[i] >> j) & 1;
       break;
-    default:
+    case JO_HISTOGRAM:
       for (int i = 0; i < c->length; i++) meas[i] = (i == (int)m);
+      break;
+    default: { /* FixedPointBoundedL2VecSum::encode_measurement */
+      const int n = c->bits;
+      const uint64_t mask = n == 64 ? ~0ull : ((1ull << n) - 1);
+      u128 norm = 0;
+      for (int i = 0; i < c->length; i++) {
+        /* CompatibleFloat::to_field_integer: the two's-complement bits with the sign bit flipped */
+        uint64_t y = (vec[i] ^ (1ull << (n - 1))) & mask;
+        for (int b = 0; b < n; b++) meas[(size_t)i * n + b] = (y >> b) & 1;
+        int64_t d = (int64_t)y - (int64_t)(1ull << (n - 1)); /* compute_norm_of_entries: sum (y - 2^(n-1))^2 */
+        norm += (u128)((__int128)d * d);
+      }
+      /* prio refuses to encode a vector whose squared norm needs more than 2n-2 bits
+       * (fill_with_bitvector_representation); the oracle encodes its low bits instead, i.e. a
+       * client that lies about the norm, which the FLP must reject. */
+      for (int b = 0; b < c->norm_bits; b++) meas[(size_t)c->length * n + b] = (fe)((norm >> b) & 1);
+    }
   }
 }
 
@@ -838,91 +967,119 @@ static void flp_truncate(const cfg_t *c, const fe *meas, fe *out) {
     case JO_HISTOGRAM:
       memcpy(out, meas, sizeof(fe) * c->out_len);
       break;
-    default: {
-      int b = c->bits;
-      for (int i = 0; i < c->out_len; i++) {
-        fe acc = 0, pw = 1;
-        for (int j = 0; j < b; j++) {
-          acc = f_add(F, acc, f_mul(F, pw, meas[i * b + j]));
-          pw = f_add(F, pw, pw);
-        }
-        out[i] = acc;
-      }
-    }
+    default: /* SumVec / Sum: out_i = sum_j 2^j meas[i*bits + j]; FixedPoint: the decoded entries */
+      for (int i = 0; i < c->out_len; i++) out[i] = decode_bits(F, meas + (size_t)i * c->bits, c->bits);
   }
 }
 
-/* FlpGeneric.prove (VDAF-08 §7.3.3): run the circuit with num_shares = 1, then
+/* FlpGeneric.prove (VDAF-08 §7.3.3): run the circuit with num_shares = 1, then per gadget
  * gadget_poly = G(wire polys), computed through a size-2P DFT. */
 static void flp_prove(const cfg_t *c, const fe *meas, const fe *prove_rand, const fe *jr, fe *proof) {
   const field_t *F = c->F;
-  int P = c->P, A = c->arity, N = 2 * P;
-  fe *wire = calloc((size_t)A * P, sizeof(fe));
-  for (int j = 0; j < A; j++) wire[j * P] = prove_rand[j];
-  grec_t g = {wire, 0, 0, NULL, 0};
-  (void)valid_eval(c, &g, meas, jr, 1);
-  fe aP = f_root(F, __builtin_ctz((unsigned)P));
-  fe aN = f_root(F, __builtin_ctz((unsigned)N));
-  fe *acc = calloc((size_t)N, sizeof(fe));
-  fe *e0 = calloc((size_t)N, sizeof(fe)), *e1 = calloc((size_t)N, sizeof(fe));
-  fe *coef = calloc((size_t)P, sizeof(fe));
-  for (int j = 0; j < (c->gadget == G_RANGE2 ? 1 : A / 2); j++) {
-    /* evaluations of wire polys at the N-th roots of unity */
-    for (int w = 0; w < (c->gadget == G_RANGE2 ? 1 : 2); w++) {
-      fe *e = w ? e1 : e0;
-      int idx = (c->gadget == G_RANGE2) ? 0 : 2 * j + w;
-      poly_interp_roots(F, &wire[idx * P], coef, P, aP);
-      memset(e, 0, sizeof(fe) * N);
-      memcpy(e, coef, sizeof(fe) * P);
-      dft(F, e, N, aN);
-    }
-    for (int i = 0; i < N; i++) {
-      fe v = (c->gadget == G_RANGE2) ? f_sub(F, f_mul(F, e0[i], e0[i]), e0[i]) : f_mul(F, e0[i], e1[i]);
-      acc[i] = f_add(F, acc[i], v);
-    }
+  grec_t g[MAX_GADGETS];
+  int pr = 0;
+  for (int gi = 0; gi < c->ng; gi++) {
+    const gadget_t *gd = &c->gd[gi];
+    g[gi] = (grec_t){gd, calloc((size_t)gd->arity * gd->P, sizeof(fe)), 0, 0, NULL, 0};
+    for (int j = 0; j < gd->arity; j++) g[gi].wire[j * gd->P] = prove_rand[pr + j];
+    pr += gd->arity;
   }
-  dft(F, acc, N, f_inv(F, aN));
-  fe ninv = f_inv(F, f_from_u64(F, (uint64_t)N));
-  for (int j = 0; j < A; j++) proof[j] = prove_rand[j];
-  for (int i = 0; i < c->gpoly_len; i++) proof[A + i] = f_mul(F, acc[i], ninv);
-  /* degree check: coefficient 2P-1 must vanish */
-  if (f_mul(F, acc[N - 1], ninv) != 0) abort();
-  free(wire);
-  free(acc);
-  free(e0);
-  free(e1);
-  free(coef);
+  (void)valid_eval(c, g, meas, jr, 1);
+  pr = 0;
+  for (int gi = 0; gi < c->ng; gi++) {
+    const gadget_t *gd = &c->gd[gi];
+    const int P = gd->P, A = gd->arity, N = 2 * P;
+    const fe *wire = g[gi].wire;
+    fe aP = f_root(F, __builtin_ctz((unsigned)P));
+    fe aN = f_root(F, __builtin_ctz((unsigned)N));
+    fe *acc = calloc((size_t)N, sizeof(fe));
+    fe *e0 = calloc((size_t)N, sizeof(fe)), *e1 = calloc((size_t)N, sizeof(fe));
+    fe *coef = calloc((size_t)P, sizeof(fe));
+    /* wire polys evaluated at the N-th roots of unity */
+#define WIRE_EVALS(dst, idx)                                   \
+  do {                                                         \
+    poly_interp_roots(F, &wire[(idx) * P], coef, P, aP);       \
+    memset((dst), 0, sizeof(fe) * N);                          \
+    memcpy((dst), coef, sizeof(fe) * P);                       \
+    dft(F, (dst), N, aN);                                      \
+  } while (0)
+    if (gd->kind == G_RANGE2) {
+      WIRE_EVALS(e0, 0);
+      for (int i = 0; i < N; i++) acc[i] = f_sub(F, f_mul(F, e0[i], e0[i]), e0[i]);
+    } else if (gd->kind == G_PSUM_POLY) {
+      for (int j = 0; j < A; j++) {
+        WIRE_EVALS(e0, j);
+        for (int i = 0; i < N; i++) acc[i] = f_add(F, acc[i], poly_eval(F, gd->poly, 3, e0[i]));
+      }
+    } else { /* Mul / ParallelSum(Mul): pairs of wires */
+      for (int j = 0; j < A / 2; j++) {
+        WIRE_EVALS(e0, 2 * j);
+        WIRE_EVALS(e1, 2 * j + 1);
+        for (int i = 0; i < N; i++) acc[i] = f_add(F, acc[i], f_mul(F, e0[i], e1[i]));
+      }
+    }
+#undef WIRE_EVALS
+    dft(F, acc, N, f_inv(F, aN));
+    fe ninv = f_inv(F, f_from_u64(F, (uint64_t)N));
+    fe *pp = proof + gd->proof_off;
+    for (int j = 0; j < A; j++) pp[j] = prove_rand[pr + j];
+    pr += A;
+    for (int i = 0; i < gd->gpoly_len; i++) pp[A + i] = f_mul(F, acc[i], ninv);
+    /* degree check: coefficient 2P-1 must vanish */
+    if (f_mul(F, acc[N - 1], ninv) != 0) abort();
+    free(acc);
+    free(e0);
+    free(e1);
+    free(coef);
+    free(g[gi].wire);
+  }
 }
 
-/* FlpGeneric.query (VDAF-08 §7.3.3). Returns 0, or -1 if t is a P-th root of unity. */
+/* FlpGeneric.query (VDAF-08 §7.3.3). Returns 0, or -1 if some t_g is a P_g-th root of unity.
+ * verifier = [v] || per gadget g: [wire_j(t_g) for j < arity_g] || gadget_poly_g(t_g). */
 static int flp_query(const cfg_t *c, const fe *meas, const fe *proof, const fe *qr, const fe *jr, int num_shares,
                      fe *verifier) {
   const field_t *F = c->F;
-  int P = c->P, A = c->arity;
-  fe *wire = calloc((size_t)A * P, sizeof(fe));
-  for (int j = 0; j < A; j++) wire[j * P] = proof[j];
-  fe aP = f_root(F, __builtin_ctz((unsigned)P));
-  grec_t g = {wire, 0, 1, proof + A, aP};
-  verifier[0] = valid_eval(c, &g, meas, jr, num_shares);
-  fe t = qr[0];
-  if (f_pow(F, t, (u128)P) == 1) {
-    free(wire);
-    return -1;
+  grec_t g[MAX_GADGETS];
+  for (int gi = 0; gi < c->ng; gi++) {
+    const gadget_t *gd = &c->gd[gi];
+    const fe *pp = proof + gd->proof_off;
+    g[gi] = (grec_t){gd, calloc((size_t)gd->arity * gd->P, sizeof(fe)), 0, 1, pp + gd->arity,
+                     f_root(F, __builtin_ctz((unsigned)gd->P))};
+    for (int j = 0; j < gd->arity; j++) g[gi].wire[j * gd->P] = pp[j];
   }
-  fe *coef = calloc((size_t)P, sizeof(fe));
-  for (int j = 0; j < A; j++) {
-    poly_interp_roots(F, &wire[j * P], coef, P, aP);
-    verifier[1 + j] = poly_eval(F, coef, P, t);
+  verifier[0] = valid_eval(c, g, meas, jr, num_shares);
+  int rc = 0, vo = 1;
+  for (int gi = 0; gi < c->ng && !rc; gi++) {
+    const gadget_t *gd = &c->gd[gi];
+    const int P = gd->P, A = gd->arity;
+    fe t = qr[gi];
+    if (f_pow(F, t, (u128)P) == 1) {
+      rc = -1;
+      break;
+    }
+    fe *coef = calloc((size_t)P, sizeof(fe));
+    for (int j = 0; j < A; j++) {
+      poly_interp_roots(F, &g[gi].wire[j * P], coef, P, g[gi].alpha);
+      verifier[vo + j] = poly_eval(F, coef, P, t);
+    }
+    verifier[vo + A] = poly_eval(F, g[gi].gpoly, gd->gpoly_len, t);
+    vo += A + 1;
+    free(coef);
   }
-  verifier[1 + A] = poly_eval(F, proof + A, c->gpoly_len, t);
-  free(coef);
-  free(wire);
-  return 0;
+  for (int gi = 0; gi < c->ng; gi++) free(g[gi].wire);
+  return rc;
 }
 
 static int flp_decide(const cfg_t *c, const fe *verifier) {
   if (verifier[0] != 0) return 0;
-  return gadget_eval(c, verifier + 1) == verifier[1 + c->arity];
+  int vo = 1;
+  for (int gi = 0; gi < c->ng; gi++) {
+    const gadget_t *gd = &c->gd[gi];
+    if (gadget_eval(c, gd, verifier + vo) != verifier[vo + gd->arity]) return 0;
+    vo += gd->arity + 1;
+  }
+  return 1;
 }
 
 /* ------------------------------------------------------------------------- */
@@ -1279,7 +1436,9 @@ static void *client_worker(void *arg) {
   const cfg_t *c = j->c;
   uint32_t sz[JO_NSIZES];
   jo_sizes(c->algo, c->bits, c->length, c->chunk, c->proofs, sz);
-  int mstride = (c->algo == JO_SUMVEC || c->algo == JO_SUMVEC_F64_MULTIPROOF) ? c->length : 1;
+  int mstride = (c->algo == JO_SUMVEC || c->algo == JO_SUMVEC_F64_MULTIPROOF || c->algo == JO_FIXEDPOINT_L2)
+                    ? c->length
+                    : 1;
   uint8_t *lin = malloc(sz[6]);
   uint8_t corr[SEED_MAX];
   for (uint64_t r = j->lo; r < j->hi; r++) {

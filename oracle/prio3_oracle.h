@@ -31,8 +31,13 @@ extern "C" {
 /* Prio3 algorithm ids == taskprov VDAF type codes, messages/src/taskprov.rs:358-363.
  * JO_SUMVEC_F64_MULTIPROOF selects Prio3SumVecField64MultiproofHmacSha256Aes128
  * (core/src/vdaf.rs:173-199: Field64, proofs >= 2, XofHmacSha256Aes128, 32-byte seeds and
- * verify key, DST algorithm id 0xFFFF1003). */
-enum { JO_COUNT = 0, JO_SUM = 1, JO_SUMVEC = 2, JO_HISTOGRAM = 3, JO_SUMVEC_F64_MULTIPROOF = 4 };
+ * verify key, DST algorithm id 0xFFFF1003).
+ * JO_FIXEDPOINT_L2 selects Prio3FixedPointBoundedL2VecSum{bitsize, length} (core/src/vdaf.rs:
+ * 26-33,86-91; aggregator/src/aggregator.rs:916-932): bits = 16 (FixedI16<U15>) or 32
+ * (FixedI32<U31>), length = entries, chunk ignored; DST algorithm id 0xFFFF0000. Measurements
+ * are the entries' two's-complement bit patterns (FixedI{n}::to_bits as u{n}). */
+enum { JO_COUNT = 0, JO_SUM = 1, JO_SUMVEC = 2, JO_HISTOGRAM = 3, JO_SUMVEC_F64_MULTIPROOF = 4,
+       JO_FIXEDPOINT_L2 = 5 };
 
 /* Verdicts, mirroring the PingPongError labels of aggregator/src/aggregator/error.rs:379-424 */
 enum {
@@ -48,8 +53,10 @@ enum {
  *  5 public_share_bytes  6 leader_input_share_bytes  7 helper_input_share_bytes
  *  8 prep_share_bytes  9 prep_msg_bytes  10 field_bytes  11 client_rand_bytes
  *  12 gadget_arity  13 gadget_calls  14 P (wire poly length)  15 seed_size
- *  16 verify_key_size                                                    */
-#define JO_NSIZES 17
+ *  16 verify_key_size  17 gadget chunk_length
+ *  18..20 second gadget (FixedPointBoundedL2VecSum's norm gadget): arity, calls, P (0 if none)
+ * Indices 12-14 and 17 describe the first gadget.                         */
+#define JO_NSIZES 21
 int jo_sizes(int algo, int bits, int length, int chunk, int proofs, uint32_t out[JO_NSIZES]);
 
 /* Client: shard one measurement. measurement: Count {0,1}; Sum integer;

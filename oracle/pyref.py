@@ -245,6 +245,30 @@ class ParallelSumMul:
         return out
 
 
+class ParallelSumPoly:
+    """ParallelSum(PolyEval(poly), count): sum_j poly(x_j) (FixedPointBoundedL2VecSum's norm gadget)."""
+
+    def __init__(self, poly, count):
+        self.poly, self.count = poly, count
+        self.ARITY, self.DEGREE = count, len(poly) - 1
+
+    def eval(self, F, x):
+        return sum(poly_eval(F, self.poly, x[j]) for j in range(self.count)) % F.p
+
+    def eval_poly(self, F, polys):
+        out = [0]
+        for j in range(self.count):
+            comp, pw = [0], [1]  # poly(f_j) by Horner-free expansion: sum_i c_i f_j^i
+            for c in self.poly:
+                term = [c * a % F.p for a in pw]
+                comp = [((comp[i] if i < len(comp) else 0) + (term[i] if i < len(term) else 0)) % F.p
+                        for i in range(max(len(comp), len(term)))]
+                pw = poly_mul(F, pw, polys[j])
+            out = [((out[i] if i < len(out) else 0) + (comp[i] if i < len(comp) else 0)) % F.p
+                   for i in range(max(len(out), len(comp)))]
+        return out
+
+
 def next_pow2(n):
     p = 1
     while p < n:
@@ -252,32 +276,51 @@ def next_pow2(n):
     return p
 
 
+def _isqrt(n):
+    r = 0
+    while (r + 1) * (r + 1) <= n:
+        r += 1
+    return r
+
+
 class Valid:
-    """Circuits as in VDAF-08 §7.4 (and prio 0.16.1 flp::types)."""
+    """Circuits as in VDAF-08 §7.4 (and prio 0.16.1 flp::types), plus prio's
+    FixedPointBoundedL2VecSum (flp::types::fixedpoint_l2; restated from memory, see DESIGN.md)."""
 
     def __init__(self, kind, bits=0, length=0, chunk=0, field=None):
         self.kind = kind
         if kind == "count":
-            self.Field, self.GADGET, self.CALLS = Field64, Mul(), 1
+            self.Field, self.GADGETS, self.GADGET_CALLS = Field64, [Mul()], [1]
             self.MEAS_LEN, self.OUTPUT_LEN, self.JOINT_RAND_LEN = 1, 1, 0
         elif kind == "sum":
-            self.Field, self.GADGET, self.CALLS = Field128, Range2(), bits
+            self.Field, self.GADGETS, self.GADGET_CALLS = Field128, [Range2()], [bits]
             self.MEAS_LEN, self.OUTPUT_LEN, self.JOINT_RAND_LEN = bits, 1, 1
         elif kind == "sumvec":
-            self.Field, self.GADGET = field or Field128, ParallelSumMul(chunk)
+            self.Field, self.GADGETS = field or Field128, [ParallelSumMul(chunk)]
             self.MEAS_LEN, self.OUTPUT_LEN, self.JOINT_RAND_LEN = bits * length, length, 1
-            self.CALLS = (self.MEAS_LEN + chunk - 1) // chunk
+            self.GADGET_CALLS = [(self.MEAS_LEN + chunk - 1) // chunk]
         elif kind == "histogram":
-            self.Field, self.GADGET = Field128, ParallelSumMul(chunk)
+            self.Field, self.GADGETS = Field128, [ParallelSumMul(chunk)]
             self.MEAS_LEN, self.OUTPUT_LEN, self.JOINT_RAND_LEN = length, length, 2
-            self.CALLS = (length + chunk - 1) // chunk
+            self.GADGET_CALLS = [(length + chunk - 1) // chunk]
+        elif kind == "fixedpoint":
+            # entries of `bits`-bit fixed point numbers in [-1, 1) plus their claimed squared norm
+            F = self.Field = Field128
+            self.norm_bits = 2 * bits - 2
+            self.MEAS_LEN, self.OUTPUT_LEN, self.JOINT_RAND_LEN = bits * length + self.norm_bits, length, 2
+            c0, c1 = max(1, _isqrt(self.MEAS_LEN)), max(1, _isqrt(length))
+            norm_poly = [1 << (2 * bits - 2), (-(1 << bits)) % F.p, 1]
+            self.GADGETS = [ParallelSumMul(c0), ParallelSumPoly(norm_poly, c1)]
+            self.GADGET_CALLS = [-(-self.MEAS_LEN // c0), -(-length // c1)]
+            chunk = c0
         self.bits, self.length, self.chunk = bits, length, chunk
-        self.P = next_pow2(1 + self.CALLS)
-        g = self.GADGET
-        self.PROOF_LEN = g.ARITY + g.DEGREE * (self.P - 1) + 1
-        self.VERIFIER_LEN = 1 + g.ARITY + 1
-        self.PROVE_RAND_LEN = g.ARITY
-        self.QUERY_RAND_LEN = 1
+        self.Ps = [next_pow2(1 + c) for c in self.GADGET_CALLS]
+        self.P = self.Ps[0]
+        self.GADGET = self.GADGETS[0]
+        self.PROOF_LEN = sum(g.ARITY + g.DEGREE * (P - 1) + 1 for g, P in zip(self.GADGETS, self.Ps))
+        self.VERIFIER_LEN = 1 + sum(g.ARITY + 1 for g in self.GADGETS)
+        self.PROVE_RAND_LEN = sum(g.ARITY for g in self.GADGETS)
+        self.QUERY_RAND_LEN = len(self.GADGETS)
 
     def encode(self, m):
         if self.kind == "count":
@@ -286,6 +329,12 @@ class Valid:
             return [(m >> i) & 1 for i in range(self.bits)]
         if self.kind == "sumvec":
             return [(m[i] >> j) & 1 for i in range(self.length) for j in range(self.bits)]
+        if self.kind == "fixedpoint":
+            n = self.bits
+            ys = [(x ^ (1 << (n - 1))) & ((1 << n) - 1) for x in m]  # to_field_integer
+            norm = sum((y - (1 << (n - 1))) ** 2 for y in ys)
+            out = [(y >> b) & 1 for y in ys for b in range(n)]
+            return out + [(norm >> b) & 1 for b in range(self.norm_bits)]  # low bits if |x| >= 1 (dishonest)
         return [1 if i == m else 0 for i in range(self.length)]
 
     def truncate(self, meas):
@@ -295,9 +344,27 @@ class Valid:
         b = self.bits
         return [sum((1 << j) * meas[i * b + j] for j in range(b)) % F.p for i in range(self.OUTPUT_LEN)]
 
-    def eval(self, call, meas, joint_rand, num_shares):
+    def _range_checks(self, call, meas, r, num_shares):
+        p = self.Field.p
+        shares_inv = pow(num_shares, p - 2, p)
+        chunk = self.GADGETS[0].ARITY // 2
+        r_power, out = r, 0
+        for i in range(self.GADGET_CALLS[0]):
+            inputs = []
+            for j in range(chunk):
+                idx = i * chunk + j
+                if idx < len(meas):
+                    inputs += [r_power * meas[idx] % p, (meas[idx] - shares_inv) % p]
+                    r_power = r_power * r % p
+                else:
+                    inputs += [0, (-shares_inv) % p]
+            out = (out + call(inputs)) % p
+        return out
+
+    def eval(self, calls, meas, joint_rand, num_shares):
         F = self.Field
         p = F.p
+        call = calls[0]
         if self.kind == "count":
             return (call([meas[0], meas[0]]) - meas[0]) % p
         if self.kind == "sum":
@@ -307,20 +374,19 @@ class Valid:
                 r = r * joint_rand[0] % p
             return out
         shares_inv = pow(num_shares, p - 2, p)
-        r = joint_rand[0]
-        r_power, range_check = r, 0
-        for i in range(self.CALLS):
-            inputs = []
-            for j in range(self.chunk):
-                idx = i * self.chunk + j
-                if idx < len(meas):
-                    inputs += [r_power * meas[idx] % p, (meas[idx] - shares_inv) % p]
-                    r_power = r_power * r % p
-                else:
-                    inputs += [0, (-shares_inv) % p]
-            range_check = (range_check + call(inputs)) % p
+        range_check = self._range_checks(call, meas, joint_rand[0], num_shares)
         if self.kind == "sumvec":
             return range_check
+        if self.kind == "fixedpoint":
+            n, E, g1 = self.bits, self.length, self.GADGETS[1]
+            ys = [sum(meas[i * n + b] << b for b in range(n)) % p for i in range(E)]
+            pad = (1 << (n - 1)) * shares_inv % p
+            computed = 0
+            for k in range(self.GADGET_CALLS[1]):
+                chunk = [ys[k * g1.count + j] if k * g1.count + j < E else pad for j in range(g1.count)]
+                computed = (computed + calls[1](chunk)) % p
+            claimed = sum(meas[E * n + b] << b for b in range(self.norm_bits)) % p
+            return (joint_rand[1] * range_check + joint_rand[1] ** 2 * (computed - claimed)) % p
         sum_check = (sum(meas) - shares_inv) % p
         return (joint_rand[1] * range_check + joint_rand[1] ** 2 * sum_check) % p
 
@@ -329,61 +395,84 @@ class FlpGeneric:
     def __init__(self, valid: Valid):
         self.V = valid
 
-    def _run(self, meas, wire_seeds, joint_rand, num_shares, out_fn):
+    def _run(self, meas, wire_seeds, joint_rand, num_shares, out_fns):
+        """wire_seeds[g] and out_fns[g] per gadget; returns (v, wires[g][j][k])."""
         V = self.V
-        wire = [[0] * V.P for _ in range(V.GADGET.ARITY)]
-        for j in range(V.GADGET.ARITY):
-            wire[j][0] = wire_seeds[j]
-        k = [0]
+        wires, ks, calls = [], [], []
+        for g, (gadget, P) in enumerate(zip(V.GADGETS, V.Ps)):
+            w = [[0] * P for _ in range(gadget.ARITY)]
+            for j in range(gadget.ARITY):
+                w[j][0] = wire_seeds[g][j]
+            wires.append(w)
+            ks.append([0])
 
-        def call(inp):
-            k[0] += 1
-            for j, x in enumerate(inp):
-                wire[j][k[0]] = x
-            return out_fn(inp, k[0])
+            def call(inp, g=g, w=w, k=ks[-1]):
+                k[0] += 1
+                for j, x in enumerate(inp):
+                    w[j][k[0]] = x
+                return out_fns[g](inp, k[0])
+            calls.append(call)
+        v = V.eval(calls, meas, joint_rand, num_shares)
+        return v, wires
 
-        v = V.eval(call, meas, joint_rand, num_shares)
-        return v, wire
+    def _split(self, vec, sizes):
+        out, o = [], 0
+        for n in sizes:
+            out.append(vec[o:o + n])
+            o += n
+        return out
 
     def prove(self, meas, prove_rand, joint_rand):
         V, F = self.V, self.V.Field
-        _, wire = self._run(meas, prove_rand, joint_rand, 1, lambda inp, k: V.GADGET.eval(F, inp))
-        alpha = F.root(V.P)
-        xs = [pow(alpha, k, F.p) for k in range(V.P)]
-        polys = [poly_interp(F, xs, w) for w in wire]
-        gp = V.GADGET.eval_poly(F, polys)
-        glen = V.GADGET.DEGREE * (V.P - 1) + 1
-        gp = (gp + [0] * glen)[:glen]
-        return list(prove_rand) + gp
+        seeds = self._split(list(prove_rand), [g.ARITY for g in V.GADGETS])
+        _, wires = self._run(meas, seeds, joint_rand, 1,
+                             [lambda inp, k, g=g: g.eval(F, inp) for g in V.GADGETS])
+        proof = []
+        for g, P, w, sd in zip(V.GADGETS, V.Ps, wires, seeds):
+            alpha = F.root(P)
+            xs = [pow(alpha, k, F.p) for k in range(P)]
+            polys = [poly_interp(F, xs, wj) for wj in w]
+            gp = g.eval_poly(F, polys)
+            glen = g.DEGREE * (P - 1) + 1
+            gp = (gp + [0] * glen)[:glen]
+            proof += list(sd) + gp
+        return proof
 
     def query(self, meas, proof, query_rand, joint_rand, num_shares):
         V, F = self.V, self.V.Field
-        A = V.GADGET.ARITY
-        seeds, gp = proof[:A], proof[A:]
-        alpha = F.root(V.P)
-        v, wire = self._run(meas, seeds, joint_rand, num_shares,
-                            lambda inp, k: poly_eval(F, gp, pow(alpha, k, F.p)))
-        t = query_rand[0]
-        if pow(t, V.P, F.p) == 1:
-            raise ValueError("query rand is a root of unity")
-        xs = [pow(alpha, k, F.p) for k in range(V.P)]
+        parts = self._split(proof, [g.ARITY + g.DEGREE * (P - 1) + 1 for g, P in zip(V.GADGETS, V.Ps)])
+        seeds = [pt[:g.ARITY] for pt, g in zip(parts, V.GADGETS)]
+        gps = [pt[g.ARITY:] for pt, g in zip(parts, V.GADGETS)]
+        fns = [lambda inp, k, gp=gp, P=P: poly_eval(F, gp, pow(F.root(P), k, F.p)) for gp, P in zip(gps, V.Ps)]
+        v, wires = self._run(meas, seeds, joint_rand, num_shares, fns)
         out = [v]
-        for w in wire:
-            out.append(poly_eval(F, poly_interp(F, xs, w), t))
-        out.append(poly_eval(F, gp, t))
+        for gi, (P, w, gp) in enumerate(zip(V.Ps, wires, gps)):
+            t = query_rand[gi]
+            if pow(t, P, F.p) == 1:
+                raise ValueError("query rand is a root of unity")
+            alpha = F.root(P)
+            xs = [pow(alpha, k, F.p) for k in range(P)]
+            for wj in w:
+                out.append(poly_eval(F, poly_interp(F, xs, wj), t))
+            out.append(poly_eval(F, gp, t))
         return out
 
     def decide(self, verifier):
         V, F = self.V, self.V.Field
         if verifier[0] != 0:
             return False
-        A = V.GADGET.ARITY
-        return V.GADGET.eval(F, verifier[1:1 + A]) == verifier[1 + A]
+        o = 1
+        for g in V.GADGETS:
+            if g.eval(F, verifier[o:o + g.ARITY]) != verifier[o + g.ARITY]:
+                return False
+            o += g.ARITY + 1
+        return True
 
 
 # --------------------------------------------------------------------------- Prio3
 
-ALGO_IDS = {"count": 0, "sum": 1, "sumvec": 2, "histogram": 3, "sumvec_f64_multiproof": 0xFFFF1003}
+ALGO_IDS = {"count": 0, "sum": 1, "sumvec": 2, "histogram": 3, "sumvec_f64_multiproof": 0xFFFF1003,
+            "fixedpoint": 0xFFFF0000}
 USAGE = dict(meas_share=1, proof_share=2, joint_randomness=3, prove_randomness=4, query_randomness=5,
              joint_rand_seed=6, joint_rand_part=7)
 

@@ -132,3 +132,99 @@ def test_multiproof_c_oracle_equals_pyref(cfg):
 def test_multiproof_rejects_single_proof():
     with pytest.raises(ValueError):
         O.Prio3Oracle(O.SUMVEC_F64_MULTIPROOF, 8, 12, 14, 1)
+
+
+# ---- Prio3FixedPointBoundedL2VecSum (core/src/vdaf.rs:86-91; aggregator.rs:916-932)
+
+FP_CFGS = [(16, 3), (32, 3), (16, 10), (16, 5)]
+
+
+def _fx(v: float, bits: int) -> int:
+    """FixedI{bits}<U{bits-1}> bit pattern of v in [-1, 1) (two's complement, as u{bits})."""
+    return int(round(v * (1 << (bits - 1)))) & ((1 << bits) - 1)
+
+
+def _decode_fp(vals, bits, num_measurements):
+    """prio CompatibleFloat::to_float (fixedpoint_l2/compatible_float.rs): f * 2^(1-n) - c."""
+    return [x * 2.0 ** (1 - bits) - num_measurements for x in vals]
+
+
+@pytest.mark.parametrize("cfg", FP_CFGS, ids=[f"fp{c[0]}_len{c[1]}" for c in FP_CFGS])
+def test_fixedpoint_c_oracle_equals_pyref(cfg):
+    bits, length = cfg
+    rng = random.Random(bits * 100 + length)
+    C = O.Prio3Oracle(O.FIXEDPOINT_L2, bits, length, 0)
+    Py = pyref.Prio3("fixedpoint", bits=bits, length=length)
+    s = C.sizes
+    assert (s.meas_len, s.output_len, s.joint_rand_len, s.proof_len, s.verifier_len) == \
+        (Py.valid.MEAS_LEN, length, 2, Py.valid.PROOF_LEN, Py.valid.VERIFIER_LEN)
+    vk = rng.randbytes(16)
+    for trial in range(3):
+        nonce, rand = rng.randbytes(16), rng.randbytes(s.client_rand)
+        lim = 1.0 / (2 * length)
+        m = [_fx(rng.uniform(-lim, lim), bits) for _ in range(length)]
+        shard = C.shard(m, nonce, rand)
+        assert shard == Py.shard(m, nonce, rand)
+        ps, lin, hin = shard
+        rc, lshare, lout, _ = C.prep_init(vk, 0, nonce, ps, lin)
+        assert rc == 0 and lshare == Py.prep_init(vk, 0, nonce, ps, lin)[1]
+        got = C.helper_prep(vk, nonce, ps, hin, lshare)
+        assert got == Py.helper_prep(vk, nonce, ps, hin, lshare) and got[0] == 0
+        agg = C.aggregate([lout, got[2]])
+        vals = [int.from_bytes(agg[i:i + 16], "little") for i in range(0, len(agg), 16)]
+        assert vals == [(x ^ (1 << (bits - 1))) for x in m]  # the offset encodings of the entries
+        for byte in range(0, len(lshare), max(1, len(lshare) // 7)):
+            t = bytearray(lshare)
+            t[byte] ^= 1 << rng.randrange(8)
+            v = C.helper_prep(vk, nonce, ps, hin, bytes(t))[0]
+            assert v == Py.helper_prep(vk, nonce, ps, hin, bytes(t))[0] and v in (2, 3, 4)
+
+
+@pytest.mark.parametrize("bits", [16, 32])
+def test_fixedpoint_norm_violation_rejected(bits):
+    """A vector of squared norm >= 1 cannot be encoded honestly (prio refuses); a client that
+    claims the low 2n-2 bits of its norm is rejected by the norm check (prepare_message_failure)."""
+    length = 4
+    C = O.Prio3Oracle(O.FIXEDPOINT_L2, bits, length, 0)
+    Py = pyref.Prio3("fixedpoint", bits=bits, length=length)
+    vk, nonce, rand = bytes(range(16)), bytes(16), bytes(range(80))
+    for m in ([_fx(0.75, bits)] * length, [_fx(-1.0, bits)] + [0] * (length - 1)):
+        ps, lin, hin = C.shard(m, nonce, rand)
+        rc, lshare, _, _ = C.prep_init(vk, 0, nonce, ps, lin)
+        assert rc == 0
+        v = C.helper_prep(vk, nonce, ps, hin, lshare)[0]
+        assert v == 3 == Py.helper_prep(vk, nonce, ps, hin, lshare)[0]
+    # the largest honest vector: squared norm just below 1
+    m = [_fx(0.49, bits)] * length
+    ps, lin, hin = C.shard(m, nonce, rand)
+    assert C.helper_prep(vk, nonce, ps, hin, C.prep_init(vk, 0, nonce, ps, lin)[1])[0] == 0
+
+
+@pytest.mark.parametrize("bits", [16, 32])
+def test_fixedpoint_reference_e2e_vectors(bits):
+    """The reference's own end-to-end expectation (interop_binaries/tests/end_to_end.rs:689-765,
+    e2e_prio3_fixed16vec / e2e_prio3_fixed32vec): these four measurements aggregate and decode
+    to [0.5, 0.5, 0.6875]; collector/src/lib.rs:1141-1213 decodes one [1/16, 1/8, 1/4]."""
+    q, e, s = 0.25, 0.125, 0.0625
+    meas = [[q, e, e], [s, e, s], [e, e, q], [s, e, q]]
+    C = O.Prio3Oracle(O.FIXEDPOINT_L2, bits, 3, 0)
+    vk = bytes(range(16))
+    outs = []
+    for i, m in enumerate(meas):
+        nonce, rand = bytes([i]) * 16, bytes([i + 7]) * 80
+        ps, lin, hin = C.shard([_fx(v, bits) for v in m], nonce, rand)
+        rc, lshare, lout, _ = C.prep_init(vk, 0, nonce, ps, lin)
+        v, _, hout = C.helper_prep(vk, nonce, ps, hin, lshare)
+        assert rc == 0 and v == 0
+        outs += [lout, hout]
+    agg = C.aggregate(outs)
+    vals = [int.from_bytes(agg[i:i + 16], "little") for i in range(0, len(agg), 16)]
+    assert _decode_fp(vals, bits, len(meas)) == [0.5, 0.5, 0.6875]
+    # collector/src/lib.rs:1141-1213: a single measurement decodes to itself
+    nonce, rand = bytes(16), bytes(80)
+    ps, lin, hin = C.shard([_fx(v, bits) for v in (s, e, q)], nonce, rand)
+    _, lshare, lout, _ = C.prep_init(vk, 0, nonce, ps, lin)
+    hout = C.helper_prep(vk, nonce, ps, hin, lshare)[2]
+    agg = C.aggregate([lout, hout])
+    vals = [int.from_bytes(agg[i:i + 16], "little") for i in range(0, len(agg), 16)]
+    assert _decode_fp(vals, bits, 1) == [0.0625, 0.125, 0.25]
