@@ -128,6 +128,11 @@ static int ilog2(int v) {
   while ((1 << l) < v) l++;
   return l;
 }
+static uint32_t isqrt_floor(uint32_t v) {
+  uint32_t r = 0;
+  while ((uint64_t)(r + 1) * (r + 1) <= v) r++;
+  return r < 1 ? 1 : r;
+}
 
 namespace jx {
 int psum_ppw(uint32_t chunk);
@@ -206,14 +211,44 @@ static int32_t make_cfg(const jx_prio3_params* p, const uint8_t* vk, uint32_t vk
       arity = 2 * p->chunk_length;
       c.out_is_meas = 1;
       break;
+    case ALGO_FIXEDPOINT_L2: {
+      // FixedPointBoundedL2VecSum::new(entries) as prio 0.16.1 sizes it (restated in
+      // oracle/prio3_oracle.c cfg_make): n-bit entries (n = 16 | 32, BitSize16 / BitSize32,
+      // core/src/vdaf.rs:26-33), 2n-2 norm bits, chunk0 = floor(sqrt(n*entries + 2n-2)),
+      // chunk1 = floor(sqrt(entries)); chunk_length is not a parameter of this VDAF.
+      if ((p->bits != 16 && p->bits != 32) || p->length < 1 || p->length > (1u << 24)) {
+        why = "Prio3FixedPointBoundedL2VecSum needs bits (bitsize) 16 or 32 and 1 <= length <= 2^24";
+        return JX_E_UNSUPPORTED;
+      }
+      c.dst_id = 0xFFFF0000u;
+      c.norm_bits = 2 * p->bits - 2;
+      c.meas_len = p->bits * p->length + c.norm_bits;
+      c.out_len = p->length;
+      c.jr_len = 2;
+      c.chunk = isqrt_floor(c.meas_len);
+      c.calls = (c.meas_len + c.chunk - 1) / c.chunk;
+      arity = 2 * c.chunk;
+      c.chunk1 = isqrt_floor(p->length);
+      c.calls1 = (p->length + c.chunk1 - 1) / c.chunk1;
+      c.P1 = next_pow2(1 + c.calls1);
+      c.logP1 = ilog2(c.P1);
+      c.gpoly1_len = 2 * (c.P1 - 1) + 1;
+      c.ppw1 = 2;
+      c.ngroups1 = (c.chunk1 + c.ppw1 - 1) / c.ppw1;
+      break;
+    }
     default:
       why = "unknown algo_id";
       return JX_E_INVALID;
   }
-  if (c.algo == ALGO_SUMVEC || c.algo == ALGO_HISTOGRAM || mp) {
+  const bool fp = c.algo == ALGO_FIXEDPOINT_L2;
+  if (c.algo == ALGO_SUMVEC || c.algo == ALGO_HISTOGRAM || mp || fp) {
     c.ppw = psum_ppw(c.chunk);
     c.ngroups = (c.chunk + c.ppw - 1) / c.ppw;
   }
+  c.ngt = c.ngroups + c.ngroups1;
+  c.qr_len = fp ? 2 : 1;
+  c.trunc_len = fp ? p->bits * p->length : c.out_len * c.bits;
   c.P = next_pow2(1 + c.calls);
   if (mp && c.P > (1u << 30)) {
     why = "too many gadget calls for Field64";
@@ -223,6 +258,11 @@ static int32_t make_cfg(const jx_prio3_params* p, const uint8_t* vk, uint32_t vk
   c.gpoly_len = 2 * (c.P - 1) + 1;
   c.proof_len = arity + c.gpoly_len;
   c.ver_len = arity + 2;
+  if (fp) {  // gadget 1's sub-proof [seeds || gadget poly] and verifier part [wires || G1(t1)]
+    c.proof1_off = c.proof_len;
+    c.proof_len += c.chunk1 + c.gpoly1_len;
+    c.ver_len += c.chunk1 + 1;
+  }
   const uint32_t fb = (c.algo == ALGO_COUNT || mp) ? 8 : 16;
   c.fb = fb;
   const bool jr = c.jr_len > 0;
@@ -243,12 +283,18 @@ static int32_t make_cfg(const jx_prio3_params* p, const uint8_t* vk, uint32_t vk
     c.ncoef = COEF_K + c.calls;
   else
     c.ncoef = COEF_K + 2 * c.calls;
+  if (fp) {
+    c.coef1 = c.ncoef;
+    c.ncoef += G1_K + c.calls1;
+  }
   for (int i = 0; i < 4; i++)
     c.vk[i] = (uint32_t)vk[4 * i] | ((uint32_t)vk[4 * i + 1] << 8) | ((uint32_t)vk[4 * i + 2] << 16) |
               ((uint32_t)vk[4 * i + 3] << 24);
   c.c_omega = 0;
   c.c_S = c.P;
   c.c_misc = c.P + c.gpoly_len;
+  c.c_omega1 = c.c_misc + NMISC;
+  c.c_S1 = c.c_omega1 + c.P1;
   return JX_OK;
 }
 
@@ -261,8 +307,26 @@ static uint4 h_u4_64(uint64_t v) {
   return r;
 }
 
+// w1^k R (k < P1) and S1_m R for gadget 1 of FixedPointBoundedL2VecSum
+static void root_tables(f128 gen, uint32_t P, uint32_t logP, uint32_t calls, uint32_t glen, uint4* omega, uint4* S) {
+  f128 w = gen;
+  for (int i = 0; i < 66 - (int)logP; i++) w = mont128(w, w);
+  f128 wk = make128(R1_128_LO, R1_128_HI);
+  std::vector<f128> pw(P);
+  for (uint32_t k = 0; k < P; k++) {
+    pw[k] = wk;
+    omega[k] = h_u4(wk);
+    wk = mont128(wk, w);
+  }
+  for (uint32_t m = 0; m < glen; m++) {
+    f128 s = make128(0, 0);
+    for (uint32_t k = 1; k <= calls; k++) s = add128(s, pw[(uint64_t)(k * m) % P]);
+    S[m] = h_u4(s);
+  }
+}
+
 static std::vector<uint4> make_consts(const Cfg& c) {
-  std::vector<uint4> t(c.P + c.gpoly_len + 4);
+  std::vector<uint4> t(c.P + c.gpoly_len + NMISC + c.P1 + c.gpoly1_len);
   if (c.algo == ALGO_COUNT) return t;
   if (c.algo == ALGO_SUMVEC_F64_MULTIPROOF) {
     // Field64: GEN = 7^((p-1)/2^32) (order 2^32), w = GEN^(2^(32 - logP)); canonical values
@@ -285,26 +349,22 @@ static std::vector<uint4> make_consts(const Cfg& c) {
   }
   // GEN = 7^((p-1)/2^66), order 2^66; w = GEN^(2^(66 - logP))
   f128 gen = h_mpow(to_mont128(h_from_u64(7)), 4611686018427387897ull);
-  f128 w = gen;
-  for (int i = 0; i < 66 - (int)c.logP; i++) w = mont128(w, w);
-  f128 wk = make128(R1_128_LO, R1_128_HI);
-  std::vector<f128> pw(c.P);
-  for (uint32_t k = 0; k < c.P; k++) {
-    pw[k] = wk;
-    t[c.c_omega + k] = h_u4(wk);
-    wk = mont128(wk, w);
-  }
-  for (uint32_t m = 0; m < c.gpoly_len; m++) {
-    f128 s = make128(0, 0);
-    for (uint32_t k = 1; k <= c.calls; k++) s = add128(s, pw[(uint64_t)(k * m) % c.P]);
-    t[c.c_S + m] = h_u4(s);
-  }
+  root_tables(gen, c.P, c.logP, c.calls, c.gpoly_len, &t[c.c_omega], &t[c.c_S]);
   f128 invP = h_minv(to_mont128(h_from_u64(c.P)));
   f128 half_m = h_minv(to_mont128(h_from_u64(2)));
   t[c.c_misc + 0] = h_u4(invP);                     // (1/P) R
   t[c.c_misc + 1] = h_u4(from_mont128(half_m));     // 1/2 canonical
   t[c.c_misc + 2] = h_u4(make128(R1_128_LO, R1_128_HI));
   t[c.c_misc + 3] = h_u4(half_m);                   // (1/2) R
+  if (c.algo == ALGO_FIXEDPOINT_L2) {
+    const uint32_t n = c.bits;
+    t[c.c_misc + 4] = h_u4(make128(n < 64 ? 1ull << n : 0, n >= 64 ? 1ull << (n - 64) : 0));  // 2^n
+    const uint32_t e2 = 2 * n - 2;                                                           // 2^(2n-2) R^-1
+    t[c.c_misc + 5] = h_u4(from_mont128(make128(e2 < 64 ? 1ull << e2 : 0, e2 >= 64 ? 1ull << (e2 - 64) : 0)));
+    t[c.c_misc + 6] = h_u4(make128(1ull << (n - 2), 0));                                      // 2^(n-2)
+    t[c.c_misc + 7] = h_u4(h_minv(to_mont128(h_from_u64(c.P1))));                            // (1/P1) R
+    root_tables(gen, c.P1, c.logP1, c.calls1, c.gpoly1_len, &t[c.c_omega1], &t[c.c_S1]);
+  }
   return t;
 }
 
@@ -337,7 +397,7 @@ static void free_staging(jx_engine* e) {
 static uint32_t stage_eb(const Cfg& c) { return c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? 8u : 16u; }
 static uint64_t coef_elems(const Cfg& c) { return c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? (uint64_t)c.np * c.nco : c.ncoef; }
 static uint64_t part_bytes(const Cfg& c) {
-  return c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? 24ull * c.np * c.ngroups : 64ull * c.ngroups;
+  return c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? 24ull * c.np * c.ngroups : 64ull * c.ngt;
 }
 
 static uint64_t per_report_bytes(const Cfg& c) {

@@ -14,6 +14,10 @@ enum Algo : uint32_t {
   // Prio3SumVecField64MultiproofHmacSha256Aes128 (core/src/vdaf.rs:173-199): Field64, num_proofs
   // >= 2, XofHmacSha256Aes128 with 32-byte seeds (kernels: jx_mp64.hip)
   ALGO_SUMVEC_F64_MULTIPROOF = 4,
+  // Prio3FixedPointBoundedL2VecSum{bitsize 16 | 32, length} (core/src/vdaf.rs:86-91, aggregator.rs:916-932):
+  // Field128, TurboSHAKE, two gadgets: ParallelSum(Mul, chunk) range check over every input bit and
+  // ParallelSum(PolyEval(2^(2n-2) - 2^n y + y^2), chunk1) over the decoded entries (the squared norm)
+  ALGO_FIXEDPOINT_L2 = 5,
 };
 constexpr uint32_t MP_MAX_PROOFS = 8;  // num_proofs supported by the multiproof kernels
 
@@ -38,6 +42,7 @@ struct Cfg {
   uint32_t ncoef;        // coefficient slots per report
   uint32_t out_is_meas;  // truncate == identity (Histogram): output share aliases the meas staging
   uint32_t ppw, ngroups; // ParallelSum FLP: chunk slots per group, groups per 64-report block
+  uint32_t ngt;          // partial-sum groups per block over all gadgets (ngroups [+ ngroups1])
   uint32_t vk[4];
   // constant table offsets (uint4 units) in Bufs::consts
   uint32_t c_omega, c_S, c_misc;
@@ -49,6 +54,14 @@ struct Cfg {
   // multiproof: HMAC-SHA256 inner/outer states after the key block, for the 32-byte verify key
   // (query randomness) and the all-zero key (joint-rand seed derivations)
   uint32_t vk_ist[8], vk_ost[8], zero_ist[8], zero_ost[8];
+  uint32_t trunc_len;  // measurement elements that truncate into the output share (SumVec/Sum/FixedPoint)
+  uint32_t qr_len;     // query randomness elements (= gadgets)
+  // FixedPointBoundedL2VecSum: the norm bits and gadget 1 (ParallelSum(PolyEval), arity chunk1)
+  uint32_t norm_bits;
+  uint32_t chunk1, calls1, P1, logP1, gpoly1_len, ppw1, ngroups1;
+  uint32_t proof1_off;  // first element of gadget 1's sub-proof [seeds (chunk1) || gadget poly]
+  uint32_t coef1;       // first coefficient slot of gadget 1 (G1_* below)
+  uint32_t c_omega1, c_S1;  // constant-table offsets of gadget 1's roots and S1_m
 };
 
 // coefficient slots (Montgomery form unless noted) for the ParallelSum / Sum FLP
@@ -61,6 +74,16 @@ enum : uint32_t {
   COEF_R2 = 5,       // joint_rand[1] (Histogram)
   COEF_K = 6,        // first per-call slot
 };
+// FixedPoint gadget-1 coefficient slots, relative to Cfg::coef1 (Montgomery form)
+enum : uint32_t {
+  G1_L = 0,   // (t1^P1 - 1)/P1
+  G1_C0 = 1,  // c'_0 = 1/(t1 - 1)
+  G1_T = 2,   // t1
+  G1_K = 3,   // c'_k, k = 1..calls1
+};
+// misc constants (uint4 slots at Cfg::c_misc): 0 (1/P)R, 1 1/2, 2 R, 3 (1/2)R; FixedPoint: 4 2^n,
+// 5 2^(2n-2) R^-1, 6 2^(n-2) (gadget-1 padding, a share of the encoded 0.0), 7 (1/P1)R
+constexpr uint32_t NMISC = 8;
 
 struct Bufs {
   uint64_t n;  // reports in this launch

@@ -278,7 +278,7 @@ __device__ __forceinline__ void emit_meas(const Cfg& c, uint4* mp, uint4* op, ui
   if (e >= c.meas_len) return;
   gmax = max(gmax, ge_screen(v));
   mp[(uint64_t)e * IL] = v;
-  if (!c.out_is_meas) {
+  if (!c.out_is_meas && e < c.trunc_len) {  // FixedPoint: the trailing norm bits are not truncated
     const uint32_t sh = 1u << tr.j;
     tr.T[0] += (uint64_t)v.x * sh;
     tr.T[1] += (uint64_t)v.y * sh;
@@ -298,10 +298,53 @@ __device__ __forceinline__ void emit_proof(const Cfg& c, uint4* pp, uint32_t e, 
   pp[(uint64_t)e * IL] = v;
 }
 
-// slot of c_k (k = 0..calls) in the coefficient table
-__device__ __forceinline__ uint32_t slot_c(const Cfg& c, uint32_t k) {
-  if (k == 0) return COEF_C0;
-  return c.algo == ALGO_SUM ? COEF_K + (k - 1) : COEF_K + 2 * (k - 1);
+// Barycentric weights of one gadget on the P-th roots of unity w^k (Montgomery form):
+//   c_k = w^k / (t - w^k) for k = 1..C at slot sk + stride*(k-1), c_0 = 1/(t - 1) at slot s0,
+// by one batch inversion (prefix products parked in the c_k slots, then one inversion chain).
+// Returns sum_{k>=1} c_k.
+__device__ f128 bary_coeffs(uint4* coef, uint64_t blk, uint32_t NC, uint32_t lane, f128 tR, const uint4* omega,
+                            uint32_t C, uint32_t s0, uint32_t sk, uint32_t stride) {
+  auto slot = [&](uint32_t k) { return k == 0 ? s0 : sk + stride * (k - 1); };
+  f128 acc = sub128(tR, u4_to_f(omega[0]));
+  st_il(coef, blk, NC, slot(0), lane, acc);
+  for (uint32_t k = 1; k <= C; k++) {
+    acc = mont128(acc, sub128(tR, u4_to_f(omega[k])));
+    st_il(coef, blk, NC, slot(k), lane, acc);
+  }
+  f128 inv = minv(acc);
+  f128 sumc = make128(0, 0);
+  for (uint32_t k = C; k >= 1; k--) {
+    f128 pre = ld_il(coef, blk, NC, slot(k - 1), lane);
+    f128 w = u4_to_f(omega[k]);
+    f128 invden = mont128(inv, pre);
+    inv = mont128(inv, sub128(tR, w));
+    f128 ck = mont128(w, invden);
+    st_il(coef, blk, NC, slot(k), lane, ck);
+    sumc = add128(sumc, ck);
+  }
+  st_il(coef, blk, NC, s0, lane, inv);  // c_0 = 1/(t - 1)
+  return sumc;
+}
+
+// `cnt` (<= 2) Field128 samples from an XOF stream whose first block is in S. Fast path: the first
+// two 16-byte chunks, FLAG_SLOW if one is >= p; slow path: rejection sampling (a rejection stays in
+// the first block except with probability ~2^-600, beyond which chunks straddling blocks are skipped).
+__device__ void sample2_f128(uint32_t* S, f128 out[2], uint32_t cnt, bool slow, uint32_t& flags) {
+  if (!slow) {
+    out[0] = w4_to_f(S[0], S[1], S[2], S[3]);
+    out[1] = w4_to_f(S[4], S[5], S[6], S[7]);
+    if (ge_p128(out[0]) || (cnt > 1 && ge_p128(out[1]))) flags |= FLAG_SLOW;
+    return;
+  }
+  out[1] = make128(0, 0);
+  uint32_t k = 0;
+  for (int guard = 0; guard < 64 && k < cnt; guard++) {
+    for (int ci = 0; ci < 10 && k < cnt; ci++) {
+      f128 v = w4_to_f(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]);
+      if (!ge_p128(v)) out[k++] = v;
+    }
+    if (k < cnt) keccak_p12(S);
+  }
 }
 
 // Tail of the XOF stage shared by the fast and slow kernels: joint randomness,
@@ -318,7 +361,7 @@ __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t
   {
     Block m;
     blk_zero(m);
-    int pos = blk_xof_prefix(m, c.algo, 6, zero);
+    int pos = blk_xof_prefix(m, c.dst_id, 6, zero);
 #pragma unroll
     for (int i = 0; i < 4; i++) blk_put_word(m, pos + 4 * i, part_l[i]);
 #pragma unroll
@@ -333,27 +376,11 @@ __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t
   {
     Block m;
     blk_zero(m);
-    int pos = blk_xof_prefix(m, c.algo, 3, corr);
+    int pos = blk_xof_prefix(m, c.dst_id, 3, corr);
     blk_put_byte(m, pos, 1);
     blk_pad(m, pos + 1);
     sponge_oneblock(S, m);
-    if (!slow) {
-      jr[0] = w4_to_f(S[0], S[1], S[2], S[3]);
-      jr[1] = w4_to_f(S[4], S[5], S[6], S[7]);
-      if (ge_p128(jr[0]) || (c.jr_len > 1 && ge_p128(jr[1]))) flags |= FLAG_SLOW;
-    } else {
-      // general rejection sampling (stays within the first block with overwhelming probability;
-      // beyond it we permute and continue)
-      int cnt = 0;
-      for (int guard = 0; guard < 64 && cnt < 2; guard++) {
-        for (int ci = 0; ci < 10 && cnt < 2; ci++) {
-          f128 v = w4_to_f(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]);
-          if (!ge_p128(v)) jr[cnt++] = v;
-        }
-        // chunks beyond the tenth straddle blocks; only reachable after 10 rejections (p ~ 2^-600)
-        if (cnt < 2) keccak_p12(S);
-      }
-    }
+    sample2_f128(S, jr, c.jr_len, slow, flags);
   }
   // prepare message = XOF(0^16, DST(6), leader's part || part_H); equals corr when the
   // leader's part matches the public share.
@@ -363,7 +390,7 @@ __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t
   if (!same) {
     Block m;
     blk_zero(m);
-    int pos = blk_xof_prefix(m, c.algo, 6, zero);
+    int pos = blk_xof_prefix(m, c.dst_id, 6, zero);
 #pragma unroll
     for (int i = 0; i < 4; i++) blk_put_word(m, pos + 4 * i, lead_part[i]);
 #pragma unroll
@@ -375,36 +402,20 @@ __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t
     if (msg[0] != corr[0] || msg[1] != corr[1] || msg[2] != corr[2] || msg[3] != corr[3]) flags |= FLAG_NEXT_FAIL;
   }
   if (write_msg) *reinterpret_cast<uint4*>(b.msgs + 16 * r) = make_uint4(msg[0], msg[1], msg[2], msg[3]);
-  // query_rands = expand(verify_key, DST(5), [PROOFS=1] || nonce, 1)
-  f128 t;
+  // query_rands = expand(verify_key, DST(5), [PROOFS=1] || nonce, QR_LEN): one t per gadget
+  f128 tq[2];
   {
     Block m;
     blk_zero(m);
-    int pos = blk_xof_prefix(m, c.algo, 5, c.vk);
+    int pos = blk_xof_prefix(m, c.dst_id, 5, c.vk);
     blk_put_byte(m, pos, 1);
 #pragma unroll
     for (int i = 0; i < 4; i++) blk_put_word(m, pos + 1 + 4 * i, nonce[i]);
     blk_pad(m, pos + 17);
     sponge_oneblock(S, m);
-    t = w4_to_f(S[0], S[1], S[2], S[3]);
-    if (ge_p128(t)) {
-      if (!slow) {
-        flags |= FLAG_SLOW;
-      } else {
-        bool found = false;
-        for (int guard = 0; guard < 64 && !found; guard++) {
-          for (int ci = 0; ci < 10 && !found; ci++) {
-            f128 v = w4_to_f(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]);
-            if (!ge_p128(v)) {
-              t = v;
-              found = true;
-            }
-          }
-          if (!found) keccak_p12(S);
-        }
-      }
-    }
+    sample2_f128(S, tq, c.qr_len, slow, flags);
   }
+  const f128 t = tq[0];
   // ---- FLP coefficients (Montgomery form). Barycentric weights on the P-th roots:
   //   wire_j(t) = L * sum_k c_k * wire_j[k],  c_k = w^k / (t - w^k),  L = (t^P - 1)/P
   const uint4* omega = b.consts + c.c_omega;
@@ -422,26 +433,10 @@ __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t
   f128 rR = to_mont128(jr[0]);
   st_il(coef, blk, NC, COEF_R, lane, rR);
   st_il(coef, blk, NC, COEF_R2, lane, to_mont128(jr[1]));
-  // batch inversion of den_k = t - w^k, k = 0..calls (prefix products parked in the c_k slots)
+  // batch inversion of den_k = t - w^k, k = 0..calls
   const uint32_t C = c.calls;
-  f128 acc = sub128(tR, u4_to_f(omega[0]));
-  st_il(coef, blk, NC, slot_c(c, 0), lane, acc);
-  for (uint32_t k = 1; k <= C; k++) {
-    acc = mont128(acc, sub128(tR, u4_to_f(omega[k])));
-    st_il(coef, blk, NC, slot_c(c, k), lane, acc);
-  }
-  f128 inv = minv(acc);
-  f128 sumc = make128(0, 0);
-  for (uint32_t k = C; k >= 1; k--) {
-    f128 pre = ld_il(coef, blk, NC, slot_c(c, k - 1), lane);
-    f128 w = u4_to_f(omega[k]);
-    f128 invden = mont128(inv, pre);
-    inv = mont128(inv, sub128(tR, w));
-    f128 ck = mont128(w, invden);
-    st_il(coef, blk, NC, slot_c(c, k), lane, ck);
-    sumc = add128(sumc, ck);
-  }
-  st_il(coef, blk, NC, COEF_C0, lane, inv);  // c_0 = 1/(t - 1)
+  const uint32_t stride = c.algo == ALGO_SUM ? 1u : 2u;
+  const f128 sumc = bary_coeffs(coef, blk, NC, lane, tR, omega, C, COEF_C0, COEF_K, stride);
   // (1/2) * sum c_k, canonical: mont(sumc*R, 1/2) = sumc/2
   st_il(coef, blk, NC, COEF_HALFSUM, lane, mont128(sumc, u4_to_f(misc[1])));
   if (c.algo != ALGO_SUM) {
@@ -449,10 +444,22 @@ __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t
     f128 rc = mpow(rR, c.chunk);
     f128 rp = R1;
     for (uint32_t k = 1; k <= C; k++) {
-      f128 ck = ld_il(coef, blk, NC, slot_c(c, k), lane);
-      st_il(coef, blk, NC, slot_c(c, k) + 1, lane, mont128(ck, rp));
+      const uint32_t sk = COEF_K + 2 * (k - 1);
+      f128 ck = ld_il(coef, blk, NC, sk, lane);
+      st_il(coef, blk, NC, sk + 1, lane, mont128(ck, rp));
       rp = mont128(rp, rc);
     }
+  }
+  if (c.algo == ALGO_FIXEDPOINT_L2) {
+    // gadget 1 (the norm's ParallelSum(PolyEval)): its own query randomness t1 and P1-th roots
+    const f128 t1R = to_mont128(tq[1]);
+    f128 tp1 = t1R;
+    for (uint32_t i = 0; i < c.logP1; i++) tp1 = mont128(tp1, tp1);
+    if (eq128(tp1, R1)) flags |= FLAG_INIT_FAIL;
+    const uint32_t B = c.coef1;
+    st_il(coef, blk, NC, B + G1_L, lane, mont128(sub128(tp1, R1), u4_to_f(misc[7])));
+    st_il(coef, blk, NC, B + G1_T, lane, t1R);
+    (void)bary_coeffs(coef, blk, NC, lane, t1R, b.consts + c.c_omega1, c.calls1, B + G1_C0, B + G1_K, 1);
   }
   return flags;
 }
@@ -512,7 +519,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
     load16(hs, kmeas);
     Block m;
     blk_zero(m);
-    int pos = blk_xof_prefix(m, c.algo, 1, kmeas);
+    int pos = blk_xof_prefix(m, c.dst_id, 1, kmeas);
     blk_put_byte(m, pos, 1);
     blk_pad(m, pos + 1);
     sponge_oneblock(S, m);
@@ -524,7 +531,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
     load16(LEADER ? ls + MB + 16 * c.proof_len : hs + 32, kblind);
     Block h;
     blk_zero(h);
-    int pos = blk_xof_prefix(h, c.algo, 7, kblind);
+    int pos = blk_xof_prefix(h, c.dst_id, 7, kblind);
     blk_put_byte(h, pos, LEADER ? 0 : 1);  // agg_id
 #pragma unroll
     for (int i = 0; i < 4; i++) blk_put_word(h, pos + 1 + 4 * i, nonce[i]);
@@ -667,7 +674,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
       load16(hs + 16, kproof);
       Block m;
       blk_zero(m);
-      int pos = blk_xof_prefix(m, c.algo, 2, kproof);
+      int pos = blk_xof_prefix(m, c.dst_id, 2, kproof);
       blk_put_byte(m, pos, 1);
       blk_put_byte(m, pos + 1, 1);
       blk_pad(m, pos + 2);
@@ -787,7 +794,7 @@ __global__ __launch_bounds__(64) void xof_slow_kernel(Cfg c, Bufs b) {
   {
     Block m;
     blk_zero(m);
-    int pos = blk_xof_prefix(m, c.algo, 1, kmeas);
+    int pos = blk_xof_prefix(m, c.dst_id, 1, kmeas);
     blk_put_byte(m, pos, 1);
     blk_pad(m, pos + 1);
     sponge_oneblock(X.s, m);
@@ -798,7 +805,7 @@ __global__ __launch_bounds__(64) void xof_slow_kernel(Cfg c, Bufs b) {
   {
     Block h;
     blk_zero(h);
-    int pos = blk_xof_prefix(h, c.algo, 7, kblind);
+    int pos = blk_xof_prefix(h, c.dst_id, 7, kblind);
     blk_put_byte(h, pos, 1);
     for (int i = 0; i < 4; i++) blk_put_word(h, pos + 1 + 4 * i, nonce[i]);
     for (int i = 0; i < 42; i++) ba_byte(A, h.w[i >> 2] >> (8 * (i & 3)));
@@ -814,7 +821,7 @@ __global__ __launch_bounds__(64) void xof_slow_kernel(Cfg c, Bufs b) {
     ba_word(A, hi32(x.lo));
     ba_word(A, lo32(x.hi));
     ba_word(A, hi32(x.hi));
-    if (!c.out_is_meas) {
+    if (!c.out_is_meas && e < c.trunc_len) {
       trunc_add(tr.a, x, tr.j);
       if (++tr.j == c.bits) {
         st_il(b.outs, blk, c.out_len, tr.i, lane, acc_reduce(tr.a));
@@ -831,7 +838,7 @@ __global__ __launch_bounds__(64) void xof_slow_kernel(Cfg c, Bufs b) {
   {
     Block m;
     blk_zero(m);
-    int pos = blk_xof_prefix(m, c.algo, 2, kproof);
+    int pos = blk_xof_prefix(m, c.dst_id, 2, kproof);
     blk_put_byte(m, pos, 1);
     blk_put_byte(m, pos + 1, 1);
     blk_pad(m, pos + 2);
@@ -1098,7 +1105,7 @@ __global__ __launch_bounds__(64, 4) void flp_psum_part_kernel(Cfg c, Bufs b) {
     }
     gpart = mont128(gpart, mpow(tR, m0));
   }
-  uint4* pp = b.part + ((blk * NG + g) * 4) * IL + lane;
+  uint4* pp = b.part + ((blk * c.ngt + g) * 4) * IL + lane;
   pp[0] = f_to_u4(prod);
   pp[IL] = f_to_u4(vpart);
   pp[2 * IL] = f_to_u4(gpart);
@@ -1113,7 +1120,7 @@ __global__ __launch_bounds__(256) void flp_psum_final_kernel(Cfg c, Bufs b) {
   const uint64_t blk = r / 64;
   const uint32_t lane = r % 64, NG = c.ngroups, A = 2 * c.chunk;
   f128 P = make128(0, 0), V = make128(0, 0), G = make128(0, 0), SX = make128(0, 0);
-  const uint4* pp = b.part + (blk * NG * 4) * IL + lane;
+  const uint4* pp = b.part + (blk * c.ngt * 4) * IL + lane;
   for (uint32_t g = 0; g < NG; g++, pp += 4 * IL) {
     P = add128(P, u4_to_f(pp[0]));
     V = add128(V, u4_to_f(pp[IL]));
@@ -1146,6 +1153,148 @@ __global__ __launch_bounds__(256) void flp_psum_final_kernel(Cfg c, Bufs b) {
   else {
     f128 V0 = add128(vh, lv), VG = add128(G, lg);
     if (!is_zero128(V0) || !eq128(P, mont128(VG, make128(1, 0))))
+      verdict = 3;
+    else if (flags & FLAG_NEXT_FAIL)
+      verdict = 4;
+  }
+  b.verdicts[r] = (uint8_t)verdict;
+}
+
+// Prio3FixedPointBoundedL2VecSum, gadget 1: ParallelSum(PolyEval(p), chunk1) over the decoded entries
+// y (= the output share, already truncated by K1), p(y) = 2^(2n-2) - 2^n y + y^2. One wave per
+// (64-report block, group of PPW slots). Wire j at t1 is the barycentric sum
+//   W_j = L1 (c'_0 s_j + sum_k c'_k y_{(k-1) chunk1 + j} + [short last chunk] c'_last 2^(n-2)),
+// the padding value 2^(n-2) being the share of the encoded 0.0 (2^(n-1) / num_shares). The group
+// also writes its share of v's gadget-1 part (sum_m g_m S1_m) and of G1(t1), and (helper) the sum of
+// p(V_j) over its slots, V_j = own + leader wire, in the R^-1 domain of the decide compare.
+template <int PPW, bool LEADER>
+__global__ __launch_bounds__(64, 4) void flp_norm_part_kernel(Cfg c, Bufs b) {
+  const uint32_t NG = c.ngroups1;
+  const uint32_t bid = blockIdx.x;
+  const uint32_t xcd = bid & 7u, q = bid >> 3;
+  const uint32_t g = q % NG;
+  const uint64_t blk = (uint64_t)(q / NG) * 8 + xcd;
+  const uint64_t nblk = (b.n + 63) / 64;
+  if (blk >= nblk) return;
+  const uint32_t lane = threadIdx.x;
+  const uint64_t r0 = blk * 64 + lane;
+  const uint64_t r = r0 < b.n ? r0 : b.n - 1;
+  const uint32_t NC = c.ncoef, C = c.calls1, ch = c.chunk1, E = c.out_len, B = c.coef1;
+  const uint32_t j0 = g * PPW;
+  const uint4* coefb = b.coef + il_idx(blk, NC, 0, lane);
+  const uint4* outb = b.outs + il_idx(blk, E, 0, lane);
+  wacc26 ao[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; i++) wacc_zero(ao[i]);
+#pragma unroll 1
+  for (uint32_t k = 1; k <= C; k++) {
+    const limbs26 ck = to_limbs26(u4_to_f(coefb[(B + G1_K + k - 1) * IL]));
+    const uint32_t nb = (k - 1) * ch + j0;
+#pragma unroll
+    for (int i = 0; i < PPW; i++) {
+      if (j0 + i < ch && nb + i < E) wacc_mac(ao[i], to_limbs26(u4_to_f(outb[(uint64_t)(nb + i) * IL])), ck);
+    }
+    if ((k & 511u) == 0) {
+#pragma unroll
+      for (int i = 0; i < PPW; i++) wacc_normalize(ao[i]);
+    }
+  }
+  const uint4* misc = b.consts + c.c_misc;
+  const f128 LR = u4_to_f(coefb[(B + G1_L) * IL]), c0R = u4_to_f(coefb[(B + G1_C0) * IL]);
+  const f128 tR = u4_to_f(coefb[(B + G1_T) * IL]);
+  const f128 cl = u4_to_f(coefb[(B + G1_K + C - 1) * IL]);  // c'_calls1 (the possibly short last call)
+  const f128 pad = mont128(u4_to_f(misc[6]), cl);          // 2^(n-2) c'_last, canonical
+  const f128 twon = u4_to_f(misc[4]), K = u4_to_f(misc[5]);
+  const uint32_t A0 = 2 * c.chunk;  // gadget 0's arity: gadget 1's wires follow it in the verifier
+  bool dfail = false;
+  f128 prod = make128(0, 0);
+#pragma unroll
+  for (int i = 0; i < PPW; i++) {
+    const uint32_t j = j0 + i;
+    if (j < ch) {
+      const f128 s = ld_il(b.proof, blk, c.proof_len, c.proof1_off + j, lane);
+      f128 O = mont128(wacc_reduce(ao[i]), make128(1, 0));  // sum_k c'_k y (canonical)
+      if ((C - 1) * ch + j >= E) O = add128(O, pad);
+      const f128 W = mont128(add128(mont128(s, c0R), O), LR);
+      if (LEADER) {
+        if (r0 < b.n) reinterpret_cast<uint4*>(b.lps_out + (uint64_t)c.lps_bytes * r)[A0 + 2 + j] = f_to_u4(W);
+      } else {
+        const f128 V = add128(W, ld_lead(b, c, r, A0 + 2 + j, dfail));
+        // p(V) R^-1 = V^2 R^-1 - 2^n V R^-1 + 2^(2n-2) R^-1
+        prod = add128(prod, add128(sub128(mont128(V, V), mont128(V, twon)), K));
+      }
+    }
+  }
+  const uint32_t GL = c.gpoly1_len;
+  const uint32_t per = (GL + NG - 1) / NG;
+  const uint32_t m0 = g * per, m1 = min(GL, m0 + per);
+  const uint4* Sm = b.consts + c.c_S1;
+  const uint32_t goff = c.proof1_off + ch;
+  f128 vpart = make128(0, 0), gpart = make128(0, 0);
+  if (m0 < m1) {
+    for (uint32_t m = m1; m-- > m0;) {
+      f128 gm = ld_il(b.proof, blk, c.proof_len, goff + m, lane);
+      vpart = add128(vpart, mont128(gm, u4_to_f(Sm[m])));
+      gpart = add128(mont128(gpart, tR), gm);
+    }
+    gpart = mont128(gpart, mpow(tR, m0));
+  }
+  uint4* pp = b.part + ((blk * c.ngt + c.ngroups + g) * 4) * IL + lane;
+  pp[0] = f_to_u4(prod);
+  pp[IL] = f_to_u4(vpart);
+  pp[2 * IL] = f_to_u4(gpart);
+  if (dfail && r0 < b.n) atomicOr(&b.flags[r0], FLAG_DFAIL);
+}
+
+// FixedPoint decide: v = jr1 * range_check + jr1^2 * (computed_norm - claimed_norm) where range_check
+// = sum_m g0_m S0_m and computed_norm = sum_m g1_m S1_m (the circuit's gadget outputs, as shares) and
+// claimed_norm = sum_b 2^b x[entries*n + b]; then both gadgets' G(wires(t_g)) == gadget_poly_g(t_g).
+template <bool LEADER>
+__global__ __launch_bounds__(256) void flp_fp_final_kernel(Cfg c, Bufs b) {
+  const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= b.n) return;
+  const uint64_t blk = r / 64;
+  const uint32_t lane = r % 64, NG0 = c.ngroups, NG1 = c.ngroups1, A0 = 2 * c.chunk, A1 = c.chunk1;
+  f128 P0 = make128(0, 0), V0 = P0, G0 = P0, P1 = P0, V1 = P0, G1 = P0;
+  const uint4* pp = b.part + (blk * c.ngt * 4) * IL + lane;
+  for (uint32_t g = 0; g < NG0; g++, pp += 4 * IL) {
+    P0 = add128(P0, u4_to_f(pp[0]));
+    V0 = add128(V0, u4_to_f(pp[IL]));
+    G0 = add128(G0, u4_to_f(pp[2 * IL]));
+  }
+  for (uint32_t g = 0; g < NG1; g++, pp += 4 * IL) {
+    P1 = add128(P1, u4_to_f(pp[0]));
+    V1 = add128(V1, u4_to_f(pp[IL]));
+    G1 = add128(G1, u4_to_f(pp[2 * IL]));
+  }
+  // claimed squared norm: the trailing norm_bits measurement elements, LE bits
+  acc192 cn;
+  acc_zero(cn);
+  const uint32_t nb0 = c.trunc_len;
+  for (uint32_t i = 0; i < c.norm_bits; i++) trunc_add(cn, ld_il(b.meas, blk, c.meas_len, nb0 + i, lane), i);
+  const f128 claimed = acc_reduce(cn);
+  const f128 r2R = ld_il(b.coef, blk, c.ncoef, COEF_R2, lane);
+  const f128 vh = add128(mont128(V0, r2R), mont128(sub128(V1, claimed), mont128(r2R, r2R)));
+  const uint32_t flags = b.flags[r];
+  if (LEADER) {
+    uint4* o = reinterpret_cast<uint4*>(b.lps_out + (uint64_t)c.lps_bytes * r);
+    o[0] = f_to_u4(vh);
+    o[A0 + 1] = f_to_u4(G0);
+    o[A0 + 2 + A1] = f_to_u4(G1);
+    b.verdicts[r] = (flags & (FLAG_INIT_FAIL | FLAG_INPUT_FAIL)) ? 1 : 0;
+    return;
+  }
+  bool df = (flags & FLAG_DFAIL) != 0;
+  const f128 lv = ld_lead(b, c, r, 0, df), lg0 = ld_lead(b, c, r, A0 + 1, df), lg1 = ld_lead(b, c, r, A0 + 2 + A1, df);
+  uint32_t verdict = 0;
+  if (flags & FLAG_INIT_FAIL)
+    verdict = 1;
+  else if (df)
+    verdict = 2;
+  else {
+    const f128 one = make128(1, 0);
+    if (!is_zero128(add128(vh, lv)) || !eq128(P0, mont128(add128(G0, lg0), one)) ||
+        !eq128(P1, mont128(add128(G1, lg1), one)))
       verdict = 3;
     else if (flags & FLAG_NEXT_FAIL)
       verdict = 4;
@@ -1508,7 +1657,33 @@ static hipError_t launch_psum_t(const Cfg& c, const Bufs& b, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int PPW, bool LEADER>
+static void launch_fp_r(const Cfg& c, const Bufs& b, hipStream_t s) {
+  const uint32_t nb = nblk_of(b.n);
+  hipLaunchKernelGGL((flp_psum_part_kernel<PPW, false, LEADER>), dim3(((nb + 7) / 8) * 8 * c.ngroups), dim3(64), 0,
+                     s, c, b);
+  hipLaunchKernelGGL((flp_norm_part_kernel<2, LEADER>), dim3(((nb + 7) / 8) * 8 * c.ngroups1), dim3(64), 0, s, c,
+                     b);
+  hipLaunchKernelGGL((flp_fp_final_kernel<LEADER>), dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, c, b);
+}
+
 hipError_t launch_flp(const Cfg& c, const Bufs& b, hipStream_t s) {
+  if (c.algo == ALGO_FIXEDPOINT_L2) {
+    if (c.ppw == 2) {
+      if (b.leader)
+        launch_fp_r<2, true>(c, b, s);
+      else
+        launch_fp_r<2, false>(c, b, s);
+    } else if (c.ppw == 1) {
+      if (b.leader)
+        launch_fp_r<1, true>(c, b, s);
+      else
+        launch_fp_r<1, false>(c, b, s);
+    } else {
+      return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if (c.algo == ALGO_SUM) {
     uint32_t nb = nblk_of(b.n);
     if (b.leader)

@@ -17,6 +17,10 @@ VERIFY_KEY_LENGTH_HMACSHA256_AES128 = 32  # core/src/vdaf.rs:24
 # private-use DST algorithm id is 0xFFFF1003)
 PRIO3_COUNT, PRIO3_SUM, PRIO3_SUMVEC, PRIO3_HISTOGRAM = 0, 1, 2, 3
 PRIO3_SUMVEC_F64_MULTIPROOF = 4
+# Prio3FixedPointBoundedL2VecSum{bitsize, length} (core/src/vdaf.rs:86-91, aggregator.rs:916-932;
+# prio's private-use DST algorithm id 0xFFFF0000)
+PRIO3_FIXEDPOINT_L2 = 5
+FIXEDPOINT_BITSIZES = {"BitSize16": 16, "BitSize32": 32}  # Prio3FixedPointBoundedL2VecSumBitSize
 
 
 def _next_pow2(v: int) -> int:
@@ -24,6 +28,11 @@ def _next_pow2(v: int) -> int:
     while p < v:
         p <<= 1
     return p
+
+
+def _isqrt(v: int) -> int:
+    import math
+    return max(1, math.isqrt(v))
 
 
 @dataclass(frozen=True)
@@ -63,6 +72,34 @@ class Prio3:
         return Prio3(PRIO3_SUMVEC_F64_MULTIPROOF, bits=bits, length=length, chunk_length=chunk_length,
                      num_proofs=proofs)
 
+    @staticmethod
+    def fixedpoint_boundedl2_vec_sum(bitsize, length: int) -> "Prio3":
+        """Prio3::new_fixedpoint_boundedl2_vec_sum_multithreaded(2, length) with FixedI16<U15>
+        (bitsize 16 / "BitSize16") or FixedI32<U31> (32 / "BitSize32"), core/src/vdaf.rs:313-334.
+        Measurements are the entries' two's-complement bit patterns; the DP strategy is a
+        collection-time step (add_noise_to_agg_share) and not part of preparation."""
+        bits = FIXEDPOINT_BITSIZES.get(bitsize, bitsize)
+        if bits not in (16, 32):
+            raise ValueError("bitsize must be 16 or 32 (BitSize16 / BitSize32)")
+        return Prio3(PRIO3_FIXEDPOINT_L2, bits=bits, length=length)
+
+    # -- FixedPointBoundedL2VecSum gadget sizes (prio 0.16.1 FixedPointBoundedL2VecSum::new)
+    @property
+    def norm_bits(self) -> int:
+        return 2 * self.bits - 2 if self.algo_id == PRIO3_FIXEDPOINT_L2 else 0
+
+    @property
+    def gadget_chunk(self) -> int:
+        return _isqrt(self.meas_len) if self.algo_id == PRIO3_FIXEDPOINT_L2 else self.chunk_length
+
+    @property
+    def norm_chunk(self) -> int:
+        return _isqrt(self.length)
+
+    @property
+    def norm_calls(self) -> int:
+        return -(-self.length // self.norm_chunk)
+
     # -- derived sizes
     @property
     def seed_size(self) -> int:
@@ -81,6 +118,7 @@ class Prio3:
     def meas_len(self) -> int:
         return {PRIO3_COUNT: 1, PRIO3_SUM: self.bits, PRIO3_SUMVEC: self.bits * self.length,
                 PRIO3_SUMVEC_F64_MULTIPROOF: self.bits * self.length,
+                PRIO3_FIXEDPOINT_L2: self.bits * self.length + 2 * self.bits - 2,
                 PRIO3_HISTOGRAM: self.length}[self.algo_id]
 
     @property
@@ -90,11 +128,12 @@ class Prio3:
     @property
     def joint_rand_len(self) -> int:
         return {PRIO3_COUNT: 0, PRIO3_SUM: 1, PRIO3_SUMVEC: 1, PRIO3_SUMVEC_F64_MULTIPROOF: 1,
-                PRIO3_HISTOGRAM: 2}[self.algo_id]
+                PRIO3_HISTOGRAM: 2, PRIO3_FIXEDPOINT_L2: 2}[self.algo_id]
 
     @property
     def arity(self) -> int:
-        return {PRIO3_COUNT: 2, PRIO3_SUM: 1}.get(self.algo_id, 2 * self.chunk_length)
+        """Arity of the first (range-check) gadget."""
+        return {PRIO3_COUNT: 2, PRIO3_SUM: 1}.get(self.algo_id, 2 * self.gadget_chunk)
 
     @property
     def calls(self) -> int:
@@ -102,7 +141,7 @@ class Prio3:
             return 1
         if self.algo_id == PRIO3_SUM:
             return self.bits
-        return -(-self.meas_len // self.chunk_length)
+        return -(-self.meas_len // self.gadget_chunk)
 
     @property
     def P(self) -> int:
@@ -110,11 +149,17 @@ class Prio3:
 
     @property
     def proof_len(self) -> int:
-        return self.arity + 2 * (self.P - 1) + 1
+        n = self.arity + 2 * (self.P - 1) + 1
+        if self.algo_id == PRIO3_FIXEDPOINT_L2:  # + the norm gadget's [seeds || gadget poly]
+            n += self.norm_chunk + 2 * (_next_pow2(1 + self.norm_calls) - 1) + 1
+        return n
 
     @property
     def verifier_len(self) -> int:
-        return self.arity + 2
+        n = self.arity + 2
+        if self.algo_id == PRIO3_FIXEDPOINT_L2:
+            n += self.norm_chunk + 1
+        return n
 
     @property
     def public_share_len(self) -> int:
@@ -143,4 +188,24 @@ class Prio3:
                 PRIO3_HISTOGRAM: f"Prio3Histogram{{length={self.length},chunk_length={self.chunk_length}}}",
                 PRIO3_SUMVEC_F64_MULTIPROOF: "Prio3SumVecField64MultiproofHmacSha256Aes128"
                 f"{{proofs={self.num_proofs},bits={self.bits},length={self.length},chunk_length={self.chunk_length}}}",
+                PRIO3_FIXEDPOINT_L2: f"Prio3FixedPointBoundedL2VecSum{{bitsize=BitSize{self.bits},length={self.length}}}",
                 }[self.algo_id]
+
+    # -- FixedPointBoundedL2VecSum measurement / result codecs (host side; collection is out of scope)
+    def encode_fixedpoint(self, values) -> list[int]:
+        """f64 entries in [-1, 1) -> FixedI{n}<U{n-1}> bit patterns (round to nearest, like fixed!)."""
+        n = self.bits
+        out = []
+        for v in values:
+            q = int(round(float(v) * (1 << (n - 1))))
+            if not -(1 << (n - 1)) <= q < (1 << (n - 1)):
+                raise ValueError(f"fixed-point entry {v} outside [-1, 1)")
+            out.append(q & ((1 << n) - 1))
+        return out
+
+    def decode_fixedpoint_result(self, agg_share: bytes, num_measurements: int) -> list[float]:
+        """FixedPointBoundedL2VecSum::decode_result on an aggregate (the sum of both aggregators'
+        shares): CompatibleFloat::to_float(d, c) = d * 2^(1-n) - c per entry."""
+        P = 2**128 - 28 * 2**64 + 1
+        vals = [int.from_bytes(agg_share[i:i + 16], "little") % P for i in range(0, len(agg_share), 16)]
+        return [x * 2.0 ** (1 - self.bits) - num_measurements for x in vals]

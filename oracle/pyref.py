@@ -123,10 +123,13 @@ class XofTurboShake128:
     def __init__(self, seed: bytes, dst: bytes, binder: bytes):
         self.m = bytes([len(dst)]) + dst + seed + binder
         self.l = 0
+        self.stream = b""
 
     def next(self, length):
         self.l += length
-        return turboshake128(self.m, 1, self.l)[-length:]
+        if len(self.stream) < self.l:  # squeeze ahead (doubling) instead of re-squeezing per call
+            self.stream = turboshake128(self.m, 1, max(self.l, 2 * len(self.stream), 168))
+        return self.stream[self.l - length:self.l]
 
     def next_vec(self, field, length):
         m = (1 << (8 * field.ENCODED_SIZE)) - 1

@@ -38,6 +38,13 @@ CONFIGS = {
     "sumvec_f64mp_3_1x7_3": dict(algo=O.SUMVEC_F64_MULTIPROOF, bits=1, length=7, chunk=3, proofs=3, n=12),
     "sumvec_f64mp_2_8x1000_88": dict(algo=O.SUMVEC_F64_MULTIPROOF, bits=8, length=1000, chunk=88, proofs=2, n=6),
     "sumvec_f64mp_3_8x1000_88": dict(algo=O.SUMVEC_F64_MULTIPROOF, bits=8, length=1000, chunk=88, proofs=3, n=6),
+    # Prio3FixedPointBoundedL2VecSum: the reference's e2e shape (length 3, both bitsizes), a length
+    # with short last chunks in both gadgets, and the BASELINE configs[4] shape (16-bit, 10000)
+    "fixedpoint16_3": dict(algo=O.FIXEDPOINT_L2, bits=16, length=3, chunk=0, n=12),
+    "fixedpoint32_3": dict(algo=O.FIXEDPOINT_L2, bits=32, length=3, chunk=0, n=12),
+    "fixedpoint16_37": dict(algo=O.FIXEDPOINT_L2, bits=16, length=37, chunk=0, n=12),
+    "fixedpoint32_100": dict(algo=O.FIXEDPOINT_L2, bits=32, length=100, chunk=0, n=12),
+    "fixedpoint16_10000": dict(algo=O.FIXEDPOINT_L2, bits=16, length=10000, chunk=0, n=6),
 }
 
 
@@ -49,7 +56,22 @@ def measurements(cfg, rng, n):
         return rng.integers(0, 1 << cfg["bits"], size=(n, 1), dtype=np.uint64)
     if a == O.HISTOGRAM:
         return rng.integers(0, cfg["length"], size=(n, 1), dtype=np.uint64)
+    if a == O.FIXEDPOINT_L2:
+        return fixedpoint_measurements(cfg["bits"], cfg["length"], rng, n)
     return rng.integers(0, 1 << cfg["bits"], size=(n, cfg["length"]), dtype=np.uint64)
+
+
+def fixedpoint_measurements(bits, length, rng, n, violate_every=6):
+    """FixedI{bits}<U{bits-1}> bit patterns with squared L2 norm < 1/4, except every
+    `violate_every`-th report (index 4 mod 6): entries of 1/2 and -1/2 whose squared norm >= 1
+    (a client lying about its norm; the FLP must reject it)."""
+    half = 1 << (bits - 1)
+    lim = max(1, int(half / (2 * np.sqrt(length))))
+    vals = rng.integers(-lim, lim, size=(n, length), dtype=np.int64)
+    for i in range(n):
+        if violate_every and i % violate_every == 4 and length >= 4:
+            vals[i] = np.where(np.arange(length) % 2 == 0, half // 2, -(half // 2))
+    return (vals & ((1 << bits) - 1)).astype(np.uint64)
 
 
 def tamper(lps: np.ndarray, sizes: O.Sizes, rng) -> list[str]:
@@ -89,8 +111,10 @@ def make(name, cfg):
     for i in range(n):
         v = int(res["verdicts"][i])
         out = res["out_shares"][i].tobytes() if v == 0 else b""
+        m = [int(x) for x in meas[i]]
         rep = {
-            "measurement": [int(x) for x in meas[i]],
+            "measurement": m if len(m) <= 1000 else
+            {"sha256_u64le": hashlib.sha256(meas[i].astype("<u8").tobytes()).hexdigest()},
             "nonce": nonces[i].tobytes().hex(),
             "public_share": ps[i].tobytes().hex(),
             "helper_input_share": his[i].tobytes().hex(),
@@ -113,7 +137,8 @@ def make(name, cfg):
         "verify_key": VK.hex(),
         "sizes": s.__dict__,
         "reports": reports,
-        "aggregate_share": res["agg"].hex(),
+        **({"aggregate_share": res["agg"].hex()} if len(res["agg"]) <= 16000 else
+           {"aggregate_share_sha256": hashlib.sha256(res["agg"]).hexdigest()}),
         "report_count": res["count"],
         "checksum": res["checksum"].hex(),
     }
@@ -125,5 +150,7 @@ def make(name, cfg):
 
 if __name__ == "__main__":
     O.build()
+    only = set(sys.argv[1:])
     for name, cfg in CONFIGS.items():
-        make(name, cfg)
+        if not only or name in only:
+            make(name, cfg)
