@@ -54,6 +54,9 @@ extern "C" {
 #define JX_PREP_SHARE_DECODE_FAILURE 2     /* PingPongError::CodecPrepShare (leader share malformed) */
 #define JX_PREPARE_MESSAGE_FAILURE 3       /* PingPongError::VdafPrepareSharesToPrepareMessage */
 #define JX_PREPARE_NEXT_FAILURE 4          /* PingPongError::VdafPrepareNext */
+/* Leader only: the helper answered PrepareStepResult::Reject for this report (label
+ * helper_step_failure, aggregation_job_driver.rs:646-660). */
+#define JX_HELPER_STEP_FAILURE 5
 
 /* Prio3 instance, mirroring janus_core::vdaf::VdafInstance (core/src/vdaf.rs:65-108).
  * algo_id: 0 Prio3Count, 1 Prio3Sum{bits}, 2 Prio3SumVec{bits,length,chunk_length},
@@ -61,12 +64,18 @@ extern "C" {
  *          4 Prio3SumVecField64MultiproofHmacSha256Aes128{proofs,bits,length,chunk_length}
  *            (core/src/vdaf.rs:173-199: Field64, XofHmacSha256Aes128, 32-byte seeds and verify key;
  *            DST algorithm id 0xFFFF1003; prep messages and joint-rand parts are 32 bytes)
- * num_proofs: 1 for ids 0-3 (the TurboSHAKE variants, core/src/vdaf.rs:203-262); 2..8 for id 4. */
+ *          5 Prio3FixedPointBoundedL2VecSum{bitsize, length} (core/src/vdaf.rs:86-91; built at
+ *            aggregator/src/aggregator.rs:916-932): bits = 16 (BitSize16, FixedI16<U15>) or 32
+ *            (BitSize32, FixedI32<U31>), length = entries, chunk_length ignored (prio derives both
+ *            gadgets' chunk lengths); Field128, TurboSHAKE, DST algorithm id 0xFFFF0000. The
+ *            dp_strategy is applied at collection time and is not part of this ABI.
+ * num_proofs: 1 for ids 0-3 and 5 (the TurboSHAKE variants, core/src/vdaf.rs:203-262); 2..8 for id 4. */
 #define JX_ALGO_COUNT 0
 #define JX_ALGO_SUM 1
 #define JX_ALGO_SUMVEC 2
 #define JX_ALGO_HISTOGRAM 3
 #define JX_ALGO_SUMVEC_F64_MULTIPROOF_HMACSHA256_AES128 4
+#define JX_ALGO_FIXEDPOINT_BOUNDED_L2_VEC_SUM 5
 typedef struct {
   uint32_t algo_id;
   uint32_t bits;
@@ -98,10 +107,15 @@ int32_t jx_engine_set_capacity(jx_engine* e, uint64_t reports);
 /* Batched helper_initialized + evaluate for n reports (host buffers).
  * out_verdicts[n] receives JX_FINISHED or a failure code; out_prep_msgs[n x PM] the outbound
  * Finish{prep_msg} payload (meaningful where verdict == JX_FINISHED); out_output_shares
- * (nullable) the output shares. Output shares stay resident for jx_accumulate. */
+ * (nullable) the output shares. Output shares stay resident for jx_accumulate: the engine holds
+ * one prepared batch at a time, named by a batch id (jx_engine_batch_id); any later prepare call
+ * replaces it, and jx_leader_prep_finish_* / jx_accumulate* refuse (JX_E_STATE) a batch id that no
+ * longer names the resident batch instead of mixing two batches. */
 int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
                              const uint8_t* helper_input_shares, const uint8_t* leader_prep_shares,
                              uint8_t* out_prep_msgs, uint8_t* out_verdicts, uint8_t* out_output_shares);
+/* Id of the resident prepared batch (0: none, or already accumulated). */
+int32_t jx_engine_batch_id(const jx_engine* e, uint64_t* batch_id);
 
 /* ---- Leader role: the leader side of the same ping-pong exchange.
  * jx_leader_prep_init_batch replaces the per-report vdaf.leader_initialized(verify_key, agg_param,
@@ -115,18 +129,39 @@ int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, co
  * jx_leader_prep_finish_batch replaces leader_continued on the helper's Finish{prep_msg}
  * (aggregation_job_driver.rs:588-602): prepare_next fails (JX_PREPARE_NEXT_FAILURE) unless prep_msg
  * equals the corrected seed. prep_msgs: n x PM (PM = 0: nullable). out_output_shares nullable.
+ * *out_batch_id names the leader batch; finish and accumulate must pass it back (JX_E_STATE when
+ * another prepare call has replaced the batch in between, e.g. two interleaved aggregation jobs).
  * After finish, jx_accumulate aggregates the leader's finished output shares. */
 int32_t jx_engine_leader_sizes(const jx_engine* e, uint32_t* leader_input_share);
 int32_t jx_leader_prep_init_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
-                                  const uint8_t* leader_input_shares, uint8_t* out_prep_shares, uint8_t* out_verdicts);
-int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t n, const uint8_t* prep_msgs, uint8_t* out_verdicts,
-                                    uint8_t* out_output_shares);
+                                  const uint8_t* leader_input_shares, uint8_t* out_prep_shares, uint8_t* out_verdicts,
+                                  uint64_t* out_batch_id);
+int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t* prep_msgs,
+                                    uint8_t* out_verdicts, uint8_t* out_output_shares);
+/* Device-pointer leader role (inputs resident in HBM; asynchronous on the engine stream, n <= the
+ * engine capacity, grown on demand; the nonces must stay valid until the batch is accumulated).
+ * d_out_verdicts nullable. Finish: d_peer_verdicts (nullable) are the helper's verdicts; a report
+ * the helper rejected gets JX_HELPER_STEP_FAILURE. */
+int32_t jx_leader_prep_init_device(jx_engine* e, uint64_t n, const void* d_nonces, const void* d_public_shares,
+                                   const void* d_leader_input_shares, void* d_out_prep_shares, void* d_out_verdicts,
+                                   uint64_t* out_batch_id);
+int32_t jx_leader_prep_finish_device(jx_engine* e, uint64_t batch_id, uint64_t n, const void* d_prep_msgs,
+                                     const void* d_peer_verdicts, void* d_out_verdicts);
 
-/* Accumulate the output shares of the last prepared batch (helper, or leader after finish) into batch aggregations:
- * report i is added iff verdict == FINISHED and accept_mask[i] != 0 (accept_mask nullable = all),
- * into aggregation `segment[i]` (segment nullable = 0). Adds to the aggregate share, the
- * report count and the ReportIdChecksum (XOR of SHA-256(report id)). */
-int32_t jx_accumulate(jx_engine* e, uint64_t n, const uint8_t* accept_mask, const uint32_t* segment);
+/* Accumulate the output shares of the resident batch `batch_id` (helper, or leader after finish) into
+ * batch aggregations (BatchAggregation::merged_with, aggregation_job_writer.rs:608-708): report i is
+ * added iff verdict == FINISHED and accept_mask[i] != 0 (accept_mask nullable = all), into
+ * aggregation `segment[i]` (any u32 batch-aggregation id; segment nullable = 0). Adds to the
+ * aggregate share, the report count and the ReportIdChecksum (XOR of SHA-256(report id)). Any
+ * number of segments is handled in one pass over the batch (device counting sort by segment). A
+ * batch is accumulated at most once (a second call returns JX_E_STATE). */
+int32_t jx_accumulate(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t* accept_mask,
+                      const uint32_t* segment);
+/* Same with device arrays: d_accept_mask (nullable) and d_segment (nullable = all reports into
+ * segment_ids[0]) holding, per report, an index into the host array segment_ids[nsegments]; reports
+ * whose index is >= nsegments are skipped. Asynchronous on the engine stream. */
+int32_t jx_accumulate_device(jx_engine* e, uint64_t batch_id, uint64_t n, const void* d_accept_mask,
+                             const void* d_segment, const uint32_t* segment_ids, uint32_t nsegments);
 
 /* Fused prep + accumulate (the metric's unit of work): prepare n reports and add every
  * finished one into aggregation `segment`. Host buffers; processed in capacity-sized chunks.
@@ -136,11 +171,14 @@ int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces
                                  uint32_t segment, uint8_t* out_prep_msgs, uint8_t* out_verdicts);
 
 /* Same with DEVICE pointers (inputs already resident in HBM, e.g. from a torch tensor).
- * d_out_prep_msgs / d_out_verdicts are device pointers (nullable). Asynchronous on the
- * engine stream; call jx_engine_sync before reading results. */
+ * Report i goes to aggregation segment_ids[d_segment[i]] (d_segment nullable: all into
+ * segment_ids[0]; indices >= nsegments are skipped); every finished report is added.
+ * d_out_prep_msgs / d_out_verdicts are device pointers (nullable). Asynchronous on the engine
+ * stream; call jx_engine_sync before reading results. */
 int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_nonces, const void* d_public_shares,
                                         const void* d_helper_input_shares, const void* d_leader_prep_shares,
-                                        uint32_t segment, void* d_out_prep_msgs, void* d_out_verdicts);
+                                        const void* d_segment, const uint32_t* segment_ids, uint32_t nsegments,
+                                        void* d_out_prep_msgs, void* d_out_verdicts);
 
 /* Read aggregation `segment`: encoded aggregate share (OUT x FB, LE), report count, checksum. */
 int32_t jx_aggregate_read(jx_engine* e, uint32_t segment, uint8_t* out_agg, uint64_t* count);

@@ -95,7 +95,7 @@ def handle_aggregate_init(engine: HelperEngine, prepare_inits: list[PrepareInit]
             accept[j] = 1
             seg[j] = segments[i] if segments else 0
             finished[i] = True
-        engine.accumulate(m, accept, seg)
+        engine.accumulate(m, accept, seg, batch_id=res.batch_id)
     responses = [PrepareResp(ids[i], results[i]) for i in range(n)]
     return AggregateInitOutcome(responses, finished, failures)
 
@@ -122,6 +122,7 @@ class LeaderStep:
     failed: dict[int, PrepareError]            # reports that failed before the helper
     n: int                                     # reports in the engine's leader batch
     step_failures: Counter = field(default_factory=Counter)
+    init: object = None                        # the engine's LeaderInit (its batch id) when n > 0
 
 
 def leader_aggregate_init(engine: HelperEngine, reports: list[LeaderReport]) -> LeaderStep:
@@ -152,7 +153,7 @@ def leader_aggregate_init(engine: HelperEngine, reports: list[LeaderReport]) -> 
             inits.append(PrepareInit(ReportShare(r.metadata, r.public_share, r.helper_encrypted_input_share),
                                      PingPongMessage.initialize(res.prep_shares[j].tobytes())))
             stepped.append(i)
-    step = LeaderStep(inits, stepped, failed, len(ok), failures)
+    step = LeaderStep(inits, stepped, failed, len(ok), failures, res if ok else None)
     step._batch_index = {i: j for j, i in enumerate(ok)}  # report index -> engine batch row
     return step
 
@@ -189,7 +190,11 @@ def leader_process_helper_response(engine: HelperEngine, step: LeaderStep, prepa
             if pm:
                 msgs[row, :pm] = np.frombuffer(res.message.prep_msg, np.uint8)
             continued[row] = True
-    fin = engine.leader_continued_batch(msgs[:, :pm] if pm else None)
+    if step.n == 0:  # no report reached the engine: nothing to continue or accumulate
+        responses = [PrepareResp(step.prepare_inits[k].report_share.metadata.report_id,
+                                 PrepareStepResult(2, error=results[i])) for k, i in enumerate(step.stepped)]
+        return AggregateInitOutcome(responses, finished, failures)
+    fin = engine.leader_continued_batch(msgs[:, :pm] if pm else None, init=step.init)
     accept = np.zeros(step.n, np.uint8)
     seg = np.zeros(step.n, np.uint32)
     for i, row in step._batch_index.items():
@@ -203,7 +208,7 @@ def leader_process_helper_response(engine: HelperEngine, step: LeaderStep, prepa
         accept[row] = 1
         seg[row] = segments[i] if segments else 0
         finished[i] = True
-    engine.accumulate(step.n, accept, seg)
+    engine.accumulate(step.n, accept, seg, batch_id=step.init.batch_id)
     responses = [PrepareResp(step.prepare_inits[k].report_share.metadata.report_id,
                              PrepareStepResult(1) if results[i] is None else
                              PrepareStepResult(2, error=results[i]))

@@ -13,6 +13,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/jx_prio3.h"
@@ -63,6 +64,19 @@ struct jx_engine {
   std::map<uint32_t, Segment> segs;
   uint64_t last_n = 0;
   bool have_batch = false;
+  // every prepared batch gets a generation id; finish / accumulate name the batch they mean
+  uint64_t batch_gen = 0, batch_id = 0;
+  // segmented accumulation scratch (allocated on first use)
+  uint32_t* d_segx = nullptr;  // cnt, off, cursor [SEG_MAX each], ioff [SEG_MAX + 1], nitems [2]
+  uint32_t* d_perm = nullptr;
+  uint64_t perm_cap = 0;
+  uint4* d_items = nullptr;
+  uint64_t* d_spart = nullptr;
+  uint64_t spart_wmax = 0;
+  void** d_ptrs = nullptr;  // [3][nptrs]: aggs, counts, checksums of the call's segments
+  uint64_t ptrs_cap = 0;
+  std::vector<void*> h_ptrs;
+  std::vector<uint32_t> h_dense;
   // the nonces of the resident batch (device pointer; engine copy or caller's)
   const uint8_t* batch_nonces = nullptr;
   // timing
@@ -595,8 +609,10 @@ static int32_t ensure_leader_capacity(jx_engine* e, uint64_t n) {
   return JX_OK;
 }
 
+// Single-segment accumulate into aggregation seg_id. With d_seg (dense indices), only reports whose
+// index is 0 are taken.
 static int32_t accumulate_core(jx_engine* e, uint64_t n, const uint8_t* verdicts, const uint8_t* d_mask,
-                               const uint32_t* d_seg, uint32_t seg_id) {
+                               const uint32_t* d_seg, uint32_t seg_id, bool dense = false) {
   const Cfg& c = e->cfg;
   Segment* s = nullptr;
   int32_t rc = get_segment(e, seg_id, &s);
@@ -608,7 +624,7 @@ static int32_t accumulate_core(jx_engine* e, uint64_t n, const uint8_t* verdicts
   a.verdicts = verdicts;
   a.mask = d_mask;
   a.seg = d_seg;
-  a.seg_id = seg_id;
+  a.seg_id = dense ? 0u : seg_id;
   a.partials = e->d_partials;
   a.nchunks = acc_nchunks(e);
   uint64_t nblk = (n + 63) / 64;
@@ -621,6 +637,129 @@ static int32_t accumulate_core(jx_engine* e, uint64_t n, const uint8_t* verdicts
   HIPCHK(e, stage_begin(e, &ev));
   HIPCHK(e, launch_accumulate(c, a, s->agg, e->stream));
   HIPCHK(e, stage_end(e, ST_ACC, ev));
+  return JX_OK;
+}
+
+// Reports per segmented-accumulate work item: enough items that out_len x items >= 16384 waves.
+static uint32_t seg_items_len(const jx_engine* e, uint64_t n) {
+  const uint64_t nch = acc_nchunks(e);
+  uint64_t L = (n + nch - 1) / nch;
+  L = (L + 63) / 64 * 64;
+  return (uint32_t)(L < 64 ? 64 : L);
+}
+
+// Accumulate the finished, accepted reports of a prepared batch into the aggregations named by a
+// dense per-report segment index d_dense[r] in [0, ids.size()) (segment ids[d]); one pass per
+// SEG_MAX segments. The device pointer table is uploaded once per call.
+static int32_t accumulate_segmented(jx_engine* e, uint64_t n, const uint8_t* verdicts, const uint8_t* d_mask,
+                                    const uint32_t* d_dense, const std::vector<uint32_t>& ids) {
+  const Cfg& c = e->cfg;
+  const uint64_t S = ids.size();
+  if (S == 0 || n == 0) return JX_OK;
+  HIPCHK(e, hipStreamSynchronize(e->stream));  // h_ptrs may still feed an earlier async upload
+  // per-pass segments: SEG_MAX, or fewer when the per-item partials would exceed ~512 MiB
+  const uint32_t L = seg_items_len(e, n);
+  const uint64_t items_n = (n + L - 1) / L;
+  const uint64_t per_item = (uint64_t)c.out_len * 24;
+  uint64_t ns_max = (512ull << 20) / per_item;
+  ns_max = ns_max > items_n + 64 ? ns_max - items_n : 64;
+  if (ns_max > SEG_MAX) ns_max = SEG_MAX;
+  const uint64_t wmax = items_n + (S < ns_max ? S : ns_max);
+  if (!e->d_segx) HIPCHK(e, hipMalloc((void**)&e->d_segx, (4 * SEG_MAX + 3) * sizeof(uint32_t)));
+  if (e->perm_cap < n) {
+    if (e->d_perm) (void)hipFree(e->d_perm);
+    e->d_perm = nullptr;
+    HIPCHK(e, hipMalloc((void**)&e->d_perm, n * sizeof(uint32_t)));
+    e->perm_cap = n;
+  }
+  if (e->spart_wmax < wmax) {
+    if (e->d_items) (void)hipFree(e->d_items);
+    if (e->d_spart) (void)hipFree(e->d_spart);
+    e->d_items = nullptr;
+    e->d_spart = nullptr;
+    HIPCHK(e, hipMalloc((void**)&e->d_items, wmax * sizeof(uint4)));
+    HIPCHK(e, hipMalloc((void**)&e->d_spart, wmax * per_item));
+    e->spart_wmax = wmax;
+  }
+  if (e->ptrs_cap < S) {
+    if (e->d_ptrs) (void)hipFree(e->d_ptrs);
+    e->d_ptrs = nullptr;
+    HIPCHK(e, hipMalloc((void**)&e->d_ptrs, 3 * S * sizeof(void*)));
+    e->ptrs_cap = S;
+  }
+  e->h_ptrs.assign(3 * S, nullptr);
+  for (uint64_t t = 0; t < S; t++) {
+    Segment* sg = nullptr;
+    int32_t rc = get_segment(e, ids[t], &sg);
+    if (rc) return rc;
+    e->h_ptrs[t] = sg->agg;
+    e->h_ptrs[S + t] = sg->count;
+    e->h_ptrs[2 * S + t] = sg->checksum;
+  }
+  HIPCHK(e, hipMemcpyAsync(e->d_ptrs, e->h_ptrs.data(), 3 * S * sizeof(void*), hipMemcpyHostToDevice, e->stream));
+  uint64_t grid = (n + 255) / 256;
+  if (grid > SELECT_WGS) grid = SELECT_WGS;
+  for (uint64_t s0 = 0; s0 < S; s0 += ns_max) {
+    const uint32_t ns = (uint32_t)(S - s0 < ns_max ? S - s0 : ns_max);
+    SegArgs a{};
+    a.n = n;
+    a.outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? e->d_meas : e->d_outs;
+    a.out_len = c.out_len;
+    a.fb = c.fb;
+    a.verdicts = verdicts;
+    a.mask = d_mask;
+    a.seg = d_dense;
+    a.s0 = (uint32_t)s0;
+    a.ns = ns;
+    a.nonces = e->batch_nonces;
+    a.cnt = e->d_segx;
+    a.off = e->d_segx + SEG_MAX;
+    a.cursor = e->d_segx + 2 * SEG_MAX;
+    a.ioff = e->d_segx + 3 * SEG_MAX;
+    a.nitems = e->d_segx + 4 * SEG_MAX + 1;
+    a.perm = e->d_perm;
+    a.L = L;
+    a.items = e->d_items;
+    a.wmax = (uint32_t)(items_n + ns);
+    a.partials = e->d_spart;
+    a.aggs = reinterpret_cast<uint4* const*>(e->d_ptrs + s0);
+    a.counts = reinterpret_cast<unsigned long long* const*>(e->d_ptrs + S + s0);
+    a.checksums = reinterpret_cast<uint32_t* const*>(e->d_ptrs + 2 * S + s0);
+    HIPCHK(e, hipMemsetAsync(a.cnt, 0, ns * sizeof(uint32_t), e->stream));
+    hipEvent_t ev = nullptr;
+    HIPCHK(e, stage_begin(e, &ev));
+    HIPCHK(e, launch_accumulate_segmented(c, a, (uint32_t)grid, e->stream));
+    HIPCHK(e, stage_end(e, ST_ACC, ev));
+  }
+  return JX_OK;
+}
+
+// Densify host segment ids: ids in first-seen order, dense index per report.
+static void densify(const uint32_t* seg, uint64_t n, std::vector<uint32_t>& dense, std::vector<uint32_t>& ids) {
+  std::unordered_map<uint32_t, uint32_t> m;
+  dense.resize(n);
+  ids.clear();
+  for (uint64_t i = 0; i < n; i++) {
+    auto it = m.find(seg[i]);
+    if (it == m.end()) {
+      it = m.emplace(seg[i], (uint32_t)ids.size()).first;
+      ids.push_back(seg[i]);
+    }
+    dense[i] = it->second;
+  }
+}
+
+// Accumulate the resident batch into segment_ids[d_dense[r]] (d_dense nullable: all into
+// segment_ids[0]). One segment takes the coalesced select/accumulate path.
+static int32_t accumulate_any(jx_engine* e, uint64_t n, const uint8_t* verdicts, const uint8_t* d_mask,
+                              const uint32_t* d_dense, const std::vector<uint32_t>& ids) {
+  if (ids.size() == 1 || !d_dense) return accumulate_core(e, n, verdicts, d_mask, d_dense, ids[0], d_dense != nullptr);
+  return accumulate_segmented(e, n, verdicts, d_mask, d_dense, ids);
+}
+
+static int32_t check_batch(jx_engine* e, uint64_t batch_id, uint64_t n, const char* what) {
+  if (batch_id == 0 || batch_id != e->batch_id || !e->have_batch || n != e->last_n)
+    return fail(e, JX_E_STATE, std::string(what) + ": batch id / size does not name the resident prepared batch");
   return JX_OK;
 }
 
@@ -691,6 +830,8 @@ void jx_engine_destroy(jx_engine* e) {
   }
   if (e->d_consts) (void)hipFree(e->d_consts);
   if (e->d_tmp) (void)hipFree(e->d_tmp);
+  for (void* q : {(void*)e->d_segx, (void*)e->d_perm, (void*)e->d_items, (void*)e->d_spart, (void*)e->d_ptrs})
+    if (q) (void)hipFree(q);
   if (e->d_lis) (void)hipFree(e->d_lis);
   if (e->d_lps_out) (void)hipFree(e->d_lps_out);
   if (e->d_in_msgs) (void)hipFree(e->d_in_msgs);
@@ -723,9 +864,13 @@ int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, co
   if (!e || !nonces || !helper_input_shares || !leader_prep_shares || !out_verdicts) return JX_E_INVALID;
   const Cfg& c = e->cfg;
   if (c.ps_bytes && !public_shares) return JX_E_INVALID;
+  e->have_batch = false;
+  e->batch_id = 0;
   if (n == 0) {
     e->have_batch = true;
+    e->leader_batch = false;
     e->last_n = 0;
+    e->batch_id = ++e->batch_gen;
     return JX_OK;
   }
   HIPCHK(e, hipSetDevice(e->device));
@@ -751,7 +896,14 @@ int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, co
   HIPCHK(e, hipStreamSynchronize(e->stream));
   e->last_n = n;
   e->have_batch = true;
+  e->batch_id = ++e->batch_gen;
   return drain_timing(e);
+}
+
+int32_t jx_engine_batch_id(const jx_engine* e, uint64_t* batch_id) {
+  if (!e || !batch_id) return JX_E_INVALID;
+  *batch_id = e->have_batch ? e->batch_id : 0;
+  return JX_OK;
 }
 
 int32_t jx_engine_leader_sizes(const jx_engine* e, uint32_t* leader_input_share) {
@@ -762,14 +914,19 @@ int32_t jx_engine_leader_sizes(const jx_engine* e, uint32_t* leader_input_share)
 
 int32_t jx_leader_prep_init_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
                                   const uint8_t* leader_input_shares, uint8_t* out_prep_shares,
-                                  uint8_t* out_verdicts) {
+                                  uint8_t* out_verdicts, uint64_t* out_batch_id) {
   if (!e || !nonces || !leader_input_shares || !out_prep_shares || !out_verdicts) return JX_E_INVALID;
   const Cfg& c = e->cfg;
   if (c.ps_bytes && !public_shares) return JX_E_INVALID;
+  e->have_batch = false;
+  e->batch_id = 0;
+  if (out_batch_id) *out_batch_id = 0;
   if (n == 0) {
     e->have_batch = true;
     e->leader_batch = true;
     e->last_n = 0;
+    e->batch_id = ++e->batch_gen;
+    if (out_batch_id) *out_batch_id = e->batch_id;
     return JX_OK;
   }
   HIPCHK(e, hipSetDevice(e->device));
@@ -785,15 +942,44 @@ int32_t jx_leader_prep_init_batch(jx_engine* e, uint64_t n, const uint8_t* nonce
   HIPCHK(e, hipStreamSynchronize(e->stream));
   e->last_n = n;
   e->have_batch = true;
+  e->batch_id = ++e->batch_gen;
+  if (out_batch_id) *out_batch_id = e->batch_id;
   return drain_timing(e);
 }
 
-int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t n, const uint8_t* prep_msgs, uint8_t* out_verdicts,
-                                    uint8_t* out_output_shares) {
+int32_t jx_leader_prep_init_device(jx_engine* e, uint64_t n, const void* d_nonces, const void* d_public_shares,
+                                   const void* d_leader_input_shares, void* d_out_prep_shares, void* d_out_verdicts,
+                                   uint64_t* out_batch_id) {
+  if (!e || !d_nonces || !d_leader_input_shares || !d_out_prep_shares || !out_batch_id) return JX_E_INVALID;
+  const Cfg& c = e->cfg;
+  if (c.ps_bytes && !d_public_shares) return JX_E_INVALID;
+  e->have_batch = false;
+  e->batch_id = 0;
+  *out_batch_id = 0;
+  HIPCHK(e, hipSetDevice(e->device));
+  if (n) {
+    int32_t rc = ensure_capacity(e, n);
+    if (rc) return rc;
+    rc = prep_core(e, n, (const uint8_t*)d_nonces, (const uint8_t*)d_public_shares, nullptr, nullptr, e->d_verdicts,
+                   e->d_msgs, (const uint8_t*)d_leader_input_shares, (uint8_t*)d_out_prep_shares);
+    if (rc) return rc;
+    if (d_out_verdicts) HIPCHK(e, hipMemcpyAsync(d_out_verdicts, e->d_verdicts, n, hipMemcpyDeviceToDevice, e->stream));
+  }
+  e->leader_batch = true;
+  e->last_n = n;
+  e->have_batch = true;
+  e->batch_id = ++e->batch_gen;
+  *out_batch_id = e->batch_id;
+  return JX_OK;
+}
+
+int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t* prep_msgs,
+                                    uint8_t* out_verdicts, uint8_t* out_output_shares) {
   if (!e || !out_verdicts) return JX_E_INVALID;
   const Cfg& c = e->cfg;
-  if (!e->have_batch || !e->leader_batch || n != e->last_n)
-    return fail(e, JX_E_STATE, "leader finish: no leader batch of this size was initialized");
+  int32_t rc0 = check_batch(e, batch_id, n, "leader finish");
+  if (rc0) return rc0;
+  if (!e->leader_batch) return fail(e, JX_E_STATE, "leader finish: the resident batch is a helper batch");
   if (c.jr_len && !prep_msgs) return JX_E_INVALID;
   if (n == 0) return JX_OK;
   HIPCHK(e, hipSetDevice(e->device));
@@ -803,7 +989,7 @@ int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t n, const uint8_t* pre
     b.n = n;
     b.verdicts = e->d_verdicts;
     b.msgs = e->d_msgs;
-    HIPCHK(e, launch_leader_finish(c, b, e->d_in_msgs, e->stream));
+    HIPCHK(e, launch_leader_finish(c, b, e->d_in_msgs, nullptr, e->stream));
   }
   HIPCHK(e, hipMemcpyAsync(out_verdicts, e->d_verdicts, n, hipMemcpyDeviceToHost, e->stream));
   if (out_output_shares) {
@@ -818,31 +1004,65 @@ int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t n, const uint8_t* pre
   return JX_OK;
 }
 
-int32_t jx_accumulate(jx_engine* e, uint64_t n, const uint8_t* accept_mask, const uint32_t* segment) {
+int32_t jx_leader_prep_finish_device(jx_engine* e, uint64_t batch_id, uint64_t n, const void* d_prep_msgs,
+                                     const void* d_peer_verdicts, void* d_out_verdicts) {
   if (!e) return JX_E_INVALID;
-  if (!e->have_batch || n != e->last_n) return fail(e, JX_E_STATE, "accumulate: no prepared batch of this size");
+  const Cfg& c = e->cfg;
+  int32_t rc = check_batch(e, batch_id, n, "leader finish");
+  if (rc) return rc;
+  if (!e->leader_batch) return fail(e, JX_E_STATE, "leader finish: the resident batch is a helper batch");
+  if (c.jr_len && !d_prep_msgs) return JX_E_INVALID;
+  if (n == 0) return JX_OK;
+  HIPCHK(e, hipSetDevice(e->device));
+  Bufs b{};
+  b.n = n;
+  b.verdicts = e->d_verdicts;
+  b.msgs = e->d_msgs;
+  HIPCHK(e, launch_leader_finish(c, b, (const uint8_t*)d_prep_msgs, (const uint8_t*)d_peer_verdicts, e->stream));
+  if (d_out_verdicts) HIPCHK(e, hipMemcpyAsync(d_out_verdicts, e->d_verdicts, n, hipMemcpyDeviceToDevice, e->stream));
+  return JX_OK;
+}
+
+int32_t jx_accumulate(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t* accept_mask,
+                      const uint32_t* segment) {
+  if (!e) return JX_E_INVALID;
+  int32_t rc = check_batch(e, batch_id, n, "accumulate");
+  if (rc) return rc;
+  e->have_batch = false;  // a batch is accumulated at most once
+  e->batch_id = 0;
   if (n == 0) return JX_OK;
   HIPCHK(e, hipSetDevice(e->device));
   const uint8_t* dm = nullptr;
-  const uint32_t* ds = nullptr;
   if (accept_mask) {
     HIPCHK(e, hipMemcpyAsync(e->d_mask, accept_mask, n, hipMemcpyHostToDevice, e->stream));
     dm = e->d_mask;
   }
-  std::set<uint32_t> ids;
+  std::vector<uint32_t> ids{0};
+  const uint32_t* ds = nullptr;
   if (segment) {
-    HIPCHK(e, hipMemcpyAsync(e->d_seg, segment, n * 4, hipMemcpyHostToDevice, e->stream));
-    ds = e->d_seg;
-    for (uint64_t i = 0; i < n; i++) ids.insert(segment[i]);
-  } else {
-    ids.insert(0);
+    densify(segment, n, e->h_dense, ids);
+    if (ids.size() > 1) {
+      HIPCHK(e, hipMemcpyAsync(e->d_seg, e->h_dense.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+      ds = e->d_seg;
+    }
   }
-  for (uint32_t id : ids) {
-    int32_t rc = accumulate_core(e, n, e->d_verdicts, dm, ds, id);
-    if (rc) return rc;
-  }
+  rc = accumulate_any(e, n, e->d_verdicts, dm, ds, ids);
+  if (rc) return rc;
   HIPCHK(e, hipStreamSynchronize(e->stream));
   return drain_timing(e);
+}
+
+int32_t jx_accumulate_device(jx_engine* e, uint64_t batch_id, uint64_t n, const void* d_accept_mask,
+                             const void* d_segment, const uint32_t* segment_ids, uint32_t nsegments) {
+  if (!e || !segment_ids || nsegments == 0) return JX_E_INVALID;
+  int32_t rc = check_batch(e, batch_id, n, "accumulate");
+  if (rc) return rc;
+  e->have_batch = false;
+  e->batch_id = 0;
+  if (n == 0) return JX_OK;
+  HIPCHK(e, hipSetDevice(e->device));
+  std::vector<uint32_t> ids(segment_ids, segment_ids + nsegments);
+  return accumulate_any(e, n, e->d_verdicts, (const uint8_t*)d_accept_mask, (const uint32_t*)d_segment, ids);
 }
 
 int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
@@ -876,21 +1096,27 @@ int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces
     HIPCHK(e, hipStreamSynchronize(e->stream));
   }
   e->have_batch = false;  // staging no longer holds one whole batch
+  e->batch_id = 0;
   return drain_timing(e);
 }
 
 int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_nonces, const void* d_ps,
-                                        const void* d_his, const void* d_lps, uint32_t segment,
-                                        void* d_out_prep_msgs, void* d_out_verdicts) {
-  if (!e || !d_nonces || !d_his || !d_lps) return JX_E_INVALID;
+                                        const void* d_his, const void* d_lps, const void* d_segment,
+                                        const uint32_t* segment_ids, uint32_t nsegments, void* d_out_prep_msgs,
+                                        void* d_out_verdicts) {
+  if (!e || !d_nonces || !d_his || !d_lps || !segment_ids || nsegments == 0) return JX_E_INVALID;
   const Cfg& c = e->cfg;
   if (c.ps_bytes && !d_ps) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
   const uint64_t chunk = launch_chunk(e, n);
   int32_t rc = ensure_capacity(e, chunk);
   if (rc) return rc;
+  e->have_batch = false;
+  e->batch_id = 0;
+  const std::vector<uint32_t> ids(segment_ids, segment_ids + nsegments);
   const uint8_t *N = (const uint8_t*)d_nonces, *PS = (const uint8_t*)d_ps, *H = (const uint8_t*)d_his,
                 *L = (const uint8_t*)d_lps;
+  const uint32_t* SG = (const uint32_t*)d_segment;
   for (uint64_t off = 0; off < n; off += chunk) {
     const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
     uint8_t* vout = d_out_verdicts ? (uint8_t*)d_out_verdicts + off : e->d_verdicts;
@@ -898,10 +1124,9 @@ int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_
     rc = prep_core(e, m, N + off * 16, PS ? PS + off * c.ps_bytes : nullptr, H + off * c.his_bytes,
                    L + off * c.lps_bytes, vout, mout);
     if (rc) return rc;
-    rc = accumulate_core(e, m, vout, nullptr, nullptr, segment);
+    rc = accumulate_any(e, m, vout, nullptr, SG ? SG + off : nullptr, ids);
     if (rc) return rc;
   }
-  e->have_batch = false;
   return JX_OK;
 }
 

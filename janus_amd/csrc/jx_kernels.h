@@ -122,6 +122,37 @@ struct AccArgs {
   unsigned long long* count;
 };
 
+// Segmented accumulation (batch aggregations of several batch identifiers in one pass,
+// aggregation_job_writer.rs:608-708): reports are counting-sorted by dense segment index on the
+// device, then summed per (segment, run of <= L sorted positions) work item, then per segment.
+constexpr uint32_t SEG_MAX = 4096;
+constexpr uint32_t SELECT_WGS = 1024;  // grid-stride workgroups of the select / segment-count kernels  // dense segment indices handled per pass (LDS histogram size)
+struct SegArgs {
+  uint64_t n;
+  const uint4* outs;
+  uint32_t out_len;
+  uint32_t fb;
+  const uint8_t* verdicts;
+  const uint8_t* mask;     // nullable
+  const uint32_t* seg;     // dense segment index per report
+  uint32_t s0, ns;         // this pass: dense indices [s0, s0 + ns)
+  const uint8_t* nonces;
+  uint32_t* cnt;           // [ns] selected reports per segment (zeroed by the host)
+  uint32_t* off;           // [ns] first sorted position of each segment
+  uint32_t* cursor;        // [ns] scatter cursors
+  uint32_t* ioff;          // [ns + 1] first work item of each segment
+  uint32_t* perm;          // [n] selected report indices grouped by segment
+  uint32_t L;              // sorted positions per work item
+  uint4* items;            // [wmax] (segment, p0, p1, 0)
+  uint32_t* nitems;        // [2]: work items, selected reports
+  uint32_t wmax;
+  uint64_t* partials;      // [wmax][out_len][3]
+  uint4* const* aggs;                  // [ns] the segments' aggregate shares
+  unsigned long long* const* counts;   // [ns]
+  uint32_t* const* checksums;          // [ns] [8]
+};
+hipError_t launch_accumulate_segmented(const Cfg& c, const SegArgs& a, uint32_t grid, hipStream_t s);
+
 // multiproof coefficient slots (canonical Field64), per proof
 enum : uint32_t { MCOEF_L = 0, MCOEF_C0 = 1, MCOEF_HALFSUM = 2, MCOEF_T = 3, MCOEF_R = 4, MCOEF_K = 5 };
 
@@ -129,7 +160,8 @@ enum : uint32_t { MCOEF_L = 0, MCOEF_C0 = 1, MCOEF_HALFSUM = 2, MCOEF_T = 3, MCO
 hipError_t launch_count(const Cfg& c, const Bufs& b, hipStream_t s);
 hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s);
 hipError_t launch_xof_slow(const Cfg& c, const Bufs& b, hipStream_t s);
-hipError_t launch_leader_finish(const Cfg& c, const Bufs& b, const uint8_t* prep_msgs, hipStream_t s);
+hipError_t launch_leader_finish(const Cfg& c, const Bufs& b, const uint8_t* prep_msgs, const uint8_t* peer,
+                                hipStream_t s);
 hipError_t launch_flp(const Cfg& c, const Bufs& b, hipStream_t s);
 hipError_t launch_accumulate(const Cfg& c, const AccArgs& a, uint4* agg, hipStream_t s);
 hipError_t launch_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, hipStream_t s);

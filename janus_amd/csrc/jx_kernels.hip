@@ -1305,10 +1305,18 @@ __global__ __launch_bounds__(256) void flp_fp_final_kernel(Cfg c, Bufs b) {
 // ---------------------------------------------------------------------------- leader prepare_next
 // leader_continued on PingPongMessage::Finish{prep_msg} (aggregation_job_driver.rs:588-602):
 // prio prepare_next fails unless prep_msg equals the corrected joint-rand seed of the state.
-__global__ __launch_bounds__(256) void leader_finish_kernel(Cfg c, Bufs b, const uint8_t* prep_msgs) {
+// peer (nullable): the helper's verdicts; a report the helper rejected (PrepareStepResult::Reject)
+// fails on the leader too (helper_step_failure, aggregation_job_driver.rs:646-660).
+__global__ __launch_bounds__(256) void leader_finish_kernel(Cfg c, Bufs b, const uint8_t* prep_msgs,
+                                                            const uint8_t* peer) {
   const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= b.n) return;
-  if (b.verdicts[r] != 0 || c.jr_len == 0) return;
+  if (b.verdicts[r] != 0) return;
+  if (peer && peer[r] != 0) {
+    b.verdicts[r] = 5;  // JX_HELPER_STEP_FAILURE
+    return;
+  }
+  if (c.jr_len == 0) return;
   for (uint32_t o = 0; o < c.seed; o += 16) {
     const uint4 m = *reinterpret_cast<const uint4*>(prep_msgs + c.seed * r + o);
     const uint4 k = *reinterpret_cast<const uint4*>(b.msgs + c.seed * r + o);
@@ -1322,7 +1330,6 @@ __global__ __launch_bounds__(256) void leader_finish_kernel(Cfg c, Bufs b, const
 // workgroups): each thread folds its reports' SHA-256(id) and selections in registers, the
 // workgroup reduces through LDS, and only one set of atomics per workgroup reaches L2 (one
 // set per wave serialised ~15k atomics on the same 40 bytes for 1M Count reports).
-constexpr uint32_t SELECT_WGS = 1024;
 __global__ __launch_bounds__(256) void select_kernel(AccArgs a, uint8_t* sel) {
   const uint64_t padded = ((a.n + 63) / 64) * 64;
   uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1447,6 +1454,183 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(Cfg c, const uint6
   } else {
     agg[i] = f_to_u4(acc_reduce(acc));
   }
+}
+
+// ---------------------------------------------------------------------------- K4 segmented
+// One pass for any number of batch aggregations: a device counting sort of the selected reports by
+// segment (LDS histograms, one global atomic per (workgroup, segment)), work items of <= L sorted
+// positions that never straddle a segment, per-item 192-bit partial sums, then one reduction per
+// (segment, element). The gathered loads are coalesced whenever a segment's reports are contiguous
+// (the usual case: Janus jobs group reports by batch), and cost 64-byte sectors per lane otherwise.
+__device__ __forceinline__ bool seg_sel(const SegArgs& a, uint64_t r, uint32_t& d) {
+  if (r >= a.n || a.verdicts[r] != 0 || (a.mask && !a.mask[r])) return false;
+  d = a.seg[r] - a.s0;
+  return d < a.ns;
+}
+
+__global__ __launch_bounds__(256) void seg_count_kernel(SegArgs a) {
+  __shared__ uint32_t h[SEG_MAX];
+  for (uint32_t t = threadIdx.x; t < a.ns; t += blockDim.x) h[t] = 0;
+  __syncthreads();
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t d;
+    if (seg_sel(a, r, d)) atomicAdd(&h[d], 1u);
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < a.ns; t += blockDim.x)
+    if (h[t]) atomicAdd(&a.cnt[t], h[t]);
+}
+
+// one workgroup: segment offsets, scatter cursors and the work-item table
+__global__ __launch_bounds__(1024) void seg_plan_kernel(SegArgs a) {
+  __shared__ uint32_t items_base;
+  if (threadIdx.x == 0) {
+    uint32_t pos = 0, w = 0;
+    for (uint32_t s = 0; s < a.ns; s++) {
+      const uint32_t c = a.cnt[s];
+      a.off[s] = pos;
+      a.cursor[s] = pos;
+      a.ioff[s] = w;
+      pos += c;
+      w += (c + a.L - 1) / a.L;
+    }
+    a.ioff[a.ns] = w;
+    a.nitems[0] = w;
+    a.nitems[1] = pos;  // selected reports = sorted positions in use
+    items_base = w;
+  }
+  __syncthreads();
+  for (uint32_t s = threadIdx.x; s < a.ns; s += blockDim.x) {
+    const uint32_t c = a.cnt[s], p0 = a.off[s];
+    uint32_t w = a.ioff[s];
+    for (uint32_t q = 0; q < c; q += a.L, w++) a.items[w] = make_uint4(s, p0 + q, p0 + min(c, q + a.L), 0);
+  }
+}
+
+__global__ __launch_bounds__(256) void seg_scatter_kernel(SegArgs a) {
+  __shared__ uint32_t h[SEG_MAX];
+  for (uint32_t t = threadIdx.x; t < a.ns; t += blockDim.x) h[t] = 0;
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t r_first = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t r = r_first; r < a.n; r += stride) {
+    uint32_t d;
+    if (seg_sel(a, r, d)) atomicAdd(&h[d], 1u);
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < a.ns; t += blockDim.x)
+    if (h[t]) h[t] = atomicAdd(&a.cursor[t], h[t]);  // this workgroup's range of segment t
+  __syncthreads();
+  for (uint64_t r = r_first; r < a.n; r += stride) {
+    uint32_t d;
+    if (seg_sel(a, r, d)) a.perm[atomicAdd(&h[d], 1u)] = (uint32_t)r;
+  }
+}
+
+__device__ __forceinline__ void acc192_wave_reduce(acc192& acc) {
+  for (int off = 32; off > 0; off >>= 1) {
+    uint64_t o0 = ((uint64_t)__shfl_xor((uint32_t)(acc.w0 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w0, off);
+    uint64_t o1 = ((uint64_t)__shfl_xor((uint32_t)(acc.w1 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w1, off);
+    uint64_t o2 = ((uint64_t)__shfl_xor((uint32_t)(acc.w2 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w2, off);
+    uint32_t cc = 0;
+    acc.w0 = addc64(acc.w0, o0, cc);
+    acc.w1 = addc64(acc.w1, o1, cc);
+    acc.w2 = acc.w2 + o2 + cc;
+  }
+}
+
+// wave per (output element, work item): lanes walk the item's sorted positions
+__global__ __launch_bounds__(256) void seg_accumulate_kernel(SegArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t w = blockIdx.y;
+  if (i >= a.out_len || w >= *a.nitems) return;
+  const uint4 it = a.items[w];
+  acc192 acc;
+  acc_zero(acc);
+  uint32_t p = it.y + lane;
+  for (; p + 192 < it.z; p += 256) {  // four gathers in flight
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t r = a.perm[p + 64 * u];
+      v[u] = a.outs[il_idx(r >> 6, a.out_len, i, r & 63)];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) acc_add128(acc, u4_to_f(v[u]));
+  }
+  for (; p < it.z; p += 64) {
+    const uint32_t r = a.perm[p];
+    acc_add128(acc, u4_to_f(a.outs[il_idx(r >> 6, a.out_len, i, r & 63)]));
+  }
+  acc192_wave_reduce(acc);
+  if (lane == 0) {
+    uint64_t* q = a.partials + ((uint64_t)w * a.out_len + i) * 3;
+    q[0] = acc.w0;
+    q[1] = acc.w1;
+    q[2] = acc.w2;
+  }
+}
+
+// ReportIdChecksum per segment: thread per sorted position; a wave whose 64 positions share a
+// segment (all but the boundary waves) folds them and issues one set of atomics
+__global__ __launch_bounds__(256) void seg_checksum_kernel(SegArgs a) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t total = a.nitems[1];
+  uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t d = 0xFFFFFFFFu;
+  if (p < total) {
+    const uint32_t r = a.perm[p];
+    uint32_t id[4];
+    load16(a.nonces + 16ull * r, id);
+    sha256_16(id, h);
+    d = a.seg[r] - a.s0;
+  }
+  const uint32_t d0 = __shfl(d, 0);
+  const bool uniform = __all(d == d0);
+  if (uniform) {
+    if (d0 == 0xFFFFFFFFu) return;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      uint32_t v = h[k];
+      for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off);
+      h[k] = v;
+    }
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+      for (int k = 0; k < 8; k++) atomicXor(&a.checksums[d0][k], h[k]);
+  } else if (d != 0xFFFFFFFFu) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) atomicXor(&a.checksums[d][k], h[k]);
+  }
+}
+
+// wave per (output element, segment): sum the segment's work-item partials into its aggregate
+__global__ __launch_bounds__(256) void seg_reduce_kernel(SegArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t s = blockIdx.y;
+  if (i >= a.out_len || s >= a.ns) return;
+  acc192 acc;
+  acc_zero(acc);
+  for (uint32_t w = a.ioff[s] + lane; w < a.ioff[s + 1]; w += 64) {
+    const uint64_t* q = a.partials + ((uint64_t)w * a.out_len + i) * 3;
+    uint32_t cc = 0;
+    acc.w0 = addc64(acc.w0, q[0], cc);
+    acc.w1 = addc64(acc.w1, q[1], cc);
+    acc.w2 = acc.w2 + q[2] + cc;
+  }
+  acc192_wave_reduce(acc);
+  if (lane != 0) return;
+  uint4* agg = a.aggs[s];
+  acc_add128(acc, u4_to_f(agg[i]));
+  if (a.fb == 8) {
+    const uint64_t v = reduce192_p64(acc.w0, acc.w1, acc.w2);
+    agg[i] = make_uint4(lo32(v), hi32(v), 0, 0);
+  } else {
+    agg[i] = f_to_u4(acc_reduce(acc));
+  }
+  if (i == 0) *a.counts[s] += a.cnt[s];
 }
 
 // multi-GPU combine: sum nparts encoded aggregate shares (LE bytes) mod p
@@ -1604,8 +1788,10 @@ uint64_t k1_round_reports(const Cfg& c, int device) {
   if (st != hipSuccess || wgs <= 0) return 0;
   return (uint64_t)cus * (uint64_t)wgs * threads;
 }
-hipError_t launch_leader_finish(const Cfg& c, const Bufs& b, const uint8_t* prep_msgs, hipStream_t s) {
-  hipLaunchKernelGGL(leader_finish_kernel, dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, c, b, prep_msgs);
+hipError_t launch_leader_finish(const Cfg& c, const Bufs& b, const uint8_t* prep_msgs, const uint8_t* peer,
+                                hipStream_t s) {
+  hipLaunchKernelGGL(leader_finish_kernel, dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, c, b, prep_msgs,
+                     peer);
   return hipGetLastError();
 }
 hipError_t launch_xof_slow(const Cfg& c, const Bufs& b, hipStream_t s) {
@@ -1717,6 +1903,19 @@ hipError_t launch_accumulate(const Cfg& c, const AccArgs& a, uint4* agg, hipStre
                      (const uint8_t*)sel);
   hipLaunchKernelGGL(reduce_partials_kernel, dim3((c.out_len + 3) / 4), dim3(256), 0, s, c,
                      (const uint64_t*)a.partials, a.nchunks, agg);
+  return hipGetLastError();
+}
+
+// grid: workgroups of the count/scatter passes (the same for both: each workgroup re-walks its reports)
+hipError_t launch_accumulate_segmented(const Cfg& c, const SegArgs& a, uint32_t grid, hipStream_t s) {
+  (void)c;
+  hipLaunchKernelGGL(seg_count_kernel, dim3(grid), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(seg_plan_kernel, dim3(1), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(seg_scatter_kernel, dim3(grid), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(seg_accumulate_kernel, dim3((a.out_len + 3) / 4, a.wmax), dim3(256), 0, s, a);
+  // one thread per possible sorted position (n bounds the selected count); the rest return at once
+  hipLaunchKernelGGL(seg_checksum_kernel, dim3((uint32_t)((a.n + 255) / 256)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(seg_reduce_kernel, dim3((a.out_len + 3) / 4, a.ns), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

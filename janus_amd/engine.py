@@ -31,12 +31,14 @@ PREPARE_INIT_FAILURE = 1
 PREP_SHARE_DECODE_FAILURE = 2
 PREPARE_MESSAGE_FAILURE = 3
 PREPARE_NEXT_FAILURE = 4
+HELPER_STEP_FAILURE = 5  # leader only: the helper rejected the report
 VERDICT_LABELS = {
     FINISHED: "finished",
     PREPARE_INIT_FAILURE: "prepare_init_failure",
     PREP_SHARE_DECODE_FAILURE: "leader_prep_share_decode_failure",
     PREPARE_MESSAGE_FAILURE: "prepare_message_failure",
     PREPARE_NEXT_FAILURE: "prepare_next_failure",
+    HELPER_STEP_FAILURE: "helper_step_failure",
 }
 
 
@@ -59,10 +61,18 @@ def _u8(a, n: int, width: int, what: str) -> np.ndarray:
     return arr
 
 
+def _seg_table(segment_ids):
+    ids = np.ascontiguousarray(np.asarray(segment_ids, dtype=np.uint32).reshape(-1))
+    if ids.size == 0:
+        raise ValueError("at least one segment id")
+    return ids, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+
+
 @dataclass
 class LeaderInit:
     verdicts: np.ndarray       # uint8[n]: 0 initialized, 1 prepare_init_failure
     prep_shares: np.ndarray    # uint8[n, LPS]: payloads of PingPongMessage::Initialize
+    batch_id: int = 0          # names the engine's resident leader batch (finish / accumulate)
 
 
 @dataclass
@@ -70,6 +80,7 @@ class BatchResult:
     verdicts: np.ndarray       # uint8[n]
     prep_msgs: np.ndarray      # uint8[n, PM]
     out_shares: np.ndarray | None  # uint8[n, OUT*FB]
+    batch_id: int = 0          # the resident batch these results belong to (for accumulate)
 
     def finished(self) -> np.ndarray:
         return self.verdicts == FINISHED
@@ -80,6 +91,7 @@ class HelperEngine:
     path) and the leader role of the same ping-pong exchange."""
 
     _leader_n = 0
+    _leader_id = 0
 
     def __init__(self, vdaf: Prio3, verify_key: bytes, device: int = 0):
         if len(verify_key) != vdaf.verify_key_len:
@@ -146,7 +158,14 @@ class HelperEngine:
                                           _ptr(his), _ptr(lps), _ptr(msgs) if self.prep_msg_len else None,
                                           _ptr(verdicts), _ptr(outs))
         check(st, self._h, "jx_helper_prep_batch")
-        return BatchResult(verdicts[:n], msgs[:n, : self.prep_msg_len], outs[:n] if outs is not None else None)
+        return BatchResult(verdicts[:n], msgs[:n, : self.prep_msg_len], outs[:n] if outs is not None else None,
+                           self.batch_id())
+
+    def batch_id(self) -> int:
+        """Id of the resident prepared batch (0: none / already accumulated)."""
+        b = ctypes.c_uint64()
+        check(self._L.jx_engine_batch_id(self._h, ctypes.byref(b)), self._h, "jx_engine_batch_id")
+        return b.value
 
     # ------------------------------------------------------------------ leader role
     def leader_initialized_batch(self, nonces, public_shares, leader_input_shares) -> "LeaderInit":
@@ -161,31 +180,63 @@ class HelperEngine:
         lis = _u8(leader_input_shares, n, self.leader_input_share_len, "leader_input_shares")
         verdicts = np.zeros(max(n, 1), np.uint8)
         shares = np.zeros((max(n, 1), self.prep_share_len), np.uint8)
+        bid = ctypes.c_uint64()
         st = self._L.jx_leader_prep_init_batch(self._h, n, _ptr(nn), _ptr(ps) if self.public_share_len else None,
-                                               _ptr(lis), _ptr(shares), _ptr(verdicts))
+                                               _ptr(lis), _ptr(shares), _ptr(verdicts), ctypes.byref(bid))
         check(st, self._h, "jx_leader_prep_init_batch")
-        self._leader_n = n
-        return LeaderInit(verdicts[:n], shares[:n])
+        self._leader_n, self._leader_id = n, bid.value
+        return LeaderInit(verdicts[:n], shares[:n], bid.value)
 
-    def leader_continued_batch(self, prep_msgs, want_out_shares: bool = False) -> BatchResult:
-        """prio ping-pong leader_continued on the helper's Finish{prep_msg} for the batch of the
-        last leader_initialized_batch (aggregation_job_driver.rs:588-602): prepare_next."""
-        n = self._leader_n
+    def leader_continued_batch(self, prep_msgs, want_out_shares: bool = False,
+                               init: "LeaderInit | None" = None) -> BatchResult:
+        """prio ping-pong leader_continued on the helper's Finish{prep_msg} (aggregation_job_driver.rs:
+        588-602): prepare_next for the batch of `init` (default: the last leader_initialized_batch).
+        Raises EngineError (JX_E_STATE) if another prepare call has replaced that batch."""
+        n = self._leader_n if init is None else len(init.verdicts)
+        bid = self._leader_id if init is None else init.batch_id
         msgs = None
         if self.prep_msg_len:
-            msgs = _u8(prep_msgs, n, self.prep_msg_len, "prep_msgs")
+            msgs = _u8(prep_msgs, n, self.prep_msg_len, "prep_msgs") if n else np.zeros((1, self.prep_msg_len), np.uint8)
         verdicts = np.zeros(max(n, 1), np.uint8)
         outs = np.zeros((max(n, 1), self.output_len * self.field_bytes), np.uint8) if want_out_shares else None
-        st = self._L.jx_leader_prep_finish_batch(self._h, n, _ptr(msgs), _ptr(verdicts), _ptr(outs))
+        st = self._L.jx_leader_prep_finish_batch(self._h, bid, n, _ptr(msgs), _ptr(verdicts), _ptr(outs))
         check(st, self._h, "jx_leader_prep_finish_batch")
         return BatchResult(verdicts[:n], msgs[:n] if msgs is not None else np.zeros((n, 0), np.uint8),
-                           outs[:n] if outs is not None else None)
+                           outs[:n] if outs is not None else None, bid)
 
-    def accumulate(self, n: int, accept_mask: np.ndarray | None = None, segments: np.ndarray | None = None):
-        """Merge the finished output shares of the last batch into batch aggregations."""
+    def accumulate(self, n: int, accept_mask: np.ndarray | None = None, segments: np.ndarray | None = None,
+                   batch_id: int | None = None):
+        """Merge the finished output shares of a prepared batch into batch aggregations (at most once
+        per batch). segments[i]: the batch-aggregation id (any u32) of report i. batch_id defaults to
+        the resident batch."""
         m = None if accept_mask is None else np.ascontiguousarray(accept_mask, dtype=np.uint8)
         s = None if segments is None else np.ascontiguousarray(segments, dtype=np.uint32)
-        check(self._L.jx_accumulate(self._h, n, _ptr(m), _ptr(s)), self._h, "jx_accumulate")
+        bid = self.batch_id() if batch_id is None else batch_id
+        check(self._L.jx_accumulate(self._h, bid, n, _ptr(m), _ptr(s)), self._h, "jx_accumulate")
+
+    # ------------------------------------------------------------------ device-pointer paths (inputs in HBM)
+    def leader_init_device(self, n: int, d_nonces: int, d_public_shares: int | None, d_leader_input_shares: int,
+                           d_out_prep_shares: int, d_out_verdicts: int | None = None) -> int:
+        """leader_initialized for n reports resident in HBM; returns the batch id. Asynchronous."""
+        bid = ctypes.c_uint64()
+        st = self._L.jx_leader_prep_init_device(self._h, n, d_nonces, d_public_shares, d_leader_input_shares,
+                                                d_out_prep_shares, d_out_verdicts, ctypes.byref(bid))
+        check(st, self._h, "jx_leader_prep_init_device")
+        return bid.value
+
+    def leader_finish_device(self, batch_id: int, n: int, d_prep_msgs: int | None, d_peer_verdicts: int | None = None,
+                             d_out_verdicts: int | None = None):
+        """leader_continued on the helper's prep messages in HBM; reports the helper rejected
+        (d_peer_verdicts != 0) fail with helper_step_failure. Asynchronous."""
+        check(self._L.jx_leader_prep_finish_device(self._h, batch_id, n, d_prep_msgs, d_peer_verdicts, d_out_verdicts),
+              self._h, "jx_leader_prep_finish_device")
+
+    def accumulate_device(self, batch_id: int, n: int, d_accept_mask: int | None = None, d_segments: int | None = None,
+                          segment_ids=(0,)):
+        """accumulate with device arrays: d_segments[i] indexes segment_ids. Asynchronous."""
+        ids, ptr = _seg_table(segment_ids)
+        check(self._L.jx_accumulate_device(self._h, batch_id, n, d_accept_mask, d_segments, ptr, ids.size), self._h,
+              "jx_accumulate_device")
 
     def prep_and_aggregate(self, nonces, public_shares, helper_input_shares, leader_prep_shares,
                            segment: int = 0, want_results: bool = True):
@@ -206,11 +257,16 @@ class HelperEngine:
 
     def prep_and_aggregate_device(self, d_nonces: int, d_public_shares: int | None, d_helper_input_shares: int,
                                   d_leader_prep_shares: int, n: int, segment: int = 0,
-                                  d_out_prep_msgs: int | None = None, d_out_verdicts: int | None = None):
+                                  d_out_prep_msgs: int | None = None, d_out_verdicts: int | None = None,
+                                  d_segments: int | None = None, segment_ids=None):
         """Same, with inputs already resident in HBM (device pointers, e.g. tensor.data_ptr()).
+        Every report goes to `segment`, or, with d_segments, report i to segment_ids[d_segments[i]].
         Asynchronous: call sync() before reading outputs."""
+        ids, ptr = _seg_table([segment] if segment_ids is None else segment_ids)
+        self._seg_keep = ids  # the table is read during the call only; keep it alive anyway
         st = self._L.jx_helper_prep_aggregate_device(self._h, n, d_nonces, d_public_shares, d_helper_input_shares,
-                                                     d_leader_prep_shares, segment, d_out_prep_msgs, d_out_verdicts)
+                                                     d_leader_prep_shares, d_segments, ptr, ids.size,
+                                                     d_out_prep_msgs, d_out_verdicts)
         check(st, self._h, "jx_helper_prep_aggregate_device")
 
     # ------------------------------------------------------------------ aggregation state

@@ -100,10 +100,9 @@ class HpkeOpener:
             raise ValueError("one enc, ciphertext and aad per report")
         if n == 0:
             return []
-        if any(len(e) != 32 for e in encs):
-            raise ValueError("encapsulated keys are 32 bytes")
-        short = [i for i, c in enumerate(ciphertexts) if len(c) < 16]
-        idx = [i for i in range(n) if i not in set(short)]
+        # a malformed share fails alone (HpkeDecryptError for that report, aggregator.rs:1772-1831):
+        # a wrong-length encapsulated key or a ciphertext shorter than the GCM tag never reaches the GPU
+        idx = [i for i in range(n) if len(encs[i]) == 32 and len(ciphertexts[i]) >= 16]
         out: list[bytes | None] = [None] * n
         if not idx:
             return out

@@ -1,0 +1,228 @@
+"""GPU: batch accumulation into many batch aggregations, batch ids, device-pointer leader role.
+
+Accumulation mirrors AggregationJobWriter::update_batch_aggregations_from_report_aggregations
+(aggregator/src/aggregator/aggregation_job_writer.rs:608-708) -> BatchAggregation::merged_with
+(aggregator_core/src/datastore/models.rs:1275-1330): per batch identifier, aggregate share +=
+output share, count += 1, checksum ^= SHA-256(report id). Every expectation comes from the C oracle.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import pytest
+
+from janus_amd._lib import EngineError
+from janus_amd.engine import HELPER_STEP_FAILURE, HelperEngine
+from janus_amd.vdaf import Prio3
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(vdaf, vk, n, seed, tamper_every=9):
+    orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
+    rng = np.random.default_rng(seed)
+    if vdaf.algo_id == O.HISTOGRAM:
+        meas = rng.integers(0, vdaf.length, size=(n, 1), dtype=np.uint64)
+    elif vdaf.algo_id == O.COUNT:
+        meas = rng.integers(0, 2, size=(n, 1), dtype=np.uint64)
+    else:
+        meas = rng.integers(0, 1 << vdaf.bits, size=(n, vdaf.length), dtype=np.uint64)
+    nonces = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+    rands = rng.integers(0, 256, size=(n, orc.sizes.client_rand), dtype=np.uint8)
+    ps, his, lps, _ = orc.client_leader_batch(vk, meas, nonces, rands, nthreads=16)
+    for i in range(0, n, tamper_every):
+        lps[i, int(rng.integers(0, lps.shape[1]))] ^= 1 << int(rng.integers(0, 8))
+    return orc, nonces, ps, his, lps
+
+
+def _expected(orc, want, nonces, sel):
+    idx = np.nonzero(sel)[0]
+    agg = orc.aggregate([want["out_shares"][i].tobytes() for i in idx]) if len(idx) else \
+        bytes(orc.sizes.output_len * orc.sizes.field_bytes)
+    cs = bytes(32)
+    for i in idx:
+        cs = bytes(a ^ b for a, b in zip(cs, O.sha256(nonces[i].tobytes())))
+    return agg, int(len(idx)), cs
+
+
+@pytest.mark.parametrize("nseg", [2, 64, 700])
+def test_many_segments_one_pass(nseg):
+    """Reports of one batch spread over nseg batch aggregations (arbitrary u32 ids, random order,
+    accept mask), merged in one pass: every segment equals the oracle's merge of its reports."""
+    vdaf = Prio3.histogram(32, 4)
+    vk = bytes(range(16))
+    n = 3000
+    orc, nonces, ps, his, lps = _batch(vdaf, vk, n, seed=nseg)
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
+    rng = np.random.default_rng(99)
+    ids = rng.choice(np.arange(1, 1 << 31, dtype=np.uint64), size=nseg, replace=False).astype(np.uint32)
+    seg = ids[rng.integers(0, nseg, size=n)]
+    mask = (rng.random(n) < 0.9).astype(np.uint8)
+    with HelperEngine(vdaf, vk) as eng:
+        res = eng.helper_initialized_batch(nonces, ps, his, lps)
+        np.testing.assert_array_equal(res.verdicts, want["verdicts"])
+        eng.accumulate(n, mask, seg, batch_id=res.batch_id)
+        for s in ids[: min(nseg, 40)]:
+            sel = (want["verdicts"] == 0) & (mask == 1) & (seg == s)
+            assert eng.aggregate_share(int(s)) == _expected(orc, want, nonces, sel), int(s)
+        # the sum over all segments is the batch total
+        total = [0] * vdaf.length
+        cnt = 0
+        for s in ids:
+            agg, c, _ = eng.aggregate_share(int(s))
+            cnt += c
+            for j in range(vdaf.length):
+                total[j] += int.from_bytes(agg[16 * j:16 * j + 16], "little")
+        sel = (want["verdicts"] == 0) & (mask == 1)
+        agg_all, cnt_all, _ = _expected(orc, want, nonces, sel)
+        assert cnt == cnt_all
+        p = 2**128 - 28 * 2**64 + 1
+        assert [x % p for x in total] == [int.from_bytes(agg_all[16 * j:16 * j + 16], "little") for j in range(vdaf.length)]
+
+
+def test_segments_cost_is_not_linear():
+    """One pass regardless of the number of segments: 1024 segments cost well under 1024x one."""
+    import torch
+
+    vdaf = Prio3.sum_vec(8, 1000, 88)
+    vk = bytes(range(16))
+    K, R = 64, 65536
+    orc, nonces, ps, his, lps = _batch(vdaf, vk, K, seed=7)
+    dev = torch.device("cuda", 0)
+    tile = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev).repeat(R // K, 1).contiguous()  # noqa: E731
+    d_n, d_ps, d_his, d_lps = tile(nonces), tile(ps), tile(his), tile(lps)
+    times = {}
+    with HelperEngine(vdaf, vk) as eng:
+        for nseg in (1, 64, 1024):
+            segs = torch.from_numpy(np.random.default_rng(nseg).integers(0, nseg, size=R).astype(np.int32)).to(dev)
+            ids = list(range(10_000, 10_000 + nseg))
+            for rep in range(2):
+                eng.timing(True)
+                eng.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(), d_lps.data_ptr(), R,
+                                              d_segments=segs.data_ptr(), segment_ids=ids)
+                eng.sync()
+                times[nseg] = eng.timing_read()["accumulate"]["ms"]
+        eng.reset_aggregates()
+    assert times[1024] < 8 * times[1] + 2.0, times  # ms; a pass per segment would be ~1000x
+    print("accumulate ms by segments:", times)
+
+
+def test_fused_device_segments_match_oracle():
+    import torch
+
+    vdaf = Prio3.sum_vec(2, 50, 9)
+    vk = bytes(range(16))
+    n = 2000
+    orc, nonces, ps, his, lps = _batch(vdaf, vk, n, seed=3)
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
+    rng = np.random.default_rng(5)
+    dense = rng.integers(0, 6, size=n).astype(np.uint32)  # 5 = out of range: skipped
+    ids = [7, 70, 700, 7000, 70000]
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d_seg = T(dense.astype(np.int32))
+    import os
+    os.environ["JX_CHUNK_REPORTS"] = "512"  # several launches: the segment array is offset per launch
+    try:
+        eng = HelperEngine(vdaf, vk)
+    finally:
+        del os.environ["JX_CHUNK_REPORTS"]
+    with eng:
+        d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
+        keep = [T(nonces), T(ps), T(his), T(lps)]  # hold the tensors: a freed block is reused at once
+        eng.prep_and_aggregate_device(*[t.data_ptr() for t in keep], n, d_out_verdicts=d_v.data_ptr(),
+                                      d_segments=d_seg.data_ptr(), segment_ids=ids)
+        eng.sync()
+        np.testing.assert_array_equal(d_v.cpu().numpy(), want["verdicts"])
+        for k, s in enumerate(ids):
+            sel = (want["verdicts"] == 0) & (dense == k)
+            assert eng.aggregate_share(s) == _expected(orc, want, nonces, sel)
+
+
+def test_batch_ids_refuse_interleaved_and_double_accumulate():
+    """two interleaved leader jobs of the same size (init A, init B, finish A) must not
+    finish A against B's device state; a batch accumulates at most once."""
+    vdaf = Prio3.count()
+    vk = bytes(range(16))
+    orc = O.Prio3Oracle(vdaf.algo_id)
+    rng = np.random.default_rng(1)
+    n = 40
+    meas = rng.integers(0, 2, size=(2 * n, 1), dtype=np.uint64)
+    nonces = rng.integers(0, 256, size=(2 * n, 16), dtype=np.uint8)
+    rands = rng.integers(0, 256, size=(2 * n, orc.sizes.client_rand), dtype=np.uint8)
+    sh = [orc.shard(meas[i], nonces[i].tobytes(), rands[i].tobytes()) for i in range(2 * n)]
+    lis = np.frombuffer(b"".join(s[1] for s in sh), np.uint8).reshape(2 * n, -1)
+    his = np.frombuffer(b"".join(s[2] for s in sh), np.uint8).reshape(2 * n, -1)
+    empty = np.zeros((n, 0), np.uint8)
+    with HelperEngine(vdaf, vk) as leader, HelperEngine(vdaf, vk) as helper:
+        a = leader.leader_initialized_batch(nonces[:n], empty, lis[:n])
+        b = leader.leader_initialized_batch(nonces[n:], empty, lis[n:])
+        assert a.batch_id != b.batch_id
+        with pytest.raises(EngineError, match="call out of order"):
+            leader.leader_continued_batch(None, init=a)
+        with pytest.raises(EngineError, match="call out of order"):
+            leader.accumulate(n, batch_id=a.batch_id)
+        hres = helper.helper_initialized_batch(nonces[n:], empty, his[n:], b.prep_shares)
+        fin = leader.leader_continued_batch(None, init=b)
+        assert not fin.verdicts.any() and not hres.verdicts.any()
+        leader.accumulate(n, batch_id=b.batch_id)
+        with pytest.raises(EngineError, match="call out of order"):
+            leader.accumulate(n, batch_id=b.batch_id)  # no double count
+        helper.accumulate(n)
+        (agg_l, c_l, _), (agg_h, c_h, _) = leader.aggregate_share(0), helper.aggregate_share(0)
+    assert c_l == c_h == n
+    p = 2**64 - 2**32 + 1
+    assert (int.from_bytes(agg_l, "little") + int.from_bytes(agg_h, "little")) % p == int(meas[n:].sum())
+
+
+def test_device_leader_ping_pong_with_peer_verdicts():
+    """Both roles with inputs resident in HBM: leader init (device) -> helper prep (device, fused) ->
+    leader finish with the helper's verdicts -> leader accumulate (device, two segments)."""
+    import torch
+
+    vdaf = Prio3.sum_vec(4, 30, 7)
+    vk = bytes(range(3, 19))
+    orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
+    n = 300
+    rng = np.random.default_rng(8)
+    meas = rng.integers(0, 16, size=(n, vdaf.length), dtype=np.uint64)
+    nonces = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+    rands = rng.integers(0, 256, size=(n, orc.sizes.client_rand), dtype=np.uint8)
+    sh = [orc.shard(meas[i], nonces[i].tobytes(), rands[i].tobytes()) for i in range(n)]
+    ps, lis, his = (np.frombuffer(b"".join(s[k] for s in sh), np.uint8).reshape(n, -1) for k in range(3))
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d_n, d_ps, d_lis, d_his = T(nonces), T(ps), T(lis), T(his)
+    d_lps = torch.zeros((n, vdaf.prep_share_len), dtype=torch.uint8, device=dev)
+    d_hv = torch.zeros(n, dtype=torch.uint8, device=dev)
+    d_msgs = torch.zeros((n, 16), dtype=torch.uint8, device=dev)
+    d_lv = torch.zeros(n, dtype=torch.uint8, device=dev)
+    seg = (np.arange(n) % 2).astype(np.int32)
+    with HelperEngine(vdaf, vk) as leader, HelperEngine(vdaf, vk) as helper:
+        bid = leader.leader_init_device(n, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(), d_lps.data_ptr())
+        leader.sync()
+        d_lps[5, 3] ^= 1  # helper rejects report 5
+        torch.cuda.synchronize()
+        helper.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(), d_lps.data_ptr(), n,
+                                         0, d_msgs.data_ptr(), d_hv.data_ptr())
+        helper.sync()
+        d_msgs[9, 0] ^= 1  # leader prepare_next fails on report 9
+        torch.cuda.synchronize()
+        leader.leader_finish_device(bid, n, d_msgs.data_ptr(), d_hv.data_ptr(), d_lv.data_ptr())
+        d_seg = T(seg)
+        leader.accumulate_device(bid, n, None, d_seg.data_ptr(), (11, 12))
+        leader.sync()
+        lv = d_lv.cpu().numpy()
+        assert lv[5] == HELPER_STEP_FAILURE and lv[9] == 4 and (lv != 0).sum() == 2
+        assert d_hv.cpu().numpy()[5] != 0
+        ok = lv == 0
+        for k, s in enumerate((11, 12)):
+            agg, cnt, _ = leader.aggregate_share(s)
+            sel = ok & (seg == k)
+            assert cnt == int(sel.sum())
+            # leader output shares == the oracle's leader prep_init output shares
+            outs = [orc.prep_init(vk, 0, nonces[i].tobytes(), ps[i].tobytes(), lis[i].tobytes())[2]
+                    for i in np.nonzero(sel)[0]]
+            assert agg == orc.aggregate(outs)
