@@ -124,6 +124,38 @@ def cpu_baseline(orc, vk, nonces, ps, his, lps, seconds, threads):
                       f"({K} distinct x {reps}), C oracle oracle/prio3_oracle.c, {threads} threads, {dt:.1f} s"}
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def ensure_world(gpus: int) -> None:
+    """`--gpus N` means N ranks, one per GPU. Without a torch.distributed launcher in the
+    environment, start one (torch.distributed.run as a child process, before this process touches
+    the GPU) and exit with its status; refuse N beyond the visible GPUs or a launcher world of
+    another size, instead of silently measuring one GPU."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != gpus:
+            sys.exit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}")
+        return
+    if gpus == 1:
+        return
+    import subprocess
+
+    import torch  # device_count() does not initialise the HIP runtime on this image
+
+    have = torch.cuda.device_count()
+    if gpus > have:
+        sys.exit(f"bench.py: --gpus {gpus} but only {have} GPU(s) visible")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *sys.argv[1:]]
+    sys.exit(subprocess.run(cmd).returncode)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -137,6 +169,7 @@ def main():
     ap.add_argument("--length", type=int, default=1000)
     ap.add_argument("--chunk", type=int, default=88)
     args = ap.parse_args()
+    ensure_world(args.gpus)
 
     import torch
     import torch.distributed as dist
@@ -148,8 +181,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    assert world == args.gpus  # ensure_world
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:

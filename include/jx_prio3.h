@@ -204,7 +204,8 @@ int32_t jx_shard_record_bytes(const jx_engine* e, uint32_t* bytes);
 int32_t jx_shard_record_export_device(jx_engine* e, uint32_t segment, void* d_dst);
 int32_t jx_shard_record_combine_device(jx_engine* e, const void* d_records, uint32_t nrecords, void* d_out);
 
-/* Wait for all work on the engine stream. */
+/* Wait for all work on the engine stream. Returns JX_E_INVALID if a combine since the last sync
+ * met a non-canonical field element (>= p) in its inputs (the host merge rejects those too). */
 int32_t jx_engine_sync(jx_engine* e);
 /* The engine's HIP stream (hipStream_t), for callers that order their own work after it. */
 int32_t jx_engine_stream(jx_engine* e, void** stream);

@@ -77,6 +77,7 @@ struct jx_engine {
   uint64_t ptrs_cap = 0;
   std::vector<void*> h_ptrs;
   std::vector<uint32_t> h_dense;
+  uint32_t* d_err = nullptr;  // combine kernels: non-canonical input seen (reported by jx_engine_sync)
   // the nonces of the resident batch (device pointer; engine copy or caller's)
   const uint8_t* batch_nonces = nullptr;
   // timing
@@ -830,7 +831,8 @@ void jx_engine_destroy(jx_engine* e) {
   }
   if (e->d_consts) (void)hipFree(e->d_consts);
   if (e->d_tmp) (void)hipFree(e->d_tmp);
-  for (void* q : {(void*)e->d_segx, (void*)e->d_perm, (void*)e->d_items, (void*)e->d_spart, (void*)e->d_ptrs})
+  for (void* q : {(void*)e->d_segx, (void*)e->d_perm, (void*)e->d_items, (void*)e->d_spart, (void*)e->d_ptrs,
+                  (void*)e->d_err})
     if (q) (void)hipFree(q);
   if (e->d_lis) (void)hipFree(e->d_lis);
   if (e->d_lps_out) (void)hipFree(e->d_lps_out);
@@ -1182,10 +1184,20 @@ int32_t jx_aggregate_export_device(jx_engine* e, uint32_t segment, void* d_dst) 
   return JX_OK;
 }
 
+static int32_t ensure_err(jx_engine* e) {
+  if (!e->d_err) {
+    HIPCHK(e, hipMalloc((void**)&e->d_err, sizeof(uint32_t)));
+    HIPCHK(e, hipMemsetAsync(e->d_err, 0, sizeof(uint32_t), e->stream));
+  }
+  return JX_OK;
+}
+
 int32_t jx_aggregate_combine_device(jx_engine* e, const void* d_parts, uint32_t nparts, void* d_out) {
   if (!e || !d_parts || !d_out || nparts == 0) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
-  HIPCHK(e, launch_combine(e->cfg, (const uint8_t*)d_parts, nparts, (uint8_t*)d_out, e->stream));
+  int32_t rc = ensure_err(e);
+  if (rc) return rc;
+  HIPCHK(e, launch_combine(e->cfg, (const uint8_t*)d_parts, nparts, (uint8_t*)d_out, e->d_err, e->stream));
   return JX_OK;
 }
 
@@ -1202,7 +1214,9 @@ int32_t jx_shard_record_export_device(jx_engine* e, uint32_t segment, void* d_ds
 int32_t jx_shard_record_combine_device(jx_engine* e, const void* d_records, uint32_t nrecords, void* d_out) {
   if (!e || !d_records || !d_out || nrecords == 0) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
-  HIPCHK(e, launch_record_combine(e->cfg, (const uint8_t*)d_records, nrecords, (uint8_t*)d_out, e->stream));
+  int32_t rc = ensure_err(e);
+  if (rc) return rc;
+  HIPCHK(e, launch_record_combine(e->cfg, (const uint8_t*)d_records, nrecords, (uint8_t*)d_out, e->d_err, e->stream));
   return JX_OK;
 }
 
@@ -1216,6 +1230,14 @@ int32_t jx_engine_sync(jx_engine* e) {
   if (!e) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
   HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (e->d_err) {
+    uint32_t bad = 0;
+    HIPCHK(e, hipMemcpy(&bad, e->d_err, sizeof bad, hipMemcpyDeviceToHost));
+    if (bad) {
+      HIPCHK(e, hipMemset(e->d_err, 0, sizeof bad));
+      return fail(e, JX_E_INVALID, "combine: a merged share holds a non-canonical field element (>= p)");
+    }
+  }
   return JX_OK;
 }
 

@@ -164,10 +164,12 @@ hipError_t launch_leader_finish(const Cfg& c, const Bufs& b, const uint8_t* prep
                                 hipStream_t s);
 hipError_t launch_flp(const Cfg& c, const Bufs& b, hipStream_t s);
 hipError_t launch_accumulate(const Cfg& c, const AccArgs& a, uint4* agg, hipStream_t s);
-hipError_t launch_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, hipStream_t s);
+hipError_t launch_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, uint32_t* err,
+                          hipStream_t s);
 hipError_t launch_record_export(const Cfg& c, const uint4* agg, const unsigned long long* count,
                                 const uint32_t* checksum, uint8_t* dst, hipStream_t s);
-hipError_t launch_record_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, hipStream_t s);
+hipError_t launch_record_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, uint32_t* err,
+                                 hipStream_t s);
 hipError_t launch_transpose_out(const Cfg& c, const uint4* outs, uint64_t n, uint8_t* dst, hipStream_t s);
 hipError_t launch_agg_encode(const Cfg& c, const uint4* agg, uint8_t* dst, hipStream_t s);
 // multiproof Field64 SumVec (jx_mp64.hip)

@@ -1634,7 +1634,9 @@ __global__ __launch_bounds__(256) void seg_reduce_kernel(SegArgs a) {
 }
 
 // multi-GPU combine: sum nparts encoded aggregate shares (LE bytes) mod p
-__global__ void combine_kernel(Cfg c, const uint8_t* parts, uint32_t nparts, uint8_t* out) {
+// err: set to 1 if an input element is not canonical (>= p): the host merge rejects such a share
+// (Field decode, janus_amd/distributed.py merge_aggregate_shares); the engine reports it on sync.
+__global__ void combine_kernel(Cfg c, const uint8_t* parts, uint32_t nparts, uint8_t* out, uint32_t* err) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= c.out_len) return;
   const uint32_t fb = c.fb;
@@ -1645,7 +1647,11 @@ __global__ void combine_kernel(Cfg c, const uint8_t* parts, uint32_t nparts, uin
       const uint8_t* p = parts + q * stride + (uint64_t)i * 8;
       uint64_t v = 0;
       for (int k = 7; k >= 0; k--) v = (v << 8) | p[k];
-      s = add64(s, v >= P64 ? v - P64 : v);
+      if (v >= P64) {
+        atomicOr(err, 1u);
+        v -= P64;
+      }
+      s = add64(s, v);
     }
     for (int k = 0; k < 8; k++) out[(uint64_t)i * 8 + k] = (uint8_t)(s >> (8 * k));
   } else {
@@ -1655,7 +1661,12 @@ __global__ void combine_kernel(Cfg c, const uint8_t* parts, uint32_t nparts, uin
       uint64_t lo = 0, hi = 0;
       for (int k = 7; k >= 0; k--) lo = (lo << 8) | p[k];
       for (int k = 15; k >= 8; k--) hi = (hi << 8) | p[k];
-      s = add128(s, make128(lo, hi));
+      f128 v = make128(lo, hi);
+      if (ge_p128(v)) {
+        atomicOr(err, 1u);
+        v = sub128(v, make128(P128_LO, P128_HI));
+      }
+      s = add128(s, v);
     }
     for (int k = 0; k < 8; k++) out[(uint64_t)i * 16 + k] = (uint8_t)(s.lo >> (8 * k));
     for (int k = 0; k < 8; k++) out[(uint64_t)i * 16 + 8 + k] = (uint8_t)(s.hi >> (8 * k));
@@ -1684,7 +1695,7 @@ __global__ void record_export_kernel(Cfg c, const uint4* agg, const unsigned lon
 
 // merge nparts shard records (compute_aggregate_share, aggregate_share.rs:87-95):
 // mod-p sum of the aggregate shares, sum of the counts, XOR of the checksums.
-__global__ void record_combine_kernel(Cfg c, const uint8_t* parts, uint32_t nparts, uint8_t* out) {
+__global__ void record_combine_kernel(Cfg c, const uint8_t* parts, uint32_t nparts, uint8_t* out, uint32_t* err) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t fb = c.fb;
   const uint64_t stride = (uint64_t)c.out_len * fb + 40;
@@ -1695,7 +1706,11 @@ __global__ void record_combine_kernel(Cfg c, const uint8_t* parts, uint32_t npar
         const uint8_t* p = parts + q * stride + (uint64_t)i * 8;
         uint64_t v = 0;
         for (int k = 7; k >= 0; k--) v = (v << 8) | p[k];
-        s = add64(s, v >= P64 ? v - P64 : v);
+        if (v >= P64) {
+          atomicOr(err, 1u);
+          v -= P64;
+        }
+        s = add64(s, v);
       }
       for (int k = 0; k < 8; k++) out[(uint64_t)i * 8 + k] = (uint8_t)(s >> (8 * k));
     } else {
@@ -1706,7 +1721,10 @@ __global__ void record_combine_kernel(Cfg c, const uint8_t* parts, uint32_t npar
         for (int k = 7; k >= 0; k--) lo = (lo << 8) | p[k];
         for (int k = 15; k >= 8; k--) hi = (hi << 8) | p[k];
         f128 v = make128(lo, hi);
-        if (ge_p128(v)) v = sub128(v, make128(P128_LO, P128_HI));
+        if (ge_p128(v)) {
+          atomicOr(err, 1u);
+          v = sub128(v, make128(P128_LO, P128_HI));
+        }
         s = add128(s, v);
       }
       for (int k = 0; k < 8; k++) out[(uint64_t)i * 16 + k] = (uint8_t)(s.lo >> (8 * k));
@@ -1919,8 +1937,9 @@ hipError_t launch_accumulate_segmented(const Cfg& c, const SegArgs& a, uint32_t 
   return hipGetLastError();
 }
 
-hipError_t launch_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, hipStream_t s) {
-  hipLaunchKernelGGL(combine_kernel, dim3((c.out_len + 255) / 256), dim3(256), 0, s, c, parts, nparts, out);
+hipError_t launch_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, uint32_t* err,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(combine_kernel, dim3((c.out_len + 255) / 256), dim3(256), 0, s, c, parts, nparts, out, err);
   return hipGetLastError();
 }
 hipError_t launch_record_export(const Cfg& c, const uint4* agg, const unsigned long long* count,
@@ -1929,9 +1948,10 @@ hipError_t launch_record_export(const Cfg& c, const uint4* agg, const unsigned l
                      checksum, dst);
   return hipGetLastError();
 }
-hipError_t launch_record_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, hipStream_t s) {
+hipError_t launch_record_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, uint32_t* err,
+                                 hipStream_t s) {
   hipLaunchKernelGGL(record_combine_kernel, dim3((c.out_len + 1 + 255) / 256), dim3(256), 0, s, c, parts, nparts,
-                     out);
+                     out, err);
   return hipGetLastError();
 }
 hipError_t launch_transpose_out(const Cfg& c, const uint4* outs, uint64_t n, uint8_t* dst, hipStream_t s) {

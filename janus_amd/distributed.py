@@ -119,11 +119,15 @@ class ShardCombiner:
         self.merged = torch.zeros(self.nbytes, dtype=torch.uint8, device=dev)
 
     def combine(self, segment: int = 0):
+        import torch
+        import torch.distributed as dist
+
         self.engine.export_record_device(segment, self.record.data_ptr())
         self.engine.sync()  # the engine stream is not torch's stream
-        gathered = all_gather_records(self.record, self.group)
-        import torch
-
+        if dist.get_backend(self.group) == "gloo":  # gloo gathers host tensors (CPU tests, 1-GPU boxes)
+            gathered = all_gather_records(self.record.cpu(), self.group).to(self.record.device)
+        else:  # RCCL over xGMI
+            gathered = all_gather_records(self.record, self.group)
         torch.cuda.current_stream().synchronize()
         self.engine.combine_records_device(gathered.data_ptr(), gathered.shape[0], self.merged.data_ptr())
         self.engine.sync()

@@ -113,3 +113,14 @@ def test_record_roundtrip():
     rec = D.pack_record(agg, 123456789, bytes(range(100, 132)))
     assert rec.size == D.record_bytes(2, 16)
     assert D.unpack_record(rec, 16) == (agg, 123456789, bytes(range(100, 132)))
+
+
+def test_bench_refuses_world_mismatch():
+    """bench.py --gpus 2 under a launcher world of another size exits non-zero (no silent 1-GPU run)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"],
+                       env=dict(os.environ, WORLD_SIZE="3"), capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr

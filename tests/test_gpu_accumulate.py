@@ -226,3 +226,26 @@ def test_device_leader_ping_pong_with_peer_verdicts():
             outs = [orc.prep_init(vk, 0, nonces[i].tobytes(), ps[i].tobytes(), lis[i].tobytes())[2]
                     for i in np.nonzero(sel)[0]]
             assert agg == orc.aggregate(outs)
+
+
+@pytest.mark.parametrize("name", ["count", "sumvec"])
+def test_device_combine_rejects_non_canonical(name):
+    """the device merge must refuse a non-canonical element (>= p) like the host merge."""
+    import torch
+
+    from janus_amd import distributed as D
+
+    vdaf = Prio3.count() if name == "count" else Prio3.sum_vec(1, 4, 2)
+    fb = vdaf.field_bytes
+    with HelperEngine(vdaf, bytes(16)) as eng:
+        nb = eng.record_bytes()
+        recs = torch.zeros((2, nb), dtype=torch.uint8, device="cuda")
+        recs[1, :fb] = 0xFF
+        out = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        eng.combine_records_device(recs.data_ptr(), 2, out.data_ptr())
+        with pytest.raises(EngineError, match="non-canonical"):
+            eng.sync()
+        eng.sync()  # the flag is cleared once reported
+        with pytest.raises(ValueError, match="not canonical"):
+            D.merge_records(recs.cpu().numpy(), fb)
