@@ -798,13 +798,30 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
     jx_engine_destroy(e);
     return JX_E_HIP;
   }
-  // default chunk for the fused path: ~48 GiB of staging (env JX_CHUNK_REPORTS overrides)
-  uint64_t per = per_report_bytes(e->cfg);
-  uint64_t chunk = (48ull << 30) / per;
+  // Default chunk for the fused path: ~48 GiB of staging, enough for several K1 occupancy rounds of
+  // the small VDAFs. A VDAF whose reports need megabytes of staging (FixedPointBoundedL2VecSum at
+  // length 10000: 2.8 MB) would fill only a few percent of the SIMDs at 48 GiB, and K1 is bound by
+  // the per-report sponge latency (15k sequential permutations), so throughput scales with the
+  // reports in flight: grow the budget toward one full K1 round, up to 1/3 of the device memory
+  // (two engines, e.g. leader and helper, still fit on one MI355X). JX_STAGING_GB / JX_CHUNK_REPORTS override.
+  const uint64_t per = per_report_bytes(e->cfg);
+  e->round_reports = k1_round_reports(e->cfg, device);
+  uint64_t budget = 48ull << 30;
+  size_t mem_free = 0, mem_total = 0;
+  if (hipMemGetInfo(&mem_free, &mem_total) == hipSuccess && e->round_reports &&
+      e->round_reports * per > budget) {
+    const uint64_t cap = mem_total / 3;
+    budget = e->round_reports * per < cap ? e->round_reports * per : cap;
+    if (budget < (48ull << 30)) budget = 48ull << 30;
+  }
+  if (const char* env = getenv("JX_STAGING_GB")) {
+    const uint64_t gb = strtoull(env, nullptr, 10);
+    if (gb >= 1) budget = gb << 30;
+  }
+  uint64_t chunk = budget / per;
   if (chunk > (1ull << 22)) chunk = 1ull << 22;
   chunk = chunk / 256 * 256;
   if (chunk < 256) chunk = 256;
-  e->round_reports = k1_round_reports(e->cfg, device);
   if (e->round_reports && chunk >= e->round_reports) chunk = chunk / e->round_reports * e->round_reports;
   if (const char* env = getenv("JX_CHUNK_REPORTS")) {
     uint64_t v = strtoull(env, nullptr, 10);
