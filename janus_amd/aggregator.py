@@ -35,15 +35,22 @@ class AggregateInitOutcome:
 
 
 def handle_aggregate_init(engine: HelperEngine, prepare_inits: list[PrepareInit], input_shares: list[bytes],
-                          segments: list[int] | None = None, replayed: set[bytes] | None = None
-                          ) -> AggregateInitOutcome:
+                          segments: list[int] | None = None, replayed: set[bytes] | None = None,
+                          writer=None) -> AggregateInitOutcome:
     """Prepare and aggregate one AggregationJobInitializeReq worth of reports.
 
     input_shares[i] is the HPKE-decrypted PlaintextInputShare payload of report i (the
     encoded Prio3 helper input share). segments[i] names the batch aggregation the report
     belongs to (batch identifier; default 0). replayed holds report ids the datastore
-    already saw (check_other_report_aggregation_exists)."""
+    already saw (check_other_report_aggregation_exists). writer (a
+    batch_aggregation.BatchAggregationWriter) records the host-side half of each batch
+    aggregation: every report's timestamp, failed ones included, and the job counters (a
+    one-round Prio3 helper job is written already finished: neither counter moves)."""
     n = len(prepare_inits)
+    if writer is not None:
+        segs = segments if segments else [0] * n
+        writer.observe_report_aggregations(segs, [p.report_share.metadata.time for p in prepare_inits])
+        writer.observe_job(segs, initial_write=True, terminal=True)
     if len(input_shares) != n:
         raise ValueError("one input share per PrepareInit")
     ids = [p.report_share.metadata.report_id for p in prepare_inits]
@@ -125,11 +132,18 @@ class LeaderStep:
     init: object = None                        # the engine's LeaderInit (its batch id) when n > 0
 
 
-def leader_aggregate_init(engine: HelperEngine, reports: list[LeaderReport]) -> LeaderStep:
+def leader_aggregate_init(engine: HelperEngine, reports: list[LeaderReport], segments: list[int] | None = None,
+                          writer=None) -> LeaderStep:
     """Prepare every report of a new aggregation job on the leader (agg_id 0) and build the
-    PrepareInits to send to the helper (aggregation_job_driver.rs:301-386)."""
+    PrepareInits to send to the helper (aggregation_job_driver.rs:301-386). writer: the job is
+    written in progress (aggregation_jobs_created + 1 per batch identifier) with every report's
+    timestamp."""
     v = engine.vdaf
     n = len(reports)
+    if writer is not None:
+        segs = segments if segments else [0] * n
+        writer.observe_report_aggregations(segs, [r.metadata.time for r in reports])
+        writer.observe_job(segs, initial_write=True, terminal=False)
     failures: Counter = Counter()
     failed: dict[int, PrepareError] = {}
     ok = [i for i, r in enumerate(reports) if len(r.leader_input_share) == engine.leader_input_share_len
@@ -159,9 +173,13 @@ def leader_aggregate_init(engine: HelperEngine, reports: list[LeaderReport]) -> 
 
 
 def leader_process_helper_response(engine: HelperEngine, step: LeaderStep, prepare_resps: list[PrepareResp],
-                                   segments: list[int] | None = None) -> AggregateInitOutcome:
+                                   segments: list[int] | None = None, writer=None) -> AggregateInitOutcome:
     """Finish the leader's reports from the helper's AggregationJobResp and accumulate the
-    finished ones (process_response_from_helper, aggregation_job_driver.rs:540-701)."""
+    finished ones (process_response_from_helper, aggregation_job_driver.rs:540-701). writer: the
+    job is updated into a terminal state (aggregation_jobs_terminated + 1 per batch identifier)."""
+    if writer is not None:
+        nrep = max([*step.stepped, *step.failed, -1]) + 1
+        writer.observe_job(segments if segments else [0] * nrep, initial_write=False, terminal=True)
     if len(prepare_resps) != len(step.stepped) or any(
             resp.report_id != step.prepare_inits[k].report_share.metadata.report_id
             for k, resp in enumerate(prepare_resps)):
@@ -221,7 +239,7 @@ def leader_process_helper_response(engine: HelperEngine, step: LeaderStep, prepa
 
 def handle_aggregate_init_encrypted(engine: HelperEngine, opener, hpke_config_id: int, task_id: bytes,
                                     prepare_inits: list[PrepareInit], segments: list[int] | None = None,
-                                    replayed: set[bytes] | None = None) -> AggregateInitOutcome:
+                                    replayed: set[bytes] | None = None, writer=None) -> AggregateInitOutcome:
     """The helper's aggregate-init loop including the decryption of the report shares
     (aggregator.rs:1763-1893): one batched HPKE open on the GPU (janus_amd.hpke.HpkeOpener) for
     the whole request, then PlaintextInputShare decoding and extension checks on the host, then
@@ -270,6 +288,10 @@ def handle_aggregate_init_encrypted(engine: HelperEngine, opener, hpke_config_id
             continue
         payloads[i] = pis.payload
     keep = [i for i in range(n) if i in payloads]
+    if writer is not None:  # every report aggregation of the request, including the ones that failed to open
+        segs = segments if segments else [0] * n
+        writer.observe_report_aggregations(segs, [p.report_share.metadata.time for p in prepare_inits])
+        writer.observe_job(segs, initial_write=True, terminal=True)
     inner = handle_aggregate_init(engine, [prepare_inits[i] for i in keep], [payloads[i] for i in keep],
                                   [segments[i] for i in keep] if segments else None, replayed)
     failures.update(inner.step_failures)

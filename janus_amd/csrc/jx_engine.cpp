@@ -192,8 +192,8 @@ static int32_t make_cfg(const jx_prio3_params* p, const uint8_t* vk, uint32_t vk
       arity = 2;
       break;
     case ALGO_SUM:
-      if (p->bits < 1 || p->bits > 32) {
-        why = "Prio3Sum bits must be in [1, 32]";
+      if (p->bits < 1 || p->bits > 64) {
+        why = "Prio3Sum bits must be in [1, 64]";
         return JX_E_UNSUPPORTED;
       }
       c.meas_len = p->bits;
@@ -204,8 +204,9 @@ static int32_t make_cfg(const jx_prio3_params* p, const uint8_t* vk, uint32_t vk
       break;
     case ALGO_SUMVEC:
     case ALGO_SUMVEC_F64_MULTIPROOF:
-      if (p->bits < 1 || p->bits > 32 || p->length < 1 || p->chunk_length < 1) {
-        why = "Prio3SumVec needs 1 <= bits <= 32, length >= 1, chunk_length >= 1";
+      if (p->bits < 1 || p->bits > (mp ? 32u : 64u) || p->length < 1 || p->chunk_length < 1) {
+        why = mp ? "Prio3SumVecField64Multiproof needs 1 <= bits <= 32, length >= 1, chunk_length >= 1"
+                 : "Prio3SumVec needs 1 <= bits <= 64, length >= 1, chunk_length >= 1";
         return JX_E_UNSUPPORTED;
       }
       c.meas_len = p->bits * p->length;

@@ -272,20 +272,35 @@ __device__ __forceinline__ f128 truncw_value(const TruncW& t) {
 // Tracked as a running max so that one compare per block decides.
 __device__ __forceinline__ uint32_t ge_screen(uint4 v) { return v.w & (v.z | 0x1Fu); }
 
+// h * 2^32 mod p (the high half of a > 32-bit truncation)
+__device__ __forceinline__ f128 shl32_mod(f128 h) {
+  return reduce192(h.lo << 32, (h.hi << 32) | (h.lo >> 32), h.hi >> 32);
+}
+
 // one measurement element at static stream position e (fast path: no rejections)
+// WIDE (bits in (32, 64], Sum / SumVec): the word columns of bits 0..31 are folded into `lo` at
+// bit 32 and restart for the bits 32.. (weights 2^(j-32) < 2^32); out = lo + 2^32 * high.
+template <bool WIDE>
 __device__ __forceinline__ void emit_meas(const Cfg& c, uint4* mp, uint4* op, uint32_t e, uint4 v, uint32_t& gmax,
-                                          TruncW& tr) {
+                                          TruncW& tr, f128& lo) {
   if (e >= c.meas_len) return;
   gmax = max(gmax, ge_screen(v));
   mp[(uint64_t)e * IL] = v;
   if (!c.out_is_meas && e < c.trunc_len) {  // FixedPoint: the trailing norm bits are not truncated
-    const uint32_t sh = 1u << tr.j;
+    const uint32_t sh = 1u << (WIDE ? (tr.j & 31u) : tr.j);
     tr.T[0] += (uint64_t)v.x * sh;
     tr.T[1] += (uint64_t)v.y * sh;
     tr.T[2] += (uint64_t)v.z * sh;
     tr.T[3] += (uint64_t)v.w * sh;
-    if (++tr.j == c.bits) {
-      op[(uint64_t)tr.i * IL] = f_to_u4(truncw_value(tr));
+    ++tr.j;
+    if (WIDE && tr.j == 32 && c.bits > 32) {
+      lo = truncw_value(tr);
+      truncw_zero(tr);
+    }
+    if (tr.j == c.bits) {
+      f128 val = truncw_value(tr);
+      if (WIDE && c.bits > 32) val = add128(lo, shl32_mod(val));
+      op[(uint64_t)tr.i * IL] = f_to_u4(val);
       truncw_zero(tr);
       tr.j = 0;
       tr.i++;
@@ -475,7 +490,7 @@ __device__ __forceinline__ bool ge_exact(uint4 v) {
 // the leader input share (meas || proofs || k_blind, decoded here: elements >= p fail) and only the
 // joint_rand_part absorb runs through Keccak.
 constexpr uint32_t K1_WAVES = 4;  // waves (64-report blocks) per K1 workgroup
-template <bool LEADER>
+template <bool LEADER, bool WIDE = false>
 __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t blk = (uint64_t)blockIdx.x * K1_WAVES + (threadIdx.x >> 6);
@@ -546,15 +561,16 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
   truncw_zero(tr);
   tr.j = 0;
   tr.i = 0;
+  f128 trunc_lo = make128(0, 0);
   uint4* const mp = b.meas + il_idx(blk, c.meas_len, 0, lane);
   uint4* const op = b.outs + il_idx(blk, c.out_len, 0, lane);
   uint32_t unused_screen = 0;
   auto emit = [&](uint32_t e, uint4 v) {
     if (LEADER) {
       if (e < c.meas_len) bad |= ge_exact(v);
-      emit_meas(c, mp, op, e, v, unused_screen, tr);
+      emit_meas<WIDE>(c, mp, op, e, v, unused_screen, tr, trunc_lo);
     } else {
-      emit_meas(c, mp, op, e, v, gmax, tr);
+      emit_meas<WIDE>(c, mp, op, e, v, gmax, tr, trunc_lo);
     }
   };
   // emit the measurement elements of block m (10 or 11, by parity)
@@ -1785,10 +1801,16 @@ hipError_t launch_count(const Cfg& c, const Bufs& b, hipStream_t s) {
 }
 hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
   uint32_t nb = nblk_of(b.n);
-  if (b.leader)
-    hipLaunchKernelGGL(xof_kernel<true>, dim3((nb + K1_WAVES - 1) / K1_WAVES), dim3(64 * K1_WAVES), 0, s, c, b);
+  const dim3 grid((nb + K1_WAVES - 1) / K1_WAVES), block(64 * K1_WAVES);
+  const bool wide = c.bits > 32 && (c.algo == ALGO_SUM || c.algo == ALGO_SUMVEC);
+  if (b.leader && wide)
+    hipLaunchKernelGGL((xof_kernel<true, true>), grid, block, 0, s, c, b);
+  else if (b.leader)
+    hipLaunchKernelGGL((xof_kernel<true, false>), grid, block, 0, s, c, b);
+  else if (wide)
+    hipLaunchKernelGGL((xof_kernel<false, true>), grid, block, 0, s, c, b);
   else
-    hipLaunchKernelGGL(xof_kernel<false>, dim3((nb + K1_WAVES - 1) / K1_WAVES), dim3(64 * K1_WAVES), 0, s, c, b);
+    hipLaunchKernelGGL((xof_kernel<false, false>), grid, block, 0, s, c, b);
   return hipGetLastError();
 }
 // Reports that occupy every K1 wave slot of the device exactly once: CUs x resident

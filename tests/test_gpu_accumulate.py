@@ -249,3 +249,40 @@ def test_device_combine_rejects_non_canonical(name):
         eng.sync()  # the flag is cleared once reported
         with pytest.raises(ValueError, match="not canonical"):
             D.merge_records(recs.cpu().numpy(), fb)
+
+
+def test_handler_batch_aggregations_with_writer():
+    """handle_aggregate_init over several batch identifiers with a BatchAggregationWriter: the device
+    half (share, count, checksum) and the host half (client timestamp interval over every report
+    aggregation, failed ones included; None share for a batch without finished reports)."""
+    from janus_amd.aggregator import handle_aggregate_init
+    from janus_amd.batch_aggregation import BatchAggregationWriter, Interval
+    from janus_amd.messages import HpkeCiphertext, PingPongMessage, PrepareInit, ReportMetadata, ReportShare
+
+    vdaf = Prio3.sum_vec(2, 10, 4)
+    vk = bytes(range(16))
+    n = 60
+    orc, nonces, ps, his, lps = _batch(vdaf, vk, n, seed=31, tamper_every=7)
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
+    times = [1_700_000_000 + 17 * i for i in range(n)]
+    segs = [100 + (i % 3) for i in range(n)]
+    segs[0] = 999  # a batch identifier whose only report fails (tampered: index 0)
+    inits = [PrepareInit(ReportShare(ReportMetadata(nonces[i].tobytes(), times[i]), ps[i].tobytes(),
+                                     HpkeCiphertext(1, b"e", b"c")), PingPongMessage.initialize(lps[i].tobytes()))
+             for i in range(n)]
+    w = BatchAggregationWriter(field_bytes=16)
+    with HelperEngine(vdaf, vk) as eng:
+        out = handle_aggregate_init(eng, inits, [his[i].tobytes() for i in range(n)], segs, writer=w)
+        assert want["verdicts"][0] != 0 and not out.finished[0]
+        rows = {s: w.batch_aggregation(eng, s) for s in w.segments()}
+    assert rows[999].aggregate_share is None and rows[999].report_count == 0
+    assert rows[999].client_timestamp_interval == Interval.from_time(times[0])
+    for s in (100, 101, 102):
+        idx = [i for i in range(n) if segs[i] == s]
+        sel = np.zeros(n, bool)
+        sel[[i for i in idx if want["verdicts"][i] == 0]] = True
+        agg, cnt, cs = _expected(orc, want, nonces, sel)
+        r = rows[s]
+        assert (r.aggregate_share, r.report_count, r.checksum) == (agg, cnt, cs)
+        t = [times[i] for i in idx]
+        assert r.client_timestamp_interval == Interval(min(t), max(t) + 1 - min(t))

@@ -25,6 +25,8 @@ CASES = {
     "count": Prio3.count(),
     "sum8": Prio3.sum(8),
     "sum32": Prio3.sum(32),
+    "sum64": Prio3.sum(64),
+    "sumvec_48x6_5": Prio3.sum_vec(48, 6, 5),
     "sumvec_small": Prio3.sum_vec(3, 37, 5),
     "sumvec_8x1000_88": Prio3.sum_vec(8, 1000, 88),
     "histogram_16_4": Prio3.histogram(16, 4),

@@ -92,6 +92,11 @@ CASES = {
     "sum5": Prio3.sum(5),
     "sum17": Prio3.sum(17),
     "sum31": Prio3.sum(31),
+    # bits > 32 (Janus's VdafInstance::Prio3Sum{bits} has no 32-bit cap, core/src/vdaf.rs:65-108)
+    "sum33": Prio3.sum(33),
+    "sum64": Prio3.sum(64),
+    "sumvec_33x5_7": Prio3.sum_vec(33, 5, 7),
+    "sumvec_64x20_9": Prio3.sum_vec(64, 20, 9),
     "sumvec_small": Prio3.sum_vec(3, 37, 5),
     "sumvec_8x1000_88": Prio3.sum_vec(8, 1000, 88),
     "histogram_256_16": Prio3.histogram(256, 16),
