@@ -86,6 +86,7 @@ struct jx_engine {
   double ms[NST] = {0, 0, 0, 0};
   uint64_t launches[NST] = {0, 0, 0, 0};
   uint32_t force_slow = 0;
+  uint32_t k1_split = 0;  // helper K1 as squeeze-only + absorb-only launches (JX_K1_SPLIT, debug option 3)
   std::string err;
 };
 
@@ -559,6 +560,7 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
   b.msgs = msgs;
   b.consts = e->d_consts;
   b.force_slow = e->force_slow;
+  b.k1_split = e->k1_split;
   hipEvent_t ev = nullptr;
   if (c.algo == ALGO_COUNT) {
     HIPCHK(e, stage_begin(e, &ev));
@@ -829,6 +831,7 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
     if (v >= 64) chunk = v / 64 * 64;
   }
   e->default_chunk = chunk;
+  if (const char* env = getenv("JX_K1_SPLIT")) e->k1_split = (uint32_t)atoi(env) % 3;
   *out = e;
   return JX_OK;
 }
@@ -1292,6 +1295,11 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
   if (!e) return JX_E_INVALID;
   if (option == 1) {
     e->force_slow = value != 0;
+    return JX_OK;
+  }
+  if (option == 3) {  // K1 variant: 0 fused two-sponge kernel, 1 squeeze-only + absorb-only launches
+    if (value < 0 || value > 2) return JX_E_INVALID;
+    e->k1_split = (uint32_t)value;  // 2: the absorb-only launch at 2 waves/SIMD
     return JX_OK;
   }
   if (option == 2) {  // accumulate chunking (tests)

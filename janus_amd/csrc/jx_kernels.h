@@ -104,6 +104,7 @@ struct Bufs {
   uint8_t* msgs;
   const uint4* consts;
   uint32_t force_slow;  // debug: route every report through the slow XOF kernel
+  uint32_t k1_split;    // helper K1 as two launches (squeeze-only, absorb-only) instead of one
 };
 
 struct AccArgs {

@@ -489,9 +489,24 @@ __device__ __forceinline__ bool ge_exact(uint4 v) {
 // LEADER (agg_id 0, leader_initialized, aggregation_job_driver.rs:345): the shares are explicit in
 // the leader input share (meas || proofs || k_blind, decoded here: elements >= p fail) and only the
 // joint_rand_part absorb runs through Keccak.
+//
+// Split helper variant (K1_SQUEEZE then K1_ABSORB, Cfg-independent engine switch): the squeeze of
+// the measurement + proof shares (one sponge per lane, <= 128 VGPRs: 4 waves/SIMD) and the
+// joint_rand_part absorb of the staged measurement share + the XOF tail (3 waves/SIMD) run as two
+// launches instead of one 2-sponge kernel at 2 waves/SIMD; +128 KB/report of staging reads.
 constexpr uint32_t K1_WAVES = 4;  // waves (64-report blocks) per K1 workgroup
-template <bool LEADER, bool WIDE = false>
-__global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
+// K1_ABSORB2: the absorb-only launch built for 2 waves/SIMD (no spills) instead of 3
+enum : int { K1_FUSED = 0, K1_LEADER = 1, K1_SQUEEZE = 2, K1_ABSORB = 3, K1_ABSORB2 = 4 };
+template <int MODE>
+struct K1Occ {  // min waves per SIMD the register budget is built for
+  static constexpr int value = MODE == K1_SQUEEZE ? 4 : (MODE == K1_ABSORB ? 3 : (MODE == K1_ABSORB2 ? 2 : 1));
+};
+template <int MODE, bool WIDE = false>
+__global__ __launch_bounds__(64 * K1_WAVES, K1Occ<MODE>::value) void xof_kernel(Cfg c, Bufs b) {
+  constexpr bool LEADER = MODE == K1_LEADER;
+  constexpr bool SQUEEZE_ONLY = MODE == K1_SQUEEZE;
+  constexpr bool ABSORB_ONLY = MODE == K1_ABSORB || MODE == K1_ABSORB2;
+  constexpr bool LOADS = LEADER || ABSORB_ONLY;  // measurement words are loaded, not squeezed
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t blk = (uint64_t)blockIdx.x * K1_WAVES + (threadIdx.x >> 6);
   const uint64_t nblk = (b.n + 63) / 64;
@@ -500,6 +515,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
   const uint64_t r = r0 < b.n ? r0 : b.n - 1;
 
   const uint8_t* hs = LEADER ? nullptr : b.his + (uint64_t)c.his_bytes * r;
+  const uint4* const mstage = b.meas + il_idx(blk, c.meas_len, 0, lane);
   const uint8_t* ls = LEADER ? b.lis + (uint64_t)c.lis_bytes * r : nullptr;
   uint32_t flags = 0;
   const uint32_t MB = c.meas_len * 16;
@@ -516,8 +532,38 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
   // block m is consumed S (-> block m+1) and J (absorb block m) permute together: two
   // independent streams (keccak_p12_x2).
   uint32_t S[50], J[50];
-  // leader: load block m of the explicit share (words past the share's end read as 0)
+  // leader: load block m of the explicit share; absorb-only: of the staged share (words past the
+  // share's end read as 0). Block m = bytes [168m, 168m + 168): elements 21(m/2) + 0..10 (even m,
+  // the last one's low half) or + 10..20 (odd m, the first one's high half).
   auto load_block = [&](uint32_t m) {
+    if (ABSORB_ONLY) {
+      const uint32_t e0 = 21 * (m >> 1) + ((m & 1) ? 10 : 0);
+      uint4 v[11];
+#pragma unroll
+      for (int q = 0; q < 11; q++) v[q] = e0 + q < c.meas_len ? mstage[(uint64_t)(e0 + q) * IL] : make_uint4(0, 0, 0, 0);
+      if ((m & 1) == 0) {
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+          S[4 * q] = v[q].x;
+          S[4 * q + 1] = v[q].y;
+          S[4 * q + 2] = v[q].z;
+          S[4 * q + 3] = v[q].w;
+        }
+        S[40] = v[10].x;
+        S[41] = v[10].y;
+      } else {
+        S[0] = v[0].z;
+        S[1] = v[0].w;
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+          S[2 + 4 * q] = v[q + 1].x;
+          S[3 + 4 * q] = v[q + 1].y;
+          S[4 + 4 * q] = v[q + 1].z;
+          S[5 + 4 * q] = v[q + 1].w;
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < 21; q++) {
       const uint32_t off = 168 * m + 8 * q;
@@ -527,7 +573,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
       S[2 * q + 1] = v.y;
     }
   };
-  if (LEADER) {
+  if (LOADS) {
     load_block(0);
   } else {
     uint32_t kmeas[4];
@@ -575,6 +621,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
   };
   // emit the measurement elements of block m (10 or 11, by parity)
   auto emit_block = [&](uint32_t m) {
+    if (ABSORB_ONLY) return;  // staged by the squeeze-only launch
     const uint32_t e0 = 21 * (m >> 1);
     if ((m & 1) == 0) {
 #pragma unroll
@@ -645,7 +692,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
   };
   // advance to block m+1: helper squeezes (together with J's permutation), leader loads
   auto advance = [&](uint32_t m) {
-    if (LEADER) {
+    if (LOADS) {
       if (m + 1 < NM) load_block(m + 1);
       keccak_p12(J);
     } else if (m + 1 < NM) {
@@ -654,8 +701,17 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
       keccak_p12(J);
     }
   };
+  if (SQUEEZE_ONLY) {  // K1a: the measurement-share squeeze alone (one sponge per lane)
+    emit_block(0);
+#pragma unroll 1
+    for (uint32_t m = 1; m < NM; m++) {
+      keccak_p12(S);
+      emit_block(m);
+    }
+  }
   // blocks m = 0 .. b_last (b_last <= NM); blocks m < NM hold measurement bytes. Block 0 is
   // peeled so that the 42-byte header is dead inside the main loop.
+  else {
   emit_block(0);
   if (b_last == 0) {
     absorb_last(0, true);
@@ -672,6 +728,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
     if (have) emit_block(b_last);
     absorb_last(b_last, have);
   }
+  }
   uint32_t own_part[4] = {J[0], J[1], J[2], J[3]};
 
   // ---- proof share ------------------------------------------------------------------
@@ -684,7 +741,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
       bad |= ge_exact(v);
       pp[(uint64_t)e * IL] = v;
     }
-  } else {  // XOF(k_proofs, DST(2), [PROOFS=1, agg_id=1])
+  } else if (!ABSORB_ONLY) {  // XOF(k_proofs, DST(2), [PROOFS=1, agg_id=1])
     {
       uint32_t kproof[4];
       load16(hs + 16, kproof);
@@ -717,6 +774,11 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
     }
     if (gmax == 0xFFFFFFFFu) flags |= FLAG_SLOW;
   }
+  if (SQUEEZE_ONLY) {  // the absorb-only launch finishes the report (and ORs these flags in)
+    if (b.force_slow) flags |= FLAG_SLOW;
+    if (r0 < b.n) b.flags[r0] = flags;
+    return;
+  }
 
   uint32_t nonce[4];
   load16(b.nonces + 16 * r, nonce);
@@ -738,6 +800,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_kernel(Cfg c, Bufs b) {
     uint32_t part_l[4], lead_part[4];
     load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
     load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
+    if (ABSORB_ONLY) flags |= b.flags[r];  // the squeeze-only launch's screen
     flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, part_l, lead_part, own_part, flags, false);
     if (b.force_slow) flags |= FLAG_SLOW;
     if (r0 < b.n) b.flags[r0] = flags;
@@ -1804,13 +1867,22 @@ hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
   const dim3 grid((nb + K1_WAVES - 1) / K1_WAVES), block(64 * K1_WAVES);
   const bool wide = c.bits > 32 && (c.algo == ALGO_SUM || c.algo == ALGO_SUMVEC);
   if (b.leader && wide)
-    hipLaunchKernelGGL((xof_kernel<true, true>), grid, block, 0, s, c, b);
+    hipLaunchKernelGGL((xof_kernel<K1_LEADER, true>), grid, block, 0, s, c, b);
   else if (b.leader)
-    hipLaunchKernelGGL((xof_kernel<true, false>), grid, block, 0, s, c, b);
-  else if (wide)
-    hipLaunchKernelGGL((xof_kernel<false, true>), grid, block, 0, s, c, b);
+    hipLaunchKernelGGL((xof_kernel<K1_LEADER, false>), grid, block, 0, s, c, b);
+  else if (b.k1_split && wide) {
+    hipLaunchKernelGGL((xof_kernel<K1_SQUEEZE, true>), grid, block, 0, s, c, b);
+    hipLaunchKernelGGL((xof_kernel<K1_ABSORB, true>), grid, block, 0, s, c, b);
+  } else if (b.k1_split == 2) {
+    hipLaunchKernelGGL((xof_kernel<K1_SQUEEZE, false>), grid, block, 0, s, c, b);
+    hipLaunchKernelGGL((xof_kernel<K1_ABSORB2, false>), grid, block, 0, s, c, b);
+  } else if (b.k1_split) {
+    hipLaunchKernelGGL((xof_kernel<K1_SQUEEZE, false>), grid, block, 0, s, c, b);
+    hipLaunchKernelGGL((xof_kernel<K1_ABSORB, false>), grid, block, 0, s, c, b);
+  } else if (wide)
+    hipLaunchKernelGGL((xof_kernel<K1_FUSED, true>), grid, block, 0, s, c, b);
   else
-    hipLaunchKernelGGL((xof_kernel<false, false>), grid, block, 0, s, c, b);
+    hipLaunchKernelGGL((xof_kernel<K1_FUSED, false>), grid, block, 0, s, c, b);
   return hipGetLastError();
 }
 // Reports that occupy every K1 wave slot of the device exactly once: CUs x resident
@@ -1824,7 +1896,7 @@ uint64_t k1_round_reports(const Cfg& c, int device) {
   const uint32_t threads = c.algo == ALGO_COUNT ? 256u : 64u * K1_WAVES;
   hipError_t st = c.algo == ALGO_COUNT
                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, count_kernel<false>, threads, 0)
-                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_kernel<false>, threads, 0);
+                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_kernel<K1_FUSED>, threads, 0);
   if (st != hipSuccess || wgs <= 0) return 0;
   return (uint64_t)cus * (uint64_t)wgs * threads;
 }

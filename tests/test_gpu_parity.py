@@ -260,3 +260,27 @@ def test_shard_records_device_merge(name):
     assert D.merge_records(recs.cpu().numpy(), vdaf.field_bytes) == (agg, count, cs)
     for e in engs:
         e.close()
+
+
+@pytest.mark.parametrize("split", [1, 2], ids=["absorb_occ3", "absorb_occ2"])
+@pytest.mark.parametrize("name", ["sumvec_8x1000_88", "histogram_256_16", "sum64", "sumvec_small", "sumvec_64x20_9"])
+def test_k1_split_variants(name, split):
+    """The split helper K1 (squeeze-only launch, then absorb-only launch) == the oracle, fast and slow path."""
+    vdaf = CASES[name]
+    vk = bytes(range(60, 76))
+    orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
+    n = 150
+    nonces, ps, his, lps = _random_batch(orc, vk, n, seed=split * 7 + sum(map(ord, name)))
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
+    with HelperEngine(vdaf, vk) as eng:
+        eng.debug(3, split)
+        res = eng.helper_initialized_batch(nonces, ps, his, lps, want_out_shares=True)
+        np.testing.assert_array_equal(res.verdicts, want["verdicts"])
+        fin = want["verdicts"] == 0
+        np.testing.assert_array_equal(res.prep_msgs[fin], want["prep_msgs"][fin])
+        np.testing.assert_array_equal(res.out_shares[fin], want["out_shares"][fin])
+        eng.accumulate(n)
+        assert eng.aggregate_share(0) == (want["agg"], want["count"], want["checksum"])
+        eng.debug(1, 1)  # slow path behind the split launches
+        res = eng.helper_initialized_batch(nonces, ps, his, lps)
+        np.testing.assert_array_equal(res.verdicts, want["verdicts"])
