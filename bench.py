@@ -33,14 +33,25 @@ METRIC = "helper reports/sec (prep_init+aggregate), Prio3SumVec len=1000 @1/2/4/
 P128 = 2**128 - 28 * 2**64 + 1
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz = 78.6 int32 Top/s
 HBM_PEAK_GBPS = 8000.0
-# Algorithmic int32 VALU work: one Keccak-p[1600,12] permutation = 190 instructions/round
-# x 12 rounds on gfx950 (theta 20 v_bitop3 + 10 v_alignbit + 60 xor, rho 48 v_alignbit, chi 50 v_bitop3,
-# iota 2); one Field128 Montgomery product (K1 coefficients / inversion) = 56; one Field128 product in the
-# FLP wire sums (K3, 2 per measurement element) = 16 32x32->64 partial products.
+# K1 roofline, two counts:
+#  (a) instruction issue: the gfx950 instructions this Keccak needs per round (theta 20 v_bitop3 +
+#      10 v_alignbit + 60 xor, rho 48 v_alignbit, chi 50 v_bitop3, iota 2 = 190) x 12 rounds = 2280
+#      per permutation; 56 per Field128 Montgomery product; 16 per lazy FLP product. frac_issue says
+#      how busy the SIMDs' issue slots are. (Its ceiling is ~0.66: alignbit issues at half rate.)
+#  (b) algorithmic, kernel-independent: the spec's 64-bit operations of Keccak-p[1600] (theta 50,
+#      rho 24 rotations, chi 75, iota 1 = 155 per round; 1860 per 12-round permutation) counted as
+#      32-bit operations (x2: 3720) and 160 per Field128 product (16 32x32->64
+#      products at ~10 ops each). SURVEY.md priced these against a 39.3 T peak (256 CU x 64 lanes x
+#      2.4 GHz, 1 op per lane-cycle), which undercounts gfx950's 4 SIMD-32 per CU by 2x; here the
+#      peak is the 78.6 T int32 lane-op rate for both counts.
 OPS_PER_PERM = 190 * 12
 OPS_PER_MONT = 56
 OPS_PER_FMUL = 16
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v3_pmc_summary.json")
+ALG_OPS_PER_PERM = 3720
+ALG_OPS_PER_FMUL = 160
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_summary.json")
+KERNEL_SOURCES = ["janus_amd/csrc/jx_kernels.hip", "janus_amd/csrc/jx_engine.cpp", "janus_amd/csrc/jx_kernels.h",
+                  "janus_amd/csrc/jx_field.h", "janus_amd/csrc/jx_keccak.h", "janus_amd/csrc/jx_sha256.h"]
 
 
 def log(*a):
@@ -48,8 +59,19 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def sources_digest() -> str:
+    """sha256 over the engine's kernel sources: ties a PMC summary to the kernels it measured."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        h.update(open(os.path.join(ROOT, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
 def sumvec_work(bits, length, chunk):
-    """Per-report algorithmic work (perms, Montgomery products) of each stage."""
+    """Per-report work of each stage (permutations, field products) and its instruction /
+    algorithmic op counts and HBM bytes."""
     M = bits * length
     MB = M * 16
     calls = -(-M // chunk)
@@ -71,23 +93,31 @@ def sumvec_work(bits, length, chunk):
     return dict(perms=perms, mont_k1=mont_k1, fmul_k3=fmul_k3, mont_k3=mont_k3,
                 ops_k1=perms * OPS_PER_PERM + mont_k1 * OPS_PER_MONT,
                 ops_k3=fmul_k3 * OPS_PER_FMUL + mont_k3 * OPS_PER_MONT,
+                alg_ops_k1=perms * ALG_OPS_PER_PERM + mont_k1 * ALG_OPS_PER_FMUL,
+                alg_ops_k3=(fmul_k3 + mont_k3) * ALG_OPS_PER_FMUL,
                 hbm_k1=16 * (M + proof_len + 6 + 2 * calls) + 16 * length + 16 + 48 + 32 + 16,
                 hbm_k3=16 * (M + proof_len + 6 + 2 * calls) + 16 * (A + 3) + 1)
 
 
 def pmc_traffic(kernel: str, reports_per_launch: float):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (separate
-    FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction), scaled to this
-    run's reports per launch. None if the summary or kernel is missing."""
+    FETCH_SIZE / WRITE_SIZE passes over uniform launches; FETCH_SIZE doubled per the gfx950
+    correction), scaled to this run's reports per launch. Refused (None + reason) when the summary
+    was taken on other kernel sources, lacks the kernel, or has no launch size."""
     try:
         d = json.load(open(PMC_SUMMARY))
-        names = [k for k in d["kernels"] if k == kernel] or \
-            [k for k in d["kernels"] if k.startswith(kernel) and "<true" not in k and "true>" not in k]
-        e = d["kernels"][names[0]]
-        per_report = (e["hbm_read_bytes"] + e["hbm_write_bytes"]) / d["workload"]["reports_per_launch"]
-        return int(per_report * reports_per_launch), os.path.relpath(PMC_SUMMARY, ROOT)
-    except (OSError, KeyError, ValueError, IndexError):
-        return None, None
+    except (OSError, ValueError) as e:
+        return None, None, f"no PMC summary: {e}"
+    src = os.path.relpath(PMC_SUMMARY, ROOT)
+    wl = d.get("workload", {})
+    if wl.get("sources_digest") != sources_digest():
+        return None, src, "PMC summary was taken on other kernel sources"
+    e = d.get("kernels", {}).get(kernel)
+    if not e or "hbm_read_bytes" not in e or "hbm_write_bytes" not in e or not wl.get("reports_per_launch"):
+        return None, src, f"PMC summary lacks {kernel} bytes or its launch size"
+    per_report = (e["hbm_read_bytes"] + e["hbm_write_bytes"]) / wl["reports_per_launch"]
+    return int(per_report * reports_per_launch), src, f"{per_report:.0f} B/report over " \
+        f"{wl['reports_per_launch']}-report launches"
 
 
 def make_pool(vdaf, vk, K, seed=0x5EED, threads=16):
@@ -105,23 +135,50 @@ def make_pool(vdaf, vk, K, seed=0x5EED, threads=16):
     return orc, nonces, ps, his, lps, want
 
 
-def cpu_baseline(orc, vk, nonces, ps, his, lps, seconds, threads):
-    """The C oracle (a literal port of the reference algorithm) timed on this host's cores."""
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(orc, vdaf, vk, nonces, ps, his, lps, seconds, threads):
+    """The CPU engine (cpu_baseline/jc_cpu_engine.cpp: the same barycentric FLP, word-wise sponges and
+    lazy field sums as the GPU path, report-parallel) timed on this host's cores at 1 thread and at
+    `threads` threads on a bounded sample, plus the literal C oracle port as a secondary figure."""
+    from cpu_baseline import cpu_engine as CE
+
     K = nonces.shape[0]
-    n = K
+
+    def rate(threads_, budget):
+        m = min(K, max(16, threads_ * 8))
+        t = time.perf_counter()
+        CE.helper_prep_aggregate(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length, vk, nonces[:m], ps[:m],
+                                 his[:m], lps[:m], nthreads=threads_)
+        r0 = m / (time.perf_counter() - t)
+        n = min(K, max(m, int(budget * r0)))
+        t = time.perf_counter()
+        CE.helper_prep_aggregate(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length, vk, nonces[:n], ps[:n],
+                                 his[:n], lps[:n], nthreads=threads_)
+        dt = time.perf_counter() - t
+        return n / dt, n, dt
+
+    r1, n1, d1 = rate(1, seconds * 0.3)
+    rN, nN, dN = rate(threads, seconds * 0.5)
+    m = min(K, 256)
     t = time.perf_counter()
-    orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=threads)
-    dt = time.perf_counter() - t
-    rate = n / dt
-    # scale the sample to ~`seconds` of CPU work
-    reps = max(1, int(seconds * rate / K))
-    tile = lambda a: np.ascontiguousarray(np.tile(a, (reps, 1)))  # noqa: E731
-    t = time.perf_counter()
-    orc.helper_prep_batch(vk, tile(nonces), tile(ps), tile(his), tile(lps), nthreads=threads)
-    dt = time.perf_counter() - t
-    return {"value": round(reps * K / dt, 2), "unit": "reports/s", "cores": threads, "kind": "port",
-            "sample": f"{reps * K} Prio3SumVec(8x1000/88) helper prep_init+prep_next+aggregate reports "
-                      f"({K} distinct x {reps}), C oracle oracle/prio3_oracle.c, {threads} threads, {dt:.1f} s"}
+    orc.helper_prep_batch(vk, nonces[:m], ps[:m], his[:m], lps[:m], nthreads=threads)
+    r_oracle = m / (time.perf_counter() - t)
+    return {"value": round(rN, 1), "unit": "reports/s", "cores": threads, "kind": "port",
+            "value_1_thread": round(r1, 1), "cpu_model": cpu_model(),
+            "oracle_port_reports_per_s": round(r_oracle, 1),
+            "sample": f"{nN} Prio3SumVec({vdaf.bits}x{vdaf.length}/{vdaf.chunk_length}) helper prep_init+prep_next+"
+                      f"aggregate reports at {threads} threads ({dN:.1f} s) and {n1} at 1 thread ({d1:.1f} s): "
+                      "C++ CPU engine cpu_baseline/jc_cpu_engine.cpp (byte-checked against the fixtures); "
+                      f"the literal C oracle (oracle/prio3_oracle.c) does {r_oracle:.0f}/s at {threads} threads"}
 
 
 def _free_port() -> int:
@@ -162,7 +219,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reports-per-gpu", type=int, default=1_250_000)
-    ap.add_argument("--pool", type=int, default=2048)
+    ap.add_argument("--pool", type=int, default=32768)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--bits", type=int, default=8)
@@ -234,23 +291,18 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
-    # ---- verification: aggregate == (steps + warmup) * multiplicity * pool aggregate
+    # ---- verification: aggregate == (steps + warmup) * (q * pool aggregate + aggregate of the first
+    # R - q K pool reports), R = q K + rem; count likewise; every verdict == the oracle's
     agg, count, _ = eng.aggregate_share(0)
     total_steps = args.steps + args.warmup
-    mult = np.bincount(np.arange(R) % args.pool, minlength=args.pool)
-    fin = want["verdicts"] == 0
-    exp_count = total_steps * int(mult[fin].sum())
-    # expected aggregate = total_steps * sum_i mult_i * out_i ; recompute from per-report out shares
-    res = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=threads, want_out_shares=True)
-    outs = res["out_shares"].reshape(args.pool, vdaf.output_len, 16)
-    vals = [int.from_bytes(bytes(b), "little") for b in outs.reshape(-1, 16)]
-    acc = [0] * vdaf.output_len
-    for i in range(args.pool):
-        if res["verdicts"][i] == 0:
-            m = int(mult[i]) * total_steps
-            for j in range(vdaf.output_len):
-                acc[j] += m * vals[i * vdaf.output_len + j]
-    exp = b"".join((x % P128).to_bytes(16, "little") for x in acc)
+    q, rem = divmod(R, args.pool)
+    head = orc.helper_prep_batch(vk, nonces[:rem], ps[:rem], his[:rem], lps[:rem], nthreads=threads) if rem else \
+        {"agg": bytes(16 * vdaf.output_len), "count": 0}
+    dec = lambda b: [int.from_bytes(b[16 * j:16 * j + 16], "little") for j in range(vdaf.output_len)]  # noqa: E731
+    pool_agg, head_agg = dec(want["agg"]), dec(head["agg"])
+    acc = [(q * a + h) * total_steps % P128 for a, h in zip(pool_agg, head_agg)]
+    exp = b"".join(x.to_bytes(16, "little") for x in acc)
+    exp_count = total_steps * (q * want["count"] + head["count"])
     verified = agg == exp and count == exp_count
     verdict_ok = bool(np.array_equal(d_verdicts.cpu().numpy(), np.tile(want["verdicts"], reps)[:R]))
     if world > 1:
@@ -262,15 +314,22 @@ def main():
     value = total_reports / elapsed
     work = sumvec_work(args.bits, args.length, args.chunk)
     launches = max(1, kt["xof"]["launches"])
-    chunk_reports = R / (launches / args.steps)  # reports per K1 launch
+    per_rank = R * args.steps               # reports this rank prepared in the timed region
+    chunk_reports = per_rank / launches     # average reports per K1 launch
     k1_ms = kt["xof"]["ms"] / launches
     k3_ms = kt["flp"]["ms"] / max(1, kt["flp"]["launches"])
-    k1_tops = work["ops_k1"] * chunk_reports / (k1_ms * 1e-3) / 1e12
-    k3_tops = work["ops_k3"] * chunk_reports / (k3_ms * 1e-3) / 1e12
-    dominant = "K1 xof_kernel" if kt["xof"]["ms"] >= kt["flp"]["ms"] else "K3 flp_psum_part_kernel"
-    ach = k1_tops if dominant.startswith("K1") else k3_tops
-    traffic, traffic_src = pmc_traffic("jx::xof_kernel" if dominant.startswith("K1") else
-                                       "jx::flp_psum_part_kernel", chunk_reports)
+    # achieved rates from total kernel time over total reports (exact for unequal launches)
+    k1_tops = work["ops_k1"] * per_rank / (kt["xof"]["ms"] * 1e-3) / 1e12
+    k3_tops = work["ops_k3"] * per_rank / (kt["flp"]["ms"] * 1e-3) / 1e12
+    k1_alg = work["alg_ops_k1"] * per_rank / (kt["xof"]["ms"] * 1e-3) / 1e12
+    k3_alg = work["alg_ops_k3"] * per_rank / (kt["flp"]["ms"] * 1e-3) / 1e12
+    k1_dom = kt["xof"]["ms"] >= kt["flp"]["ms"]
+    dominant = "K1 xof_kernel" if k1_dom else "K3 flp_psum_part_kernel"
+    ach, alg = (k1_tops, k1_alg) if k1_dom else (k3_tops, k3_alg)
+    traffic, traffic_src, traffic_note = pmc_traffic("jx::xof_kernel<0, false>" if k1_dom else
+                                                     "jx::flp_psum_part_kernel<2, false, false>", chunk_reports)
+    alg_bytes = (work["hbm_k1"] if k1_dom else work["hbm_k3"]) * chunk_reports
+    dom_ms = k1_ms if k1_dom else k3_ms
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -290,12 +349,17 @@ def main():
                    "reports_per_gpu": R, "global_reports_per_step": R * world,
                    "parallelism": f"report-sharded x{world} (RCCL all-gather + device mod-p combine)"},
         "roofline": {"bound": "valu", "kernel": dominant, "achieved": round(ach, 3), "peak": round(VALU_PEAK_TOPS, 2),
-                     "unit": "TOP/s (int32 VALU instructions/s, algorithmic count: DESIGN.md §5)",
+                     "unit": "TOP/s int32 instruction issue (2280 per Keccak-p[1600,12]; DESIGN.md §5)",
                      "frac": round(ach / VALU_PEAK_TOPS, 4),
-                     "traffic": traffic, "traffic_unit": "HBM bytes per launch (rocprofv3 2*FETCH_SIZE + WRITE_SIZE)",
-                     "traffic_source": traffic_src,
-                     "algorithmic_bytes": int(work["hbm_k1"] * chunk_reports),
-                     "hbm_GBps": round(work["hbm_k1"] * chunk_reports / (k1_ms * 1e-3) / 1e9, 1),
+                     "achieved_algorithmic": round(alg, 3),
+                     "frac_algorithmic": round(alg / VALU_PEAK_TOPS, 4),
+                     "algorithmic_unit": "TOP/s of the spec's 32-bit ops (3720 per Keccak-p[1600,12], 160 per "
+                                         "Field128 product), kernel-independent",
+                     "traffic": traffic, "traffic_unit": "HBM bytes per average launch (rocprofv3 2*FETCH_SIZE + "
+                                                         "WRITE_SIZE)",
+                     "traffic_source": traffic_src, "traffic_note": traffic_note,
+                     "algorithmic_bytes": int(alg_bytes), "reports_per_launch": round(chunk_reports, 1),
+                     "hbm_GBps": round(alg_bytes / (dom_ms * 1e-3) / 1e9, 1),
                      "hbm_peak_GBps": HBM_PEAK_GBPS},
         "kernels": {"k1_xof_ms_per_launch": round(k1_ms, 3), "k3_flp_ms_per_launch": round(k3_ms, 3),
                     "k4_acc_ms_per_launch": round(kt["accumulate"]["ms"] / max(1, kt["accumulate"]["launches"]), 3),
@@ -308,7 +372,7 @@ def main():
         "verified": bool(verified and verdict_ok),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(orc, vk, nonces, ps, his, lps, args.cpu_seconds, threads)
+        out["cpu_baseline"] = cpu_baseline(orc, vdaf, vk, nonces, ps, his, lps, args.cpu_seconds, threads)
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

@@ -19,6 +19,7 @@ import csv
 import glob
 import json
 import os
+import sys
 
 
 def short(name: str) -> str:
@@ -29,8 +30,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("prof_dir")
     ap.add_argument("--reports-per-launch", type=int, default=0)
+    ap.add_argument("--command", default="")
     a = ap.parse_args()
-    out = {"kernels": {}}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    out = {"workload": {"reports_per_launch": a.reports_per_launch, "sources_digest": bench.sources_digest(),
+                        "command": a.command,
+                        "counters": "separate rocprofv3 --pmc passes; hbm_read_bytes = 2 x FETCH_SIZE x 1024 "
+                                    "(gfx950 correction), hbm_write_bytes = WRITE_SIZE x 1024"},
+           "kernels": {}}
     stats = os.path.join(a.prof_dir, "trace", "run_kernel_stats.csv")
     if os.path.exists(stats):
         for r in csv.DictReader(open(stats)):
@@ -67,7 +76,7 @@ def main():
                 e["valu_util"] = p["SQ_INSTS_VALU"] / (256 * 4 * cyc / 2)
         if a.reports_per_launch and "hbm_read_bytes" in e and "hbm_write_bytes" in e:
             e["hbm_bytes_per_report"] = (e["hbm_read_bytes"] + e["hbm_write_bytes"]) / a.reports_per_launch
-    json.dump(out, __import__("sys").stdout, indent=1)
+    json.dump(out, sys.stdout, indent=1)
 
 
 if __name__ == "__main__":
