@@ -159,10 +159,11 @@ def cpu_baseline(orc, vdaf, vk, nonces, ps, his, lps, seconds, threads):
         CE.helper_prep_aggregate(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length, vk, nonces[:m], ps[:m],
                                  his[:m], lps[:m], nthreads=threads_)
         r0 = m / (time.perf_counter() - t)
-        n = min(K, max(m, int(budget * r0)))
+        n = max(m, int(budget * r0))  # the pool tiled to ~budget seconds
+        idx = np.arange(n) % K
         t = time.perf_counter()
-        CE.helper_prep_aggregate(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length, vk, nonces[:n], ps[:n],
-                                 his[:n], lps[:n], nthreads=threads_)
+        CE.helper_prep_aggregate(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length, vk, nonces[idx], ps[idx],
+                                 his[idx], lps[idx], nthreads=threads_)
         dt = time.perf_counter() - t
         return n / dt, n, dt
 
