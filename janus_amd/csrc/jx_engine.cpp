@@ -87,6 +87,7 @@ struct jx_engine {
   uint64_t launches[NST] = {0, 0, 0, 0};
   uint32_t force_slow = 0;
   uint32_t k1_split = 0;  // helper K1 as squeeze-only + absorb-only launches (JX_K1_SPLIT, debug option 3)
+  uint32_t k3_pf = 1;     // K3 load pipeline variant (JX_K3_PF, debug option 4)
   std::string err;
 };
 
@@ -561,6 +562,7 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
   b.consts = e->d_consts;
   b.force_slow = e->force_slow;
   b.k1_split = e->k1_split;
+  b.k3_pf = e->k3_pf;
   hipEvent_t ev = nullptr;
   if (c.algo == ALGO_COUNT) {
     HIPCHK(e, stage_begin(e, &ev));
@@ -832,6 +834,10 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
   }
   e->default_chunk = chunk;
   if (const char* env = getenv("JX_K1_SPLIT")) e->k1_split = (uint32_t)atoi(env) % 3;
+  if (const char* env = getenv("JX_K3_PF")) {
+    const int v = atoi(env);
+    if (v == 1 || v == 2 || v == 12 || v == 13) e->k3_pf = (uint32_t)v;
+  }
   *out = e;
   return JX_OK;
 }
@@ -1300,6 +1306,11 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
   if (option == 3) {  // K1 variant: 0 fused two-sponge kernel, 1 squeeze-only + absorb-only launches
     if (value < 0 || value > 2) return JX_E_INVALID;
     e->k1_split = (uint32_t)value;  // 2: the absorb-only launch at 2 waves/SIMD
+    return JX_OK;
+  }
+  if (option == 4) {  // K3 load pipeline: 1 or 2 calls ahead; 12 / 13 = 2 / 3 ahead at 3 waves/SIMD
+    if (value != 1 && value != 2 && value != 12 && value != 13) return JX_E_INVALID;
+    e->k3_pf = (uint32_t)value;
     return JX_OK;
   }
   if (option == 2) {  // accumulate chunking (tests)

@@ -277,7 +277,15 @@ JX_HD void wacc_mac(wacc26& a, const limbs26& x, const limbs26& c) {
 #pragma unroll
   for (int i = 0; i < 5; i++)
 #pragma unroll
-    for (int j = 0; j < 5; j++) a.col[i + j] += (uint64_t)x.l[i] * c.l[j];
+    for (int j = 0; j < 5; j++) {
+      a.col[i + j] += (uint64_t)x.l[i] * c.l[j];
+#ifdef __HIP_DEVICE_COMPILE__
+      // keeps every product accumulating straight into its column (one v_mad_u64_u32 each);
+      // without it the compiler sums a column's products in a side chain and adds that with
+      // an extra 64-bit add per column
+      asm("" : "+v"(a.col[i + j]));
+#endif
+    }
 }
 // carry-propagate so that col[0..7] < 2^26 (keeps headroom for further terms)
 JX_HD void wacc_normalize(wacc26& a) {

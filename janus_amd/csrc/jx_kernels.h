@@ -105,6 +105,7 @@ struct Bufs {
   const uint4* consts;
   uint32_t force_slow;  // debug: route every report through the slow XOF kernel
   uint32_t k1_split;    // helper K1 as two launches (squeeze-only, absorb-only) instead of one
+  uint32_t k3_pf;       // ParallelSum FLP part kernel: calls of loads in flight (1..3)
 };
 
 struct AccArgs {

@@ -1048,8 +1048,10 @@ __global__ __launch_bounds__(256) void flp_sum_kernel(Cfg c, Bufs b) {
 // slots, its share of v (sum_m g_m S_m), its share of G(t), and (Histogram) sum of x.
 // Phase 2 (flp_psum_final_kernel): one report per lane; adds the partials, the leader's
 // v and G(t), and decides.
-template <int PPW, bool HIST, bool LEADER>
-__global__ __launch_bounds__(64, 4) void flp_psum_part_kernel(Cfg c, Bufs b) {
+// PF: calls whose loads are in flight ahead of the one being multiplied (a ring of PF register
+// sets; the HBM latency is several calls' worth of VALU work at 4 waves/SIMD).
+template <int PPW, bool HIST, bool LEADER, int PF = 1, int OCC = 4>
+__global__ __launch_bounds__(64, OCC) void flp_psum_part_kernel(Cfg c, Bufs b) {
   const uint32_t NG = c.ngroups;
   // Workgroup ids are dispatched round-robin over the 8 XCDs; map them so that the NG
   // groups of one block run back to back on one XCD and share its L2 (coefficients,
@@ -1084,30 +1086,44 @@ __global__ __launch_bounds__(64, 4) void flp_psum_part_kernel(Cfg c, Bufs b) {
   if (j0 + PPW <= chunk && M >= j0 + PPW) kf = min(C, (M - j0 - PPW) / chunk + 1);
   for (uint32_t k0 = 1; k0 <= kf; k0 += 512) {  // <= 5 * 512 limb products (< 2^52) per column
     const uint32_t k1 = min(kf, k0 + 511);
-    // software pipeline: the loads of call k+1 are in flight while call k multiplies
-    uint4 cn = coefb[(COEF_K + 2 * (k0 - 1)) * IL], dn = coefb[(COEF_K + 2 * (k0 - 1) + 1) * IL];
-    uint4 xn[PPW];
+    // software pipeline: the loads of calls k+1 .. k+PF are in flight while call k multiplies
+    uint4 cr[PF], dr[PF], xr[PF][PPW];
 #pragma unroll
-    for (int i = 0; i < PPW; i++) xn[i] = measb[(uint64_t)((k0 - 1) * chunk + j0 + i) * IL];
-#pragma unroll 1
-    for (uint32_t k = k0; k <= k1; k++) {
-      const limbs26 ck = to_limbs26(u4_to_f(cn));
-      const limbs26 dk = to_limbs26(u4_to_f(dn));
-      f128 x[PPW];
+    for (int u = 0; u < PF; u++) {
+      const uint32_t k = k0 + u;
+      if (k <= k1) {
+        cr[u] = coefb[(COEF_K + 2 * (k - 1)) * IL];
+        dr[u] = coefb[(COEF_K + 2 * (k - 1) + 1) * IL];
 #pragma unroll
-      for (int i = 0; i < PPW; i++) x[i] = u4_to_f(xn[i]);
-      if (k < k1) {
-        cn = coefb[(COEF_K + 2 * k) * IL];
-        dn = coefb[(COEF_K + 2 * k + 1) * IL];
-#pragma unroll
-        for (int i = 0; i < PPW; i++) xn[i] = measb[(uint64_t)(k * chunk + j0 + i) * IL];
+        for (int i = 0; i < PPW; i++) xr[u][i] = measb[(uint64_t)((k - 1) * chunk + j0 + i) * IL];
       }
+    }
+#pragma unroll 1
+    for (uint32_t kb = k0; kb <= k1; kb += PF) {
 #pragma unroll
-      for (int i = 0; i < PPW; i++) {
-        const limbs26 xl = to_limbs26(x[i]);
-        wacc_mac(ae[i], xl, dk);
-        wacc_mac(ao[i], xl, ck);
-        if (HIST) acc_add128(sx, x[i]);
+      for (int u = 0; u < PF; u++) {
+        const uint32_t k = kb + u;
+        if (k <= k1) {
+          const limbs26 ck = to_limbs26(u4_to_f(cr[u]));
+          const limbs26 dk = to_limbs26(u4_to_f(dr[u]));
+          f128 x[PPW];
+#pragma unroll
+          for (int i = 0; i < PPW; i++) x[i] = u4_to_f(xr[u][i]);
+          const uint32_t kn = k + PF;
+          if (kn <= k1) {
+            cr[u] = coefb[(COEF_K + 2 * (kn - 1)) * IL];
+            dr[u] = coefb[(COEF_K + 2 * (kn - 1) + 1) * IL];
+#pragma unroll
+            for (int i = 0; i < PPW; i++) xr[u][i] = measb[(uint64_t)((kn - 1) * chunk + j0 + i) * IL];
+          }
+#pragma unroll
+          for (int i = 0; i < PPW; i++) {
+            const limbs26 xl = to_limbs26(x[i]);
+            wacc_mac(ae[i], xl, dk);
+            wacc_mac(ao[i], xl, ck);
+            if (HIST) acc_add128(sx, x[i]);
+          }
+        }
       }
     }
 #pragma unroll
@@ -1918,7 +1934,7 @@ hipError_t launch_xof_slow(const Cfg& c, const Bufs& b, hipStream_t s) {
 int psum_ppw(uint32_t chunk) {
   if (const char* env = getenv("JX_PPW")) {
     int v = atoi(env);
-    if (v == 8 || v == 4 || v == 2 || v == 1) return v;
+    if (v == 2 || v == 1) return v;  // (4 and 8 slots per wave spill: 0.3-4 KB/lane, removed)
   }
   const int cands[] = {2, 1};
   int best = 2, best_cost = 1 << 30;
@@ -1933,11 +1949,22 @@ int psum_ppw(uint32_t chunk) {
   return best;
 }
 
+// k3_pf: calls of loads in flight, + 10 for the 3-waves/SIMD (168-VGPR) build
+template <int PPW, bool HIST, bool LEADER>
+static void launch_psum_part(const Cfg& c, const Bufs& b, hipStream_t s, uint32_t grid) {
+  if (b.k3_pf == 2)
+    hipLaunchKernelGGL((flp_psum_part_kernel<PPW, HIST, LEADER, 2>), dim3(grid), dim3(64), 0, s, c, b);
+  else if (b.k3_pf == 12)
+    hipLaunchKernelGGL((flp_psum_part_kernel<PPW, HIST, LEADER, 2, 3>), dim3(grid), dim3(64), 0, s, c, b);
+  else if (b.k3_pf == 13)
+    hipLaunchKernelGGL((flp_psum_part_kernel<PPW, HIST, LEADER, 3, 3>), dim3(grid), dim3(64), 0, s, c, b);
+  else
+    hipLaunchKernelGGL((flp_psum_part_kernel<PPW, HIST, LEADER>), dim3(grid), dim3(64), 0, s, c, b);
+}
 template <int PPW, bool HIST, bool LEADER>
 static void launch_psum_r(const Cfg& c, const Bufs& b, hipStream_t s) {
   const uint32_t nb = nblk_of(b.n);
-  const uint32_t grid = ((nb + 7) / 8) * 8 * c.ngroups;
-  hipLaunchKernelGGL((flp_psum_part_kernel<PPW, HIST, LEADER>), dim3(grid), dim3(64), 0, s, c, b);
+  launch_psum_part<PPW, HIST, LEADER>(c, b, s, ((nb + 7) / 8) * 8 * c.ngroups);
   hipLaunchKernelGGL((flp_psum_final_kernel<HIST, LEADER>), dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s,
                      c, b);
 }
@@ -1958,8 +1985,7 @@ static hipError_t launch_psum_t(const Cfg& c, const Bufs& b, hipStream_t s) {
 template <int PPW, bool LEADER>
 static void launch_fp_r(const Cfg& c, const Bufs& b, hipStream_t s) {
   const uint32_t nb = nblk_of(b.n);
-  hipLaunchKernelGGL((flp_psum_part_kernel<PPW, false, LEADER>), dim3(((nb + 7) / 8) * 8 * c.ngroups), dim3(64), 0,
-                     s, c, b);
+  launch_psum_part<PPW, false, LEADER>(c, b, s, ((nb + 7) / 8) * 8 * c.ngroups);
   hipLaunchKernelGGL((flp_norm_part_kernel<2, LEADER>), dim3(((nb + 7) / 8) * 8 * c.ngroups1), dim3(64), 0, s, c,
                      b);
   hipLaunchKernelGGL((flp_fp_final_kernel<LEADER>), dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, c, b);
@@ -1991,10 +2017,6 @@ hipError_t launch_flp(const Cfg& c, const Bufs& b, hipStream_t s) {
     return hipGetLastError();
   }
   switch (c.ppw) {
-    case 8:
-      return launch_psum_t<8>(c, b, s);
-    case 4:
-      return launch_psum_t<4>(c, b, s);
     case 2:
       return launch_psum_t<2>(c, b, s);
     case 1:

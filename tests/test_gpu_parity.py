@@ -284,3 +284,38 @@ def test_k1_split_variants(name, split):
         eng.debug(1, 1)  # slow path behind the split launches
         res = eng.helper_initialized_batch(nonces, ps, his, lps)
         np.testing.assert_array_equal(res.verdicts, want["verdicts"])
+
+
+@pytest.mark.parametrize("pf", [2, 12, 13], ids=["pf2_occ4", "pf2_occ3", "pf3_occ3"])
+@pytest.mark.parametrize("name", ["sumvec_8x1000_88", "histogram_256_16", "sumvec_64x20_9", "sumvec_small"])
+def test_k3_pipeline_variants(name, pf):
+    """The deeper-pipelined ParallelSum FLP part kernels == the oracle, helper (verdicts, messages,
+    output shares, aggregate) and leader (prep shares)."""
+    vdaf = CASES[name]
+    vk = bytes(range(90, 106))
+    orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
+    n = 150
+    nonces, ps, his, lps = _random_batch(orc, vk, n, seed=pf * 11 + sum(map(ord, name)))
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
+    with HelperEngine(vdaf, vk) as eng:
+        eng.debug(4, pf)
+        res = eng.helper_initialized_batch(nonces, ps, his, lps, want_out_shares=True)
+        np.testing.assert_array_equal(res.verdicts, want["verdicts"])
+        fin = want["verdicts"] == 0
+        np.testing.assert_array_equal(res.prep_msgs[fin], want["prep_msgs"][fin])
+        np.testing.assert_array_equal(res.out_shares[fin], want["out_shares"][fin])
+        eng.accumulate(n)
+        assert eng.aggregate_share(0) == (want["agg"], want["count"], want["checksum"])
+    rng = np.random.default_rng(pf)
+    meas = rng.integers(0, 1 << vdaf.bits, size=(24, vdaf.length), dtype=np.uint64) \
+        if vdaf.algo_id == O.SUMVEC else rng.integers(0, vdaf.length, size=(24, 1), dtype=np.uint64)
+    ln = rng.integers(0, 256, size=(24, 16), dtype=np.uint8)
+    rands = rng.integers(0, 256, size=(24, orc.sizes.client_rand), dtype=np.uint8)
+    shards = [orc.shard(meas[i], ln[i].tobytes(), rands[i].tobytes()) for i in range(24)]
+    lps_, lis_ = (np.stack([np.frombuffer(s[k], np.uint8) for s in shards]) for k in (0, 1))
+    with HelperEngine(vdaf, vk) as eng:
+        eng.debug(4, pf)
+        init = eng.leader_initialized_batch(ln, lps_, lis_)
+    for i in range(24):
+        rc, share, _, _ = orc.prep_init(vk, 0, ln[i].tobytes(), lps_[i].tobytes(), lis_[i].tobytes())
+        assert rc == 0 and init.prep_shares[i].tobytes() == share, i
