@@ -810,7 +810,11 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
   // reports in flight: grow the budget toward one full K1 round, up to 1/3 of the device memory
   // (two engines, e.g. leader and helper, still fit on one MI355X). JX_STAGING_GB / JX_CHUNK_REPORTS override.
   const uint64_t per = per_report_bytes(e->cfg);
-  e->round_reports = k1_round_reports(e->cfg, device);
+  if (const char* env = getenv("JX_K1_SPLIT")) {
+    const int v = atoi(env);
+    if (v >= 0 && v <= 4) e->k1_split = (uint32_t)v;
+  }
+  e->round_reports = k1_round_reports(e->cfg, device, e->k1_split);
   uint64_t budget = 48ull << 30;
   size_t mem_free = 0, mem_total = 0;
   if (hipMemGetInfo(&mem_free, &mem_total) == hipSuccess && e->round_reports &&
@@ -833,10 +837,9 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
     if (v >= 64) chunk = v / 64 * 64;
   }
   e->default_chunk = chunk;
-  if (const char* env = getenv("JX_K1_SPLIT")) e->k1_split = (uint32_t)atoi(env) % 3;
   if (const char* env = getenv("JX_K3_PF")) {
     const int v = atoi(env);
-    if (v == 1 || v == 2 || v == 12 || v == 13) e->k3_pf = (uint32_t)v;
+    if (v == 1 || v == 2 || v == 12 || v == 13 || v == 20 || v == 21) e->k3_pf = (uint32_t)v;
   }
   *out = e;
   return JX_OK;
@@ -1304,12 +1307,12 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
     return JX_OK;
   }
   if (option == 3) {  // K1 variant: 0 fused two-sponge kernel, 1 squeeze-only + absorb-only launches
-    if (value < 0 || value > 2) return JX_E_INVALID;
-    e->k1_split = (uint32_t)value;  // 2: the absorb-only launch at 2 waves/SIMD
+    if (value < 0 || value > 4) return JX_E_INVALID;
+    e->k1_split = (uint32_t)value;  // 2: the absorb-only launch at 2 waves/SIMD; 3: lane-split; 4: sequential S, J
     return JX_OK;
   }
-  if (option == 4) {  // K3 load pipeline: 1 or 2 calls ahead; 12 / 13 = 2 / 3 ahead at 3 waves/SIMD
-    if (value != 1 && value != 2 && value != 12 && value != 13) return JX_E_INVALID;
+  if (option == 4) {  // K3 load pipeline: 1 or 2 calls ahead; 12 / 13 = 2 / 3 ahead at 3 waves/SIMD; 20 / 21 LDS-DMA ring
+    if (value != 1 && value != 2 && value != 12 && value != 13 && value != 20 && value != 21) return JX_E_INVALID;
     e->k3_pf = (uint32_t)value;
     return JX_OK;
   }

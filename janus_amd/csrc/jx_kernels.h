@@ -175,7 +175,7 @@ hipError_t launch_record_combine(const Cfg& c, const uint8_t* parts, uint32_t np
 hipError_t launch_transpose_out(const Cfg& c, const uint4* outs, uint64_t n, uint8_t* dst, hipStream_t s);
 hipError_t launch_agg_encode(const Cfg& c, const uint4* agg, uint8_t* dst, hipStream_t s);
 // multiproof Field64 SumVec (jx_mp64.hip)
-uint64_t k1_round_reports(const Cfg& c, int device);
+uint64_t k1_round_reports(const Cfg& c, int device, uint32_t k1_split = 0);
 uint64_t mp_k1_round_reports(int device);
 hipError_t launch_mp_xof(const Cfg& c, const Bufs& b, hipStream_t s);
 hipError_t launch_mp_slow(const Cfg& c, const Bufs& b, hipStream_t s);

@@ -18,6 +18,8 @@
 // Algorithm: draft-irtf-cfrg-vdaf-08 as implemented by prio 0.16.1; see DESIGN.md.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "jx_field.h"
 #include "jx_kernels.h"
 #include "jx_keccak.h"
@@ -247,6 +249,14 @@ __device__ __forceinline__ void trunc_add(acc192& a, f128 x, uint32_t sh) {
   a.w2 = a.w2 + w2 + cc;
 }
 
+// A value the optimizer cannot see through (no instruction is emitted): keeps x * 2^j a single
+// v_mad_u64_u32 (x * 2^j + T) instead of the zero-extend + 64-bit shift + 64-bit add it would
+// strength-reduce the multiply to.
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // Output-share truncation in the fast XOF kernel (SumVec / Sum):
 //   out_i = sum_{j<bits} 2^j x_{bits*i+j} mod p.
 // Word columns T_w = sum_j x_{j,w} 2^j (< 2^(32+bits) <= 2^64) cost one v_mad_u64_u32 per 32-bit
@@ -283,28 +293,30 @@ __device__ __forceinline__ f128 shl32_mod(f128 h) {
 template <bool WIDE>
 __device__ __forceinline__ void emit_meas(const Cfg& c, uint4* mp, uint4* op, uint32_t e, uint4 v, uint32_t& gmax,
                                           TruncW& tr, f128& lo) {
-  if (e >= c.meas_len) return;
-  gmax = max(gmax, ge_screen(v));
-  mp[(uint64_t)e * IL] = v;
-  if (!c.out_is_meas && e < c.trunc_len) {  // FixedPoint: the trailing norm bits are not truncated
-    const uint32_t sh = 1u << (WIDE ? (tr.j & 31u) : tr.j);
-    tr.T[0] += (uint64_t)v.x * sh;
-    tr.T[1] += (uint64_t)v.y * sh;
-    tr.T[2] += (uint64_t)v.z * sh;
-    tr.T[3] += (uint64_t)v.w * sh;
-    ++tr.j;
-    if (WIDE && tr.j == 32 && c.bits > 32) {
-      lo = truncw_value(tr);
-      truncw_zero(tr);
-    }
-    if (tr.j == c.bits) {
-      f128 val = truncw_value(tr);
-      if (WIDE && c.bits > 32) val = add128(lo, shl32_mod(val));
-      op[(uint64_t)tr.i * IL] = f_to_u4(val);
-      truncw_zero(tr);
-      tr.j = 0;
-      tr.i++;
-    }
+  // e is uniform. Straight-line except for the store guard and the once-per-output-element finish:
+  // elements past the share (last block) or not truncated (Histogram; FixedPoint's trailing norm
+  // bits) add with weight 0 instead of branching around the column sums.
+  const bool in = e < c.meas_len;
+  if (in) mp[(uint64_t)e * IL] = v;
+  gmax = max(gmax, in ? ge_screen(v) : 0u);
+  const bool tin = !c.out_is_meas && e < c.trunc_len;
+  const uint32_t sh = opaque_u32(tin ? 1u << (WIDE ? (tr.j & 31u) : tr.j) : 0u);
+  tr.T[0] += (uint64_t)v.x * sh;
+  tr.T[1] += (uint64_t)v.y * sh;
+  tr.T[2] += (uint64_t)v.z * sh;
+  tr.T[3] += (uint64_t)v.w * sh;
+  tr.j += tin ? 1u : 0u;
+  if (WIDE && tin && tr.j == 32 && c.bits > 32) {
+    lo = truncw_value(tr);
+    truncw_zero(tr);
+  }
+  if (tin && tr.j == c.bits) {
+    f128 val = truncw_value(tr);
+    if (WIDE && c.bits > 32) val = add128(lo, shl32_mod(val));
+    op[(uint64_t)tr.i * IL] = f_to_u4(val);
+    truncw_zero(tr);
+    tr.j = 0;
+    tr.i++;
   }
 }
 __device__ __forceinline__ void emit_proof(const Cfg& c, uint4* pp, uint32_t e, uint4 v, uint32_t& gmax) {
@@ -496,10 +508,13 @@ __device__ __forceinline__ bool ge_exact(uint4 v) {
 // launches instead of one 2-sponge kernel at 2 waves/SIMD; +128 KB/report of staging reads.
 constexpr uint32_t K1_WAVES = 4;  // waves (64-report blocks) per K1 workgroup
 // K1_ABSORB2: the absorb-only launch built for 2 waves/SIMD (no spills) instead of 3
-enum : int { K1_FUSED = 0, K1_LEADER = 1, K1_SQUEEZE = 2, K1_ABSORB = 3, K1_ABSORB2 = 4 };
+// K1_SEQ: the fused kernel with the S and J permutations one after the other (not interleaved), built
+// for 3 waves/SIMD
+enum : int { K1_FUSED = 0, K1_LEADER = 1, K1_SQUEEZE = 2, K1_ABSORB = 3, K1_ABSORB2 = 4, K1_SEQ = 5 };
 template <int MODE>
 struct K1Occ {  // min waves per SIMD the register budget is built for
-  static constexpr int value = MODE == K1_SQUEEZE ? 4 : (MODE == K1_ABSORB ? 3 : (MODE == K1_ABSORB2 ? 2 : 1));
+  static constexpr int value =
+      MODE == K1_SQUEEZE ? 4 : (MODE == K1_ABSORB || MODE == K1_SEQ ? 3 : (MODE == K1_ABSORB2 ? 2 : 1));
 };
 template <int MODE, bool WIDE = false>
 __global__ __launch_bounds__(64 * K1_WAVES, K1Occ<MODE>::value) void xof_kernel(Cfg c, Bufs b) {
@@ -695,6 +710,9 @@ __global__ __launch_bounds__(64 * K1_WAVES, K1Occ<MODE>::value) void xof_kernel(
     if (LOADS) {
       if (m + 1 < NM) load_block(m + 1);
       keccak_p12(J);
+    } else if (m + 1 < NM && MODE == K1_SEQ) {
+      keccak_p12(S);
+      keccak_p12(J);
     } else if (m + 1 < NM) {
       keccak_p12_x2(S, J);
     } else {
@@ -802,6 +820,289 @@ __global__ __launch_bounds__(64 * K1_WAVES, K1Occ<MODE>::value) void xof_kernel(
     load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
     if (ABSORB_ONLY) flags |= b.flags[r];  // the squeeze-only launch's screen
     flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, part_l, lead_part, own_part, flags, false);
+    if (b.force_slow) flags |= FLAG_SLOW;
+    if (r0 < b.n) b.flags[r0] = flags;
+  }
+}
+
+// ---------------------------------------------------------------------------- K1, lane-split helper
+// A wave holds 32 reports. Lanes 0..31 (the S half) run the measurement-share squeeze of report
+// (lane & 31), lanes 32..63 (the J half) the joint_rand_part absorb of the same report: a lane
+// carries ONE Keccak state (<= 128 VGPRs, 4 waves/SIMD, against 2 for the two-sponge fused kernel)
+// and one keccak_p12 instruction stream advances both sponges. After each permutation the S half
+// emits block m (stores, truncation, >= p screen) and forms J's message words of block m (the 16-bit
+// funnel shift of blocks m-1 and m); v_permlane32_swap_b32 hands them to the J half,
+// which XORs them into its state (the S half XORs the swap's zeros). The J half squeezes block 0
+// itself (the same sponge) to build its first message block; after the measurement every lane runs
+// the proof-share squeeze (emitted by the S half) and then the J half finishes the XOF tail.
+
+// lanes 32..63 receive lanes 0..31's v; lanes 0..31 receive 0
+__device__ __forceinline__ uint32_t lower_to_upper(uint32_t v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(0u, v, false, false);
+  return r[0];
+}
+
+template <bool WIDE>
+__global__ __launch_bounds__(64 * K1_WAVES, 4) void xof_lanes_kernel(Cfg c, Bufs b) {
+  const uint32_t lane = threadIdx.x & 63;
+  const bool jh = lane >= 32;
+  const uint64_t gw = (uint64_t)blockIdx.x * K1_WAVES + (threadIdx.x >> 6);  // 32 reports per wave
+  const uint64_t blk = gw >> 1;
+  const uint32_t il = ((uint32_t)gw & 1u) * 32u + (lane & 31u);  // this report's slot in its 64-report block
+  const uint64_t nblk = (b.n + 63) / 64;
+  if (blk >= nblk) return;
+  const uint64_t r0 = blk * 64 + il;
+  const uint64_t r = r0 < b.n ? r0 : b.n - 1;
+  const uint8_t* hs = b.his + (uint64_t)c.his_bytes * r;
+  const uint32_t MB = c.meas_len * 16;
+  const uint32_t ML = 42 + MB;
+  const uint32_t NM = (MB + 167) / 168;
+  const uint32_t b_last = ML / 168;
+
+  uint32_t st[50];
+  {  // squeeze block 0 = XOF(k_meas, DST(1), [1]) in both halves
+    uint32_t kmeas[4];
+    load16(hs, kmeas);
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.dst_id, 1, kmeas);
+    blk_put_byte(m, pos, 1);
+    blk_pad(m, pos + 1);
+    sponge_oneblock(st, m);
+  }
+  uint32_t hdr[11];
+  {
+    uint32_t nonce[4], kblind[4];
+    load16(b.nonces + 16 * r, nonce);
+    load16(hs + 32, kblind);
+    Block h;
+    blk_zero(h);
+    int pos = blk_xof_prefix(h, c.dst_id, 7, kblind);
+    blk_put_byte(h, pos, 1);  // agg_id
+#pragma unroll
+    for (int i = 0; i < 4; i++) blk_put_word(h, pos + 1 + 4 * i, nonce[i]);
+#pragma unroll
+    for (int w = 0; w < 11; w++) hdr[w] = h.w[w];
+  }
+  // aux: the half-specific state carried across permutations, in the SAME registers for both halves.
+  // S half: the truncation word columns T0..T3 (8 words), the element carry (2), the >= p screen
+  // (1) [, WIDE: the low 32-bit truncation (4)]. J half: pv = the raw words 31..41 of the previous
+  // squeezed block (the 16-bit funnel shift of J's message words 0..10 needs them).
+  constexpr int NAUX = WIDE ? 15 : 11;
+  uint32_t aux[NAUX];
+#pragma unroll
+  for (int w = 0; w < NAUX; w++) aux[w] = 0;
+  uint4* const mp = b.meas + il_idx(blk, c.meas_len, 0, il);
+  uint4* const op = b.outs + il_idx(blk, c.out_len, 0, il);
+  // uniform truncation position (output element ti, bit tj) of the next measurement element
+  uint32_t tj = 0, ti = 0;
+  const uint32_t tlen = c.out_is_meas ? 0u : min(c.trunc_len, c.meas_len);
+  // S half (call inside `if (!jh)`): store the elements of squeezed block m, screen them, and add
+  // them into the truncation word columns; an output element is finished every `bits` elements
+  auto s_emit_block = [&](uint32_t m) {
+    TruncW tr;
+#pragma unroll
+    for (int w = 0; w < 4; w++) tr.T[w] = (uint64_t)aux[2 * w] | ((uint64_t)aux[2 * w + 1] << 32);
+    tr.j = tj;
+    tr.i = ti;
+    uint32_t carry0 = aux[8], carry1 = aux[9], gmax = aux[10];
+    f128 trunc_lo = make128(0, 0);
+    if (WIDE) trunc_lo = make128((uint64_t)aux[11] | ((uint64_t)aux[12] << 32), (uint64_t)aux[13] | ((uint64_t)aux[14] << 32));
+    auto emit = [&](uint32_t e, uint4 v) {
+      if (e >= c.meas_len) return;
+      gmax = max(gmax, ge_screen(v));
+      mp[(uint64_t)e * IL] = v;
+      if (e < tlen) {
+        const uint32_t sh = opaque_u32(1u << (WIDE ? (tr.j & 31u) : tr.j));
+        tr.T[0] += (uint64_t)v.x * sh;
+        tr.T[1] += (uint64_t)v.y * sh;
+        tr.T[2] += (uint64_t)v.z * sh;
+        tr.T[3] += (uint64_t)v.w * sh;
+        ++tr.j;
+        if (WIDE && tr.j == 32 && c.bits > 32) {
+          trunc_lo = truncw_value(tr);
+          truncw_zero(tr);
+        }
+        if (tr.j == c.bits) {
+          f128 val = truncw_value(tr);
+          if (WIDE && c.bits > 32) val = add128(trunc_lo, shl32_mod(val));
+          op[(uint64_t)tr.i * IL] = f_to_u4(val);
+          truncw_zero(tr);
+          tr.j = 0;
+          tr.i++;
+        }
+      }
+    };
+    const uint32_t e0 = 21 * (m >> 1);
+    if ((m & 1) == 0) {
+#pragma unroll
+      for (int ci = 0; ci < 10; ci++)
+        emit(e0 + ci, make_uint4(st[4 * ci], st[4 * ci + 1], st[4 * ci + 2], st[4 * ci + 3]));
+      carry0 = st[40];
+      carry1 = st[41];
+    } else {
+      emit(e0 + 10, make_uint4(carry0, carry1, st[0], st[1]));
+#pragma unroll
+      for (int ci = 0; ci < 10; ci++)
+        emit(e0 + 11 + ci, make_uint4(st[2 + 4 * ci], st[3 + 4 * ci], st[4 + 4 * ci], st[5 + 4 * ci]));
+    }
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      aux[2 * w] = (uint32_t)tr.T[w];
+      aux[2 * w + 1] = (uint32_t)(tr.T[w] >> 32);
+    }
+    aux[8] = carry0;
+    aux[9] = carry1;
+    aux[10] = gmax;
+    if (WIDE) {
+      aux[11] = (uint32_t)trunc_lo.lo;
+      aux[12] = (uint32_t)(trunc_lo.lo >> 32);
+      aux[13] = (uint32_t)trunc_lo.hi;
+      aux[14] = (uint32_t)(trunc_lo.hi >> 32);
+    }
+  };
+  // uniform: advance (ti, tj) past the truncated elements of block m
+  auto advance_trunc = [&](uint32_t m) {
+    const uint32_t e0 = 21 * (m >> 1) + ((m & 1) ? 10u : 0u);
+    const uint32_t e1 = e0 + ((m & 1) ? 11u : 10u);
+    const uint32_t cnt = e1 <= tlen ? e1 - e0 : (e0 < tlen ? tlen - e0 : 0u);
+    tj += cnt;
+    while (tj >= c.bits && cnt) {
+      tj -= c.bits;
+      ti++;
+    }
+  };
+  // last absorbed block: message bytes [0, nb) of the block, then TurboSHAKE padding
+  auto pad_last = [&](uint32_t* jw, uint32_t nb) {
+#pragma unroll
+    for (int w = 0; w < 42; w++) {
+      const uint32_t lo_b = 4 * w;
+      if (lo_b >= nb)
+        jw[w] = 0;
+      else if (lo_b + 4 > nb)
+        jw[w] &= (1u << (8 * (nb - lo_b))) - 1u;
+      if ((uint32_t)w == (nb >> 2)) jw[w] ^= 1u << (8 * (nb & 3));
+    }
+    jw[41] ^= 0x80000000u;
+  };
+
+  if (!jh) s_emit_block(0);
+  advance_trunc(0);
+  {
+    // J's message block 0: the 42-byte header || S_0[0, 126) (the J half holds S_0 too)
+    uint32_t jw[42];
+#pragma unroll
+    for (int w = 0; w < 10; w++) jw[w] = hdr[w];
+    jw[10] = (hdr[10] & 0xffffu) | (st[0] << 16);
+#pragma unroll
+    for (int w = 11; w < 42; w++) jw[w] = alignbit(st[w - 10], st[w - 11], 16);
+    if (b_last == 0) pad_last(jw, ML);
+    if (jh) {
+#pragma unroll
+      for (int w = 0; w < 11; w++) aux[w] = st[31 + w];
+#pragma unroll
+      for (int w = 0; w < 42; w++) st[w] = jw[w];
+#pragma unroll
+      for (int w = 42; w < 50; w++) st[w] = 0;
+    }
+  }
+#pragma unroll 1
+  for (uint32_t m = 1; m <= b_last; m++) {
+    keccak_p12(st);  // S: squeeze block m; J: absorb block m - 1
+    const bool have = m < NM;
+    if (have) {
+      if (!jh) s_emit_block(m);
+      advance_trunc(m);
+    }
+    // S -> J: the shifted message words 11..41 of block m (formed by the S half) and the raw words 0 and
+    // 31..41 (J's funnel shift of words 0..10 and its next pv). v_permlane32_swap moves lanes 0..31 of
+    // its second operand into lanes 32..63 of the first; the first operand is any dead register (the
+    // previous swap's clobbered source), so the shifted words cost one swap each.
+    uint32_t jw[42], raw[12];
+    uint32_t dead = st[0];
+    if (have) {
+#pragma unroll
+      for (int w = 11; w < 42; w++) {
+        const auto r2 = __builtin_amdgcn_permlane32_swap(dead, alignbit(st[w - 10], st[w - 11], 16), false, false);
+        jw[w] = r2[0];
+        dead = r2[1];
+      }
+      {
+        const auto r2 = __builtin_amdgcn_permlane32_swap(dead, st[0], false, false);
+        raw[0] = r2[0];
+        dead = r2[1];
+      }
+#pragma unroll
+      for (int k = 0; k < 11; k++) {
+        const auto r2 = __builtin_amdgcn_permlane32_swap(dead, st[31 + k], false, false);
+        raw[1 + k] = r2[0];
+        dead = r2[1];
+      }
+    } else {
+#pragma unroll
+      for (int w = 11; w < 42; w++) jw[w] = 0;
+#pragma unroll
+      for (int k = 0; k < 12; k++) raw[k] = 0;
+    }
+    if (jh) {
+#pragma unroll
+      for (int w = 0; w < 10; w++) jw[w] = alignbit(aux[w + 1], aux[w], 16);
+      jw[10] = alignbit(raw[0], aux[10], 16);
+      if (m == b_last) pad_last(jw, ML - 168 * m);
+#pragma unroll
+      for (int w = 0; w < 42; w++) st[w] ^= jw[w];
+#pragma unroll
+      for (int k = 0; k < 11; k++) aux[k] = raw[1 + k];
+    }
+  }
+  keccak_p12(st);  // J: absorb block b_last
+  uint32_t own_part[4] = {st[0], st[1], st[2], st[3]};
+
+  // proof share: XOF(k_proofs, DST(2), [PROOFS=1, agg_id=1]) in both halves, emitted by the S half
+  uint4* const pp = b.proof + il_idx(blk, c.proof_len, 0, il);
+  {
+    uint32_t kproof[4];
+    load16(hs + 16, kproof);
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.dst_id, 2, kproof);
+    blk_put_byte(m, pos, 1);
+    blk_put_byte(m, pos + 1, 1);
+    blk_pad(m, pos + 2);
+    sponge_oneblock(st, m);
+  }
+  uint32_t carry0 = 0, carry1 = 0, gmax = aux[10];  // S half: the measurement's screen so far
+  auto emit_p = [&](uint32_t e, uint4 v) {
+    if (e >= c.proof_len) return;
+    gmax = max(gmax, ge_screen(v));
+    if (!jh) pp[(uint64_t)e * IL] = v;
+  };
+  const uint32_t NP = (c.proof_len * 16 + 167) / 168;
+#pragma unroll 1
+  for (uint32_t m = 0; m < NP; m++) {
+    if (m > 0) keccak_p12(st);
+    const uint32_t e0 = 21 * (m >> 1);
+    if ((m & 1) == 0) {
+#pragma unroll
+      for (int ci = 0; ci < 10; ci++) emit_p(e0 + ci, make_uint4(st[4 * ci], st[4 * ci + 1], st[4 * ci + 2], st[4 * ci + 3]));
+      carry0 = st[40];
+      carry1 = st[41];
+    } else {
+      emit_p(e0 + 10, make_uint4(carry0, carry1, st[0], st[1]));
+#pragma unroll
+      for (int ci = 0; ci < 10; ci++)
+        emit_p(e0 + 11 + ci, make_uint4(st[2 + 4 * ci], st[3 + 4 * ci], st[4 + 4 * ci], st[5 + 4 * ci]));
+    }
+  }
+  // the S half's screen (measurement + proof elements) goes to the J half, which finishes the report
+  const uint32_t smax = lower_to_upper(gmax);
+  if (jh) {
+    uint32_t flags = smax == 0xFFFFFFFFu ? FLAG_SLOW : 0u;
+    uint32_t nonce[4], part_l[4], lead_part[4];
+    load16(b.nonces + 16 * r, nonce);
+    load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
+    load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
+    flags = xof_tail(c, b, blk, il, r, r0 < b.n, nonce, part_l, lead_part, own_part, flags, false);
     if (b.force_slow) flags |= FLAG_SLOW;
     if (r0 < b.n) b.flags[r0] = flags;
   }
@@ -1038,100 +1339,19 @@ __global__ __launch_bounds__(256) void flp_sum_kernel(Cfg c, Bufs b) {
   if (r0 < b.n) b.verdicts[r0] = (uint8_t)verdict;
 }
 
-// Prio3SumVec / Prio3Histogram: gadget ParallelSum(Mul, chunk), arity 2*chunk.
-//
-// Phase 1 (flp_psum_part_kernel): one wave per (64-report block, slot group). Lanes are
-// reports (the interleaved staging makes every load a coalesced 1 KiB). Group g owns the
-// chunk slots [g*PPW, (g+1)*PPW) -- 2*PPW lazy wire accumulators per lane, small enough to
-// stay in registers at >= 3 waves/SIMD -- and the gadget-polynomial coefficients
-// [g*per, (g+1)*per). It writes four partial sums per report: sum_i Ve_i*Vo_i over its
-// slots, its share of v (sum_m g_m S_m), its share of G(t), and (Histogram) sum of x.
-// Phase 2 (flp_psum_final_kernel): one report per lane; adds the partials, the leader's
-// v and G(t), and decides.
-// PF: calls whose loads are in flight ahead of the one being multiplied (a ring of PF register
-// sets; the HBM latency is several calls' worth of VALU work at 4 waves/SIMD).
-template <int PPW, bool HIST, bool LEADER, int PF = 1, int OCC = 4>
-__global__ __launch_bounds__(64, OCC) void flp_psum_part_kernel(Cfg c, Bufs b) {
+// The part kernels' common end: the calls kf+1..C (the ragged last call, or every call of a padded
+// group) with guarded direct loads, then the wires at t, the leader's verifier share and the gadget
+// polynomial's share of v and G(t) for group g of block blk.
+template <int PPW, bool HIST, bool LEADER>
+__device__ __forceinline__ void psum_part_finish(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t g, uint32_t lane,
+                                                 uint32_t kf, wacc26* ae, wacc26* ao, acc192& sx) {
   const uint32_t NG = c.ngroups;
-  // Workgroup ids are dispatched round-robin over the 8 XCDs; map them so that the NG
-  // groups of one block run back to back on one XCD and share its L2 (coefficients,
-  // leader share).
-  const uint32_t bid = blockIdx.x;
-  const uint32_t xcd = bid & 7u, q = bid >> 3;
-  const uint32_t g = q % NG;
-  const uint64_t blk = (uint64_t)(q / NG) * 8 + xcd;
-  const uint64_t nblk = (b.n + 63) / 64;
-  if (blk >= nblk) return;
-  const uint32_t lane = threadIdx.x;
   const uint64_t r0 = blk * 64 + lane;
   const uint64_t r = r0 < b.n ? r0 : b.n - 1;
   const uint32_t NC = c.ncoef, C = c.calls, chunk = c.chunk, M = c.meas_len, A = 2 * chunk;
   const uint32_t j0 = g * PPW;
-
-  // wire sums over the calls: ae[i] = sum_k d_k x_{k,i} * R, ao[i] = sum_k c_k x_{k,i} * R
-  // (c_k, d_k are stored in Montgomery form), as unreduced 26-bit-limb column sums.
-  wacc26 ae[PPW], ao[PPW];
-  acc192 sx;
-#pragma unroll
-  for (int i = 0; i < PPW; i++) {
-    wacc_zero(ae[i]);
-    wacc_zero(ao[i]);
-  }
-  acc_zero(sx);
   const uint4* coefb = b.coef + il_idx(blk, NC, 0, lane);
   const uint4* measb = b.meas + il_idx(blk, M, 0, lane);
-  // calls whose PPW slots of this group are all real measurement elements run branch-free;
-  // the rest (the ragged last chunk, slots beyond chunk) take the guarded tail loop
-  uint32_t kf = 0;
-  if (j0 + PPW <= chunk && M >= j0 + PPW) kf = min(C, (M - j0 - PPW) / chunk + 1);
-  for (uint32_t k0 = 1; k0 <= kf; k0 += 512) {  // <= 5 * 512 limb products (< 2^52) per column
-    const uint32_t k1 = min(kf, k0 + 511);
-    // software pipeline: the loads of calls k+1 .. k+PF are in flight while call k multiplies
-    uint4 cr[PF], dr[PF], xr[PF][PPW];
-#pragma unroll
-    for (int u = 0; u < PF; u++) {
-      const uint32_t k = k0 + u;
-      if (k <= k1) {
-        cr[u] = coefb[(COEF_K + 2 * (k - 1)) * IL];
-        dr[u] = coefb[(COEF_K + 2 * (k - 1) + 1) * IL];
-#pragma unroll
-        for (int i = 0; i < PPW; i++) xr[u][i] = measb[(uint64_t)((k - 1) * chunk + j0 + i) * IL];
-      }
-    }
-#pragma unroll 1
-    for (uint32_t kb = k0; kb <= k1; kb += PF) {
-#pragma unroll
-      for (int u = 0; u < PF; u++) {
-        const uint32_t k = kb + u;
-        if (k <= k1) {
-          const limbs26 ck = to_limbs26(u4_to_f(cr[u]));
-          const limbs26 dk = to_limbs26(u4_to_f(dr[u]));
-          f128 x[PPW];
-#pragma unroll
-          for (int i = 0; i < PPW; i++) x[i] = u4_to_f(xr[u][i]);
-          const uint32_t kn = k + PF;
-          if (kn <= k1) {
-            cr[u] = coefb[(COEF_K + 2 * (kn - 1)) * IL];
-            dr[u] = coefb[(COEF_K + 2 * (kn - 1) + 1) * IL];
-#pragma unroll
-            for (int i = 0; i < PPW; i++) xr[u][i] = measb[(uint64_t)((kn - 1) * chunk + j0 + i) * IL];
-          }
-#pragma unroll
-          for (int i = 0; i < PPW; i++) {
-            const limbs26 xl = to_limbs26(x[i]);
-            wacc_mac(ae[i], xl, dk);
-            wacc_mac(ao[i], xl, ck);
-            if (HIST) acc_add128(sx, x[i]);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < PPW; i++) {
-      wacc_normalize(ae[i]);
-      wacc_normalize(ao[i]);
-    }
-  }
 #pragma unroll 1
   for (uint32_t k = kf + 1; k <= C; k++) {  // the ragged last call(s), or every call of a padded group
     const limbs26 ck = to_limbs26(u4_to_f(coefb[(COEF_K + 2 * (k - 1)) * IL]));
@@ -1206,6 +1426,228 @@ __global__ __launch_bounds__(64, OCC) void flp_psum_part_kernel(Cfg c, Bufs b) {
   pp[2 * IL] = f_to_u4(gpart);
   if (HIST) pp[3 * IL] = f_to_u4(acc_reduce(sx));
   if (dfail && r0 < b.n) atomicOr(&b.flags[r0], FLAG_DFAIL);
+}
+
+// Prio3SumVec / Prio3Histogram: gadget ParallelSum(Mul, chunk), arity 2*chunk.
+//
+// Phase 1 (flp_psum_part_kernel): one wave per (64-report block, slot group). Lanes are
+// reports (the interleaved staging makes every load a coalesced 1 KiB). Group g owns the
+// chunk slots [g*PPW, (g+1)*PPW) -- 2*PPW lazy wire accumulators per lane, small enough to
+// stay in registers at >= 3 waves/SIMD -- and the gadget-polynomial coefficients
+// [g*per, (g+1)*per). It writes four partial sums per report: sum_i Ve_i*Vo_i over its
+// slots, its share of v (sum_m g_m S_m), its share of G(t), and (Histogram) sum of x.
+// Phase 2 (flp_psum_final_kernel): one report per lane; adds the partials, the leader's
+// v and G(t), and decides.
+// PF: calls whose loads are in flight ahead of the one being multiplied (a ring of PF register
+// sets; the HBM latency is several calls' worth of VALU work at 4 waves/SIMD).
+template <int PPW, bool HIST, bool LEADER, int PF = 1, int OCC = 4>
+__global__ __launch_bounds__(64, OCC) void flp_psum_part_kernel(Cfg c, Bufs b) {
+  const uint32_t NG = c.ngroups;
+  // Workgroup ids are dispatched round-robin over the 8 XCDs; map them so that the NG
+  // groups of one block run back to back on one XCD and share its L2 (coefficients,
+  // leader share).
+  const uint32_t bid = blockIdx.x;
+  const uint32_t xcd = bid & 7u, q = bid >> 3;
+  const uint32_t g = q % NG;
+  const uint64_t blk = (uint64_t)(q / NG) * 8 + xcd;
+  const uint64_t nblk = (b.n + 63) / 64;
+  if (blk >= nblk) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t NC = c.ncoef, C = c.calls, chunk = c.chunk, M = c.meas_len;
+  const uint32_t j0 = g * PPW;
+
+  // wire sums over the calls: ae[i] = sum_k d_k x_{k,i} * R, ao[i] = sum_k c_k x_{k,i} * R
+  // (c_k, d_k are stored in Montgomery form), as unreduced 26-bit-limb column sums.
+  wacc26 ae[PPW], ao[PPW];
+  acc192 sx;
+#pragma unroll
+  for (int i = 0; i < PPW; i++) {
+    wacc_zero(ae[i]);
+    wacc_zero(ao[i]);
+  }
+  acc_zero(sx);
+  const uint4* coefb = b.coef + il_idx(blk, NC, 0, lane);
+  const uint4* measb = b.meas + il_idx(blk, M, 0, lane);
+  // calls whose PPW slots of this group are all real measurement elements run branch-free;
+  // the rest (the ragged last chunk, slots beyond chunk) take the guarded tail loop
+  uint32_t kf = 0;
+  if (j0 + PPW <= chunk && M >= j0 + PPW) kf = min(C, (M - j0 - PPW) / chunk + 1);
+  for (uint32_t k0 = 1; k0 <= kf; k0 += 512) {  // <= 5 * 512 limb products (< 2^52) per column
+    const uint32_t k1 = min(kf, k0 + 511);
+    // software pipeline: the loads of calls k+1 .. k+PF are in flight while call k multiplies
+    uint4 cr[PF], dr[PF], xr[PF][PPW];
+#pragma unroll
+    for (int u = 0; u < PF; u++) {
+      const uint32_t k = k0 + u;
+      if (k <= k1) {
+        cr[u] = coefb[(COEF_K + 2 * (k - 1)) * IL];
+        dr[u] = coefb[(COEF_K + 2 * (k - 1) + 1) * IL];
+#pragma unroll
+        for (int i = 0; i < PPW; i++) xr[u][i] = measb[(uint64_t)((k - 1) * chunk + j0 + i) * IL];
+      }
+    }
+#pragma unroll 1
+    for (uint32_t kb = k0; kb <= k1; kb += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; u++) {
+        const uint32_t k = kb + u;
+        if (k <= k1) {
+          const limbs26 ck = to_limbs26(u4_to_f(cr[u]));
+          const limbs26 dk = to_limbs26(u4_to_f(dr[u]));
+          f128 x[PPW];
+#pragma unroll
+          for (int i = 0; i < PPW; i++) x[i] = u4_to_f(xr[u][i]);
+          const uint32_t kn = k + PF;
+          if (kn <= k1) {
+            cr[u] = coefb[(COEF_K + 2 * (kn - 1)) * IL];
+            dr[u] = coefb[(COEF_K + 2 * (kn - 1) + 1) * IL];
+#pragma unroll
+            for (int i = 0; i < PPW; i++) xr[u][i] = measb[(uint64_t)((kn - 1) * chunk + j0 + i) * IL];
+          }
+#pragma unroll
+          for (int i = 0; i < PPW; i++) {
+            const limbs26 xl = to_limbs26(x[i]);
+            wacc_mac(ae[i], xl, dk);
+            wacc_mac(ao[i], xl, ck);
+            if (HIST) acc_add128(sx, x[i]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PPW; i++) {
+      wacc_normalize(ae[i]);
+      wacc_normalize(ao[i]);
+    }
+  }
+  psum_part_finish<PPW, HIST, LEADER>(c, b, blk, g, lane, kf, ae, ao, sx);
+}
+
+// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt left unconstrained)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt(0x3f70 | (N & 15) | ((N >> 4) << 14));
+}
+__device__ __forceinline__ void glds16(const uint4* src, uint4* lds_row) {
+  __builtin_amdgcn_global_load_lds((const void*)src, (void*)lds_row, 16, 0, 0);
+}
+
+// K3 with an LDS-DMA ring (k3_pf = 20 / 21: D = 3 / 4). A workgroup is K3W waves = K3W consecutive slot
+// groups of one 64-report block. Per call k, wave 0 streams c_k and wave 1 d_k (one
+// global_load_lds_dwordx4 each: 1 KiB, the block's 64 reports) into ring slot (k-1) % D, and every live
+// wave its own PPW measurement elements; the coefficients are fetched once per K3W groups instead of
+// once per group, and D-1 calls stay in flight without holding VGPRs. One s_barrier per call: after it,
+// every wave's loads of call k have landed (each waited for its own with vmcnt) and every wave has
+// finished reading call k-1's slot, which the next issue overwrites. Calls beyond floor(M / chunk)
+// (the ragged last one) go through psum_part_finish's guarded loads.
+constexpr uint32_t K3W = 4;
+// LDS address of a __shared__ object
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) uint8_t*)p;
+}
+// Four 16-byte LDS reads and one wait, in asm: the compiler's LDS-DMA wait tracking cannot tell which
+// ring slot a read touches and would otherwise drain every outstanding global_load_lds (vmcnt(0))
+// before each read, serialising the ring; the explicit wait_vmcnt + s_barrier order the reads here.
+__device__ __forceinline__ void lds_read4(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint4& v0, uint4& v1,
+                                          uint4& v2, uint4& v3) {
+  asm volatile(
+      "ds_read_b128 %0, %4\n\t"
+      "ds_read_b128 %1, %5\n\t"
+      "ds_read_b128 %2, %6\n\t"
+      "ds_read_b128 %3, %7\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3)
+      : "v"(a0), "v"(a1), "v"(a2), "v"(a3)
+      : "memory");
+}
+template <int PPW, bool HIST, bool LEADER, int D>
+__global__ __launch_bounds__(64 * K3W, 4) void flp_psum_part_glds_kernel(Cfg c, Bufs b) {
+  static_assert(PPW == 2, "lds_read4 reads c, d and two measurement rows");
+  constexpr int ROWS = 2 + K3W * PPW;  // c_k, d_k, then x[wave][i]
+  __shared__ uint4 ring[D][ROWS][64];
+  const uint32_t NG = c.ngroups, NW = (NG + K3W - 1) / K3W;
+  const uint32_t bid = blockIdx.x, xcd = bid & 7u, q = bid >> 3;
+  const uint32_t wg = q % NW;
+  const uint64_t blk = (uint64_t)(q / NW) * 8 + xcd;
+  const uint64_t nblk = (b.n + 63) / 64;
+  if (blk >= nblk) return;  // uniform over the workgroup
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t g = wg * K3W + wave;
+  const uint32_t C = c.calls, chunk = c.chunk, M = c.meas_len;
+  const uint32_t j0 = g * PPW;
+  const bool full = g < NG && j0 + PPW <= chunk;  // this wave's PPW slots are all real
+  const uint4* coefb = b.coef + il_idx(blk, c.ncoef, 0, lane);
+  const uint4* measb = b.meas + il_idx(blk, M, 0, lane);
+  // calls whose every slot is a measurement element; a wave whose group is padded or absent runs the
+  // loop for the barriers (and, waves 0/1, the coefficient loads) but computes in the tail only
+  const uint32_t kfw = C < M / chunk ? C : M / chunk;
+  const uint32_t kf = full ? kfw : 0;
+
+  wacc26 ae[PPW], ao[PPW];
+  acc192 sx;
+#pragma unroll
+  for (int i = 0; i < PPW; i++) {
+    wacc_zero(ae[i]);
+    wacc_zero(ao[i]);
+  }
+  acc_zero(sx);
+  // loads of call k into ring slot (k - 1) % D
+  auto issue = [&](uint32_t k) {
+    const uint32_t sl = (k - 1) % D;
+    if (wave < 2) glds16(coefb + (uint64_t)(COEF_K + 2 * (k - 1) + wave) * IL, &ring[sl][wave][0]);
+    if (full) {
+#pragma unroll
+      for (int i = 0; i < PPW; i++)
+        glds16(measb + (uint64_t)((k - 1) * chunk + j0 + i) * IL, &ring[sl][2 + wave * PPW + i][0]);
+    }
+  };
+  // loads a wave issues per call: 1 (coefficient, waves 0/1) + PPW (measurement, full groups)
+  auto wait_call = [&](bool tail) {
+    if (tail) {
+      wait_vmcnt<0>();
+    } else if (wave < 2 && full) {
+      wait_vmcnt<(D - 2) * (PPW + 1)>();
+    } else if (full) {
+      wait_vmcnt<(D - 2) * PPW>();
+    } else if (wave < 2) {
+      wait_vmcnt<D - 2>();
+    }
+  };
+  for (uint32_t k = 1; k < D && k <= kfw; k++) issue(k);
+  const uint32_t ring_base = lds_addr(&ring[0][0][lane]);
+  constexpr uint32_t SLOT_BYTES = ROWS * 64 * 16, ROW_BYTES = 64 * 16;
+#pragma unroll 1
+  for (uint32_t k = 1; k <= kfw; k++) {
+    wait_call(k + D - 2 > kfw);  // near the end fewer calls are in flight: wait for all
+    __builtin_amdgcn_s_barrier();
+    if (k + D - 1 <= kfw) issue(k + D - 1);
+    if (full) {
+      const uint32_t a = ring_base + ((k - 1) % D) * SLOT_BYTES;
+      uint4 cv, dv, xv[PPW];
+      lds_read4(a, a + ROW_BYTES, a + (2 + wave * PPW) * ROW_BYTES, a + (3 + wave * PPW) * ROW_BYTES, cv, dv, xv[0],
+                xv[1]);
+      const limbs26 ck = to_limbs26(u4_to_f(cv));
+      const limbs26 dk = to_limbs26(u4_to_f(dv));
+#pragma unroll
+      for (int i = 0; i < PPW; i++) {
+        const f128 x = u4_to_f(xv[i]);
+        const limbs26 xl = to_limbs26(x);
+        wacc_mac(ae[i], xl, dk);
+        wacc_mac(ao[i], xl, ck);
+        if (HIST) acc_add128(sx, x);
+      }
+      if ((k & 511u) == 0) {  // <= 5 * 512 limb products (< 2^52) per column
+#pragma unroll
+        for (int i = 0; i < PPW; i++) {
+          wacc_normalize(ae[i]);
+          wacc_normalize(ao[i]);
+        }
+      }
+    }
+  }
+  if (g >= NG) return;
+  psum_part_finish<PPW, HIST, LEADER>(c, b, blk, g, lane, kf, ae, ao, sx);
 }
 
 template <bool HIST, bool LEADER>
@@ -1886,6 +2328,14 @@ hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
     hipLaunchKernelGGL((xof_kernel<K1_LEADER, true>), grid, block, 0, s, c, b);
   else if (b.leader)
     hipLaunchKernelGGL((xof_kernel<K1_LEADER, false>), grid, block, 0, s, c, b);
+  else if (b.k1_split == 3) {  // lane-split: 32 reports per wave
+    const dim3 g2((2 * nb + K1_WAVES - 1) / K1_WAVES);
+    if (wide)
+      hipLaunchKernelGGL((xof_lanes_kernel<true>), g2, block, 0, s, c, b);
+    else
+      hipLaunchKernelGGL((xof_lanes_kernel<false>), g2, block, 0, s, c, b);
+  } else if (b.k1_split == 4 && !wide)
+    hipLaunchKernelGGL((xof_kernel<K1_SEQ, false>), grid, block, 0, s, c, b);
   else if (b.k1_split && wide) {
     hipLaunchKernelGGL((xof_kernel<K1_SQUEEZE, true>), grid, block, 0, s, c, b);
     hipLaunchKernelGGL((xof_kernel<K1_ABSORB, true>), grid, block, 0, s, c, b);
@@ -1905,16 +2355,25 @@ hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
 // workgroups per CU (from the kernel's register/LDS footprint) x 64 reports per wave. K1 waves
 // all run the same length, so a launch runs in ceil(reports / this) equal "rounds"; the
 // engine sizes its launches in whole rounds so only the last launch has a partial one.
-uint64_t k1_round_reports(const Cfg& c, int device) {
+uint64_t k1_round_reports(const Cfg& c, int device, uint32_t k1_split) {
   if (c.algo == ALGO_SUMVEC_F64_MULTIPROOF) return mp_k1_round_reports(device);
   int cus = 0, wgs = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return 0;
   const uint32_t threads = c.algo == ALGO_COUNT ? 256u : 64u * K1_WAVES;
-  hipError_t st = c.algo == ALGO_COUNT
-                      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, count_kernel<false>, threads, 0)
-                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_kernel<K1_FUSED>, threads, 0);
+  hipError_t st;
+  uint32_t per_wg = threads;  // reports per workgroup
+  if (c.algo == ALGO_COUNT) {
+    st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, count_kernel<false>, threads, 0);
+  } else if (k1_split == 3) {
+    st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_lanes_kernel<false>, threads, 0);
+    per_wg = threads / 2;
+  } else if (k1_split == 4) {
+    st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_kernel<K1_SEQ>, threads, 0);
+  } else {
+    st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_kernel<K1_FUSED>, threads, 0);
+  }
   if (st != hipSuccess || wgs <= 0) return 0;
-  return (uint64_t)cus * (uint64_t)wgs * threads;
+  return (uint64_t)cus * (uint64_t)wgs * per_wg;
 }
 hipError_t launch_leader_finish(const Cfg& c, const Bufs& b, const uint8_t* prep_msgs, const uint8_t* peer,
                                 hipStream_t s) {
@@ -1949,9 +2408,19 @@ int psum_ppw(uint32_t chunk) {
   return best;
 }
 
-// k3_pf: calls of loads in flight, + 10 for the 3-waves/SIMD (168-VGPR) build
+// k3_pf: calls of loads in flight, + 10 for the 3-waves/SIMD (168-VGPR) build; 20 / 21: the LDS-DMA ring
 template <int PPW, bool HIST, bool LEADER>
 static void launch_psum_part(const Cfg& c, const Bufs& b, hipStream_t s, uint32_t grid) {
+  if constexpr (PPW == 2) {
+    if (b.k3_pf == 20 || b.k3_pf == 21) {  // LDS-DMA ring, K3W groups per workgroup
+      const uint32_t g2 = grid / c.ngroups * ((c.ngroups + K3W - 1) / K3W);
+      if (b.k3_pf == 20)
+        hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 3>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
+      else
+        hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
+      return;
+    }
+  }
   if (b.k3_pf == 2)
     hipLaunchKernelGGL((flp_psum_part_kernel<PPW, HIST, LEADER, 2>), dim3(grid), dim3(64), 0, s, c, b);
   else if (b.k3_pf == 12)
