@@ -87,7 +87,7 @@ struct jx_engine {
   uint64_t launches[NST] = {0, 0, 0, 0};
   uint32_t force_slow = 0;
   uint32_t k1_split = 0;  // helper K1 as squeeze-only + absorb-only launches (JX_K1_SPLIT, debug option 3)
-  uint32_t k3_pf = 1;     // K3 load pipeline variant (JX_K3_PF, debug option 4)
+  uint32_t k3_pf = 21;    // K3 load pipeline variant (JX_K3_PF, debug option 4): the depth-4 LDS-DMA ring
   std::string err;
 };
 
@@ -562,6 +562,11 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
   b.consts = e->d_consts;
   b.force_slow = e->force_slow;
   b.k1_split = e->k1_split;
+  // A helper launch that would give the fused two-sponge K1 less than one wave per SIMD is bound by
+  // the per-report sponge latency, not by issue: the lane-split kernel runs it in twice the waves
+  // (FixedPointBoundedL2VecSum 16 x 10000, 24,576 reports: 153 -> 92 ms on MI355X).
+  const bool wide = c.bits > 32 && (c.algo == ALGO_SUM || c.algo == ALGO_SUMVEC);
+  if (e->k1_split == 0 && !leader && !wide && e->round_reports && 2 * n < e->round_reports) b.k1_split = 3;
   b.k3_pf = e->k3_pf;
   hipEvent_t ev = nullptr;
   if (c.algo == ALGO_COUNT) {
@@ -812,7 +817,7 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
   const uint64_t per = per_report_bytes(e->cfg);
   if (const char* env = getenv("JX_K1_SPLIT")) {
     const int v = atoi(env);
-    if (v >= 0 && v <= 4) e->k1_split = (uint32_t)v;
+    if (v >= 0 && v <= 5) e->k1_split = (uint32_t)v;
   }
   e->round_reports = k1_round_reports(e->cfg, device, e->k1_split);
   uint64_t budget = 48ull << 30;
@@ -839,7 +844,7 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
   e->default_chunk = chunk;
   if (const char* env = getenv("JX_K3_PF")) {
     const int v = atoi(env);
-    if (v == 1 || v == 2 || v == 12 || v == 13 || v == 20 || v == 21) e->k3_pf = (uint32_t)v;
+    if (v == 1 || v == 2 || v == 12 || v == 13 || (v >= 20 && v <= 23)) e->k3_pf = (uint32_t)v;  // 22/23: timing probes
   }
   *out = e;
   return JX_OK;
@@ -1306,9 +1311,11 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
     e->force_slow = value != 0;
     return JX_OK;
   }
-  if (option == 3) {  // K1 variant: 0 fused two-sponge kernel, 1 squeeze-only + absorb-only launches
-    if (value < 0 || value > 4) return JX_E_INVALID;
-    e->k1_split = (uint32_t)value;  // 2: the absorb-only launch at 2 waves/SIMD; 3: lane-split; 4: sequential S, J
+  if (option == 3) {  // helper K1 variant
+    if (value < 0 || value > 5) return JX_E_INVALID;
+    // 0: automatic (fused; lane-split below one fused wave per SIMD), 1 / 2: squeeze-only + absorb-only
+    // launches (absorb at 3 / 2 waves/SIMD), 3: lane-split, 4: sequential S, J permutations, 5: fused
+    e->k1_split = (uint32_t)value;
     return JX_OK;
   }
   if (option == 4) {  // K3 load pipeline: 1 or 2 calls ahead; 12 / 13 = 2 / 3 ahead at 3 waves/SIMD; 20 / 21 LDS-DMA ring

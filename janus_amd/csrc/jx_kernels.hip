@@ -1108,6 +1108,188 @@ __global__ __launch_bounds__(64 * K1_WAVES, 4) void xof_lanes_kernel(Cfg c, Bufs
   }
 }
 
+// ---------------------------------------------------------------------------- K1, leader role
+// leader_initialized (aggregation_job_driver.rs:345): prepare_init with agg_id 0 on the explicit leader
+// input share [meas || proofs || k_blind], one report per lane. Only the joint_rand_part absorb runs
+// through Keccak; block m+1 of the share (21 8-byte loads per lane) is fetched into the block buffer
+// while J permutes block m, so the loads land under the permutation. Elements >= p fail the report
+// (decode). One buffer, one sponge: no spills even when a launch holds a third of a wave per SIMD
+// (FixedPointBoundedL2VecSum at length 10000), where every scratch access would be exposed.
+template <bool WIDE>
+__global__ __launch_bounds__(64 * K1_WAVES) void xof_leader_kernel(Cfg c, Bufs b) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t blk = (uint64_t)blockIdx.x * K1_WAVES + (threadIdx.x >> 6);
+  const uint64_t nblk = (b.n + 63) / 64;
+  if (blk >= nblk) return;
+  const uint64_t r0 = blk * 64 + lane;
+  const uint64_t r = r0 < b.n ? r0 : b.n - 1;
+  const uint8_t* ls = b.lis + (uint64_t)c.lis_bytes * r;
+  const uint32_t MB = c.meas_len * 16;
+  const uint32_t ML = 42 + MB;
+  const uint32_t NM = (MB + 167) / 168;
+  const uint32_t b_last = ML / 168;
+
+  uint32_t buf[42];  // block m of the explicit measurement share (words past the share read as 0)
+  auto load_block = [&](uint32_t m) {
+#pragma unroll
+    for (int q = 0; q < 21; q++) {
+      const uint32_t off = 168 * m + 8 * q;
+      uint2 v = make_uint2(0, 0);
+      if (off < MB) v = *reinterpret_cast<const uint2*>(ls + off);
+      buf[2 * q] = v.x;
+      buf[2 * q + 1] = v.y;
+    }
+  };
+  uint32_t carry0 = 0, carry1 = 0, unused_screen = 0;
+  bool bad = false;
+  TruncW tr;
+  truncw_zero(tr);
+  tr.j = 0;
+  tr.i = 0;
+  f128 trunc_lo = make128(0, 0);
+  uint4* const mp = b.meas + il_idx(blk, c.meas_len, 0, lane);
+  uint4* const op = b.outs + il_idx(blk, c.out_len, 0, lane);
+  auto emit = [&](uint32_t e, uint4 v) {
+    if (e < c.meas_len) bad |= ge_exact(v);
+    emit_meas<WIDE>(c, mp, op, e, v, unused_screen, tr, trunc_lo);
+  };
+  auto emit_block = [&](uint32_t m) {
+    const uint32_t e0 = 21 * (m >> 1);
+    if ((m & 1) == 0) {
+#pragma unroll
+      for (int ci = 0; ci < 10; ci++)
+        emit(e0 + ci, make_uint4(buf[4 * ci], buf[4 * ci + 1], buf[4 * ci + 2], buf[4 * ci + 3]));
+      carry0 = buf[40];
+      carry1 = buf[41];
+    } else {
+      emit(e0 + 10, make_uint4(carry0, carry1, buf[0], buf[1]));
+#pragma unroll
+      for (int ci = 0; ci < 10; ci++)
+        emit(e0 + 11 + ci, make_uint4(buf[2 + 4 * ci], buf[3 + 4 * ci], buf[4 + 4 * ci], buf[5 + 4 * ci]));
+    }
+  };
+  uint32_t hdr[11];
+  {
+    uint32_t nonce[4], kblind[4];
+    load16(b.nonces + 16 * r, nonce);
+    load16(ls + MB + 16 * c.proof_len, kblind);
+    Block h;
+    blk_zero(h);
+    int pos = blk_xof_prefix(h, c.dst_id, 7, kblind);
+    blk_put_byte(h, pos, 0);  // agg_id
+#pragma unroll
+    for (int i = 0; i < 4; i++) blk_put_word(h, pos + 1 + 4 * i, nonce[i]);
+#pragma unroll
+    for (int w = 0; w < 11; w++) hdr[w] = h.w[w];
+  }
+  uint32_t J[50], prev[11];
+  // J's message words of block m from prev (block m-1) and buf (block m, if present); block 0 starts
+  // with the header
+  auto message = [&](uint32_t m, bool have, uint32_t* jw) {
+    const uint32_t s0 = have ? buf[0] : 0u;
+    if (m == 0) {
+#pragma unroll
+      for (int w = 0; w < 10; w++) jw[w] = hdr[w];
+      jw[10] = (hdr[10] & 0xffffu) | (s0 << 16);
+    } else {
+#pragma unroll
+      for (int w = 0; w < 10; w++) jw[w] = alignbit(prev[w + 1], prev[w], 16);
+      jw[10] = alignbit(s0, prev[10], 16);
+    }
+#pragma unroll
+    for (int w = 11; w < 42; w++) jw[w] = have ? alignbit(buf[w - 10], buf[w - 11], 16) : 0u;
+  };
+  load_block(0);
+  emit_block(0);
+  if (b_last == 0) {
+    uint32_t jw[42];
+    message(0, true, jw);
+    const uint32_t nb = ML;
+#pragma unroll
+    for (int w = 0; w < 42; w++) {
+      const uint32_t lo_b = 4 * w;
+      if (lo_b >= nb)
+        jw[w] = 0;
+      else if (lo_b + 4 > nb)
+        jw[w] &= (1u << (8 * (nb - lo_b))) - 1u;
+      if ((uint32_t)w == (nb >> 2)) jw[w] ^= 1u << (8 * (nb & 3));
+    }
+    jw[41] ^= 0x80000000u;
+#pragma unroll
+    for (int w = 0; w < 42; w++) J[w] = jw[w];
+#pragma unroll
+    for (int w = 42; w < 50; w++) J[w] = 0;
+    keccak_p12(J);
+  } else {
+    {
+      uint32_t jw[42];
+      message(0, true, jw);
+#pragma unroll
+      for (int w = 0; w < 42; w++) J[w] = jw[w];
+#pragma unroll
+      for (int w = 42; w < 50; w++) J[w] = 0;
+#pragma unroll
+      for (int w = 0; w < 11; w++) prev[w] = buf[31 + w];
+    }
+    if (1 < NM) load_block(1);
+    keccak_p12(J);
+#pragma unroll 1
+    for (uint32_t m = 1; m < b_last; m++) {  // m < b_last <= NM: block m holds measurement bytes
+      emit_block(m);
+      uint32_t jw[42];
+      message(m, true, jw);
+#pragma unroll
+      for (int w = 0; w < 42; w++) J[w] ^= jw[w];
+#pragma unroll
+      for (int w = 0; w < 11; w++) prev[w] = buf[31 + w];
+      if (m + 1 < NM) load_block(m + 1);
+      keccak_p12(J);
+    }
+    const bool have = b_last < NM;
+    if (have) emit_block(b_last);
+    uint32_t jw[42];
+    message(b_last, have, jw);
+    const uint32_t nb = ML - 168 * b_last;
+#pragma unroll
+    for (int w = 0; w < 42; w++) {
+      const uint32_t lo_b = 4 * w;
+      if (lo_b >= nb)
+        jw[w] = 0;
+      else if (lo_b + 4 > nb)
+        jw[w] &= (1u << (8 * (nb - lo_b))) - 1u;
+      if ((uint32_t)w == (nb >> 2)) jw[w] ^= 1u << (8 * (nb & 3));
+    }
+    jw[41] ^= 0x80000000u;
+#pragma unroll
+    for (int w = 0; w < 42; w++) J[w] ^= jw[w];
+    keccak_p12(J);
+  }
+  uint32_t own_part[4] = {J[0], J[1], J[2], J[3]};
+  // proof share: explicit, decoded (>= p fails)
+  uint4* const pp = b.proof + il_idx(blk, c.proof_len, 0, lane);
+  const uint4* src = reinterpret_cast<const uint4*>(ls + MB);
+#pragma unroll 1
+  for (uint32_t e = 0; e < c.proof_len; e++) {
+    const uint4 v = src[e];
+    bad |= ge_exact(v);
+    pp[(uint64_t)e * IL] = v;
+  }
+  uint32_t nonce[4], part_h[4];
+  load16(b.nonces + 16 * r, nonce);
+  // corrected seed = XOF(0, DST(6), own part || helper's part from the public share): the leader's
+  // prepare state (written to msgs), and own part goes out in the prep share
+  load16(b.ps + (uint64_t)c.ps_bytes * r + 16, part_h);
+  uint32_t flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, own_part, own_part, part_h, 0u, false);
+  if (flags & FLAG_SLOW)  // a rejected joint/query randomness sample (~2^-120): redo exactly
+    flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, own_part, own_part, part_h, flags & ~FLAG_SLOW, true);
+  if (bad) flags |= FLAG_INPUT_FAIL;
+  if (r0 < b.n) {
+    *reinterpret_cast<uint4*>(b.lps_out + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16) =
+        make_uint4(own_part[0], own_part[1], own_part[2], own_part[3]);
+    b.flags[r0] = flags;
+  }
+}
+
 // ---------------------------------------------------------------------------- K1': slow XOF path
 // General byte-stream implementation with rejection sampling at any position. Runs only
 // for reports flagged FLAG_SLOW (a sampled chunk was >= p; ~1e-14 per SumVec report).
@@ -1561,7 +1743,9 @@ __device__ __forceinline__ void lds_read4(uint32_t a0, uint32_t a1, uint32_t a2,
       : "v"(a0), "v"(a1), "v"(a2), "v"(a3)
       : "memory");
 }
-template <int PPW, bool HIST, bool LEADER, int D>
+// PROBE (timing experiments only, results are wrong): 1 = loads and barriers without the limb
+// products, 2 = limb products on whatever the ring holds, without loads
+template <int PPW, bool HIST, bool LEADER, int D, int PROBE = 0>
 __global__ __launch_bounds__(64 * K3W, 4) void flp_psum_part_glds_kernel(Cfg c, Bufs b) {
   static_assert(PPW == 2, "lds_read4 reads c, d and two measurement rows");
   constexpr int ROWS = 2 + K3W * PPW;  // c_k, d_k, then x[wave][i]
@@ -1594,6 +1778,7 @@ __global__ __launch_bounds__(64 * K3W, 4) void flp_psum_part_glds_kernel(Cfg c, 
   acc_zero(sx);
   // loads of call k into ring slot (k - 1) % D
   auto issue = [&](uint32_t k) {
+    if (PROBE == 2) return;
     const uint32_t sl = (k - 1) % D;
     if (wave < 2) glds16(coefb + (uint64_t)(COEF_K + 2 * (k - 1) + wave) * IL, &ring[sl][wave][0]);
     if (full) {
@@ -1622,7 +1807,7 @@ __global__ __launch_bounds__(64 * K3W, 4) void flp_psum_part_glds_kernel(Cfg c, 
     wait_call(k + D - 2 > kfw);  // near the end fewer calls are in flight: wait for all
     __builtin_amdgcn_s_barrier();
     if (k + D - 1 <= kfw) issue(k + D - 1);
-    if (full) {
+    if (full && PROBE != 1) {
       const uint32_t a = ring_base + ((k - 1) % D) * SLOT_BYTES;
       uint4 cv, dv, xv[PPW];
       lds_read4(a, a + ROW_BYTES, a + (2 + wave * PPW) * ROW_BYTES, a + (3 + wave * PPW) * ROW_BYTES, cv, dv, xv[0],
@@ -2325,10 +2510,15 @@ hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
   const dim3 grid((nb + K1_WAVES - 1) / K1_WAVES), block(64 * K1_WAVES);
   const bool wide = c.bits > 32 && (c.algo == ALGO_SUM || c.algo == ALGO_SUMVEC);
   if (b.leader && wide)
-    hipLaunchKernelGGL((xof_kernel<K1_LEADER, true>), grid, block, 0, s, c, b);
+    hipLaunchKernelGGL((xof_leader_kernel<true>), grid, block, 0, s, c, b);
   else if (b.leader)
-    hipLaunchKernelGGL((xof_kernel<K1_LEADER, false>), grid, block, 0, s, c, b);
-  else if (b.k1_split == 3) {  // lane-split: 32 reports per wave
+    hipLaunchKernelGGL((xof_leader_kernel<false>), grid, block, 0, s, c, b);
+  else if (b.k1_split == 5) {  // the fused kernel, forced (tests; the engine picks lanes for small launches)
+    if (wide)
+      hipLaunchKernelGGL((xof_kernel<K1_FUSED, true>), grid, block, 0, s, c, b);
+    else
+      hipLaunchKernelGGL((xof_kernel<K1_FUSED, false>), grid, block, 0, s, c, b);
+  } else if (b.k1_split == 3) {  // lane-split: 32 reports per wave
     const dim3 g2((2 * nb + K1_WAVES - 1) / K1_WAVES);
     if (wide)
       hipLaunchKernelGGL((xof_lanes_kernel<true>), g2, block, 0, s, c, b);
@@ -2418,6 +2608,14 @@ static void launch_psum_part(const Cfg& c, const Bufs& b, hipStream_t s, uint32_
         hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 3>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
       else
         hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
+      return;
+    }
+    if (b.k3_pf == 22 || b.k3_pf == 23) {  // timing probes (wrong results): loads only / products only
+      const uint32_t g2 = grid / c.ngroups * ((c.ngroups + K3W - 1) / K3W);
+      if (b.k3_pf == 22)
+        hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4, 1>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
+      else
+        hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4, 2>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
       return;
     }
   }

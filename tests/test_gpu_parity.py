@@ -262,13 +262,15 @@ def test_shard_records_device_merge(name):
         e.close()
 
 
-@pytest.mark.parametrize("split", [1, 2, 3, 4], ids=["absorb_occ3", "absorb_occ2", "lanes", "seq_occ3"])
+@pytest.mark.parametrize("split", [1, 2, 3, 4, 5], ids=["absorb_occ3", "absorb_occ2", "lanes", "seq_occ3", "fused"])
 @pytest.mark.parametrize("name", ["sumvec_8x1000_88", "histogram_256_16", "sum64", "sumvec_small", "sumvec_64x20_9",
                                   "sum5", "sum32"])
 def test_k1_split_variants(name, split):
     """The helper K1 variants == the oracle, fast and slow path: the split launches (squeeze-only, then
-    absorb-only), the lane-split kernel (S and J sponges in the two halves of a wave) and the fused kernel
-    with sequential permutations. sum5 has its whole joint_rand_part message in one block."""
+    absorb-only), the lane-split kernel (S and J sponges in the two halves of a wave; the engine's choice
+    for launches under one fused wave per SIMD, i.e. every small test batch), the fused kernel with
+    sequential permutations, and the fused two-sponge kernel itself (the engine's choice for large
+    launches, forced here). sum5 has its whole joint_rand_part message in one block."""
     vdaf = CASES[name]
     vk = bytes(range(60, 76))
     orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
@@ -289,7 +291,7 @@ def test_k1_split_variants(name, split):
         np.testing.assert_array_equal(res.verdicts, want["verdicts"])
 
 
-@pytest.mark.parametrize("pf", [2, 12, 13, 20, 21], ids=["pf2_occ4", "pf2_occ3", "pf3_occ3", "glds3", "glds4"])
+@pytest.mark.parametrize("pf", [1, 2, 12, 13, 20, 21], ids=["pf1_occ4", "pf2_occ4", "pf2_occ3", "pf3_occ3", "glds3", "glds4"])
 @pytest.mark.parametrize("name", ["sumvec_8x1000_88", "histogram_256_16", "sumvec_64x20_9", "sumvec_small"])
 def test_k3_pipeline_variants(name, pf):
     """The deeper-pipelined ParallelSum FLP part kernels (register rings; the LDS-DMA ring of depth 3 / 4
