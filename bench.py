@@ -45,6 +45,13 @@ HBM_PEAK_GBPS = 8000.0
 #      2.4 GHz, 1 op per lane-cycle), which undercounts gfx950's 4 SIMD-32 per CU by 2x; here the
 #      peak is the 78.6 T int32 lane-op rate for both counts.
 OPS_PER_PERM = 190 * 12
+# Instruction-mix ceiling of the Keccak round: gfx950 does not issue every instruction at the flat
+# 78.6 T rate. Measured rates at 8 waves/SIMD on independent chains (profiles/r01_microbench_valu.jsonl,
+# tools/microbench_valu.hip), as fractions of 78.6 T: v_bitop3_b32 0.70, v_alignbit_b32 0.465;
+# v_xor_b32 is taken at 1.0 (its microbench reads 1.13: the compiler fuses xor pairs into v_bitop3).
+# A round (62 xor + 70 bitop3 + 58 alignbit) therefore issues at most 190 / (62 + 70/0.70 + 58/0.465)
+# = 0.663 of 78.6 T = 52.1 T, at the nominal 2.4 GHz; the PMC clock under K1 is lower (power).
+KECCAK_ROUND_MIX = {"v_xor_b32": (62, 1.0), "v_bitop3_b32": (70, 0.70), "v_alignbit_b32": (58, 0.465)}
 OPS_PER_MONT = 56
 OPS_PER_FMUL = 16
 ALG_OPS_PER_PERM = 3720
@@ -97,6 +104,23 @@ def sumvec_work(bits, length, chunk):
                 alg_ops_k3=(fmul_k3 + mont_k3) * ALG_OPS_PER_FMUL,
                 hbm_k1=16 * (M + proof_len + 6 + 2 * calls) + 16 * length + 16 + 48 + 32 + 16,
                 hbm_k3=16 * (M + proof_len + 6 + 2 * calls) + 16 * (A + 3) + 1)
+
+
+def keccak_mix_ceiling_tops() -> float:
+    n = sum(c for c, _ in KECCAK_ROUND_MIX.values())
+    return VALU_PEAK_TOPS * n / sum(c / r for c, r in KECCAK_ROUND_MIX.values())
+
+
+def pmc_clock(kernel: str):
+    """Shader clock under `kernel` from the committed PMC summary (GRBM_GUI_ACTIVE / 8 XCDs / duration),
+    or None when the summary was taken on other kernel sources."""
+    try:
+        d = json.load(open(PMC_SUMMARY))
+    except (OSError, ValueError):
+        return None
+    if d.get("workload", {}).get("sources_digest") != sources_digest():
+        return None
+    return d.get("kernels", {}).get(kernel, {}).get("clock_GHz")
 
 
 def pmc_traffic(kernel: str, reports_per_launch: float):
@@ -330,6 +354,8 @@ def main():
     traffic, traffic_src, traffic_note = pmc_traffic("jx::xof_kernel<0, false>" if k1_dom else
                                                      "jx::flp_psum_part_kernel<2, false, false>", chunk_reports)
     alg_bytes = (work["hbm_k1"] if k1_dom else work["hbm_k3"]) * chunk_reports
+    k1_clock = pmc_clock("jx::xof_kernel<0, false>")
+    k1_clock = round(k1_clock, 3) if k1_clock else None
     dom_ms = k1_ms if k1_dom else k3_ms
     out = {
         "metric": METRIC,
@@ -352,6 +378,14 @@ def main():
         "roofline": {"bound": "valu", "kernel": dominant, "achieved": round(ach, 3), "peak": round(VALU_PEAK_TOPS, 2),
                      "unit": "TOP/s int32 instruction issue (2280 per Keccak-p[1600,12]; DESIGN.md §5)",
                      "frac": round(ach / VALU_PEAK_TOPS, 4),
+                     "mix_ceiling": round(keccak_mix_ceiling_tops(), 2),
+                     "frac_of_mix_ceiling": round(ach / keccak_mix_ceiling_tops(), 4) if k1_dom else None,
+                     "clock_GHz_pmc": k1_clock,
+                     "frac_of_mix_ceiling_at_clock": round(ach / (keccak_mix_ceiling_tops() * k1_clock / 2.4), 4)
+                     if (k1_dom and k1_clock) else None,
+                     "mix_note": "mix_ceiling = the Keccak round's issue ceiling at the measured per-instruction "
+                                 "rates (bench.py KECCAK_ROUND_MIX, DESIGN.md §5), nominal 2.4 GHz; "
+                                 "_at_clock scales it to the PMC shader clock under K1",
                      "achieved_algorithmic": round(alg, 3),
                      "frac_algorithmic": round(alg / VALU_PEAK_TOPS, 4),
                      "algorithmic_unit": "TOP/s of the spec's 32-bit ops (3720 per Keccak-p[1600,12], 160 per "

@@ -1711,8 +1711,10 @@ __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
   __builtin_amdgcn_s_waitcnt(0x3f70 | (N & 15) | ((N >> 4) << 14));
 }
+// AUX = cache policy: 0 default, 2 non-temporal (streamed data read once)
+template <int AUX = 0>
 __device__ __forceinline__ void glds16(const uint4* src, uint4* lds_row) {
-  __builtin_amdgcn_global_load_lds((const void*)src, (void*)lds_row, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((const void*)src, (void*)lds_row, 16, 0, AUX);
 }
 
 // K3 with an LDS-DMA ring (k3_pf = 20 / 21: D = 3 / 4). A workgroup is K3W waves = K3W consecutive slot
@@ -1745,7 +1747,8 @@ __device__ __forceinline__ void lds_read4(uint32_t a0, uint32_t a1, uint32_t a2,
 }
 // PROBE (timing experiments only, results are wrong): 1 = loads and barriers without the limb
 // products, 2 = limb products on whatever the ring holds, without loads
-template <int PPW, bool HIST, bool LEADER, int D, int PROBE = 0>
+// XNT: the measurement elements (read once) are loaded non-temporal
+template <int PPW, bool HIST, bool LEADER, int D, int PROBE = 0, int XNT = 0>
 __global__ __launch_bounds__(64 * K3W, 4) void flp_psum_part_glds_kernel(Cfg c, Bufs b) {
   static_assert(PPW == 2, "lds_read4 reads c, d and two measurement rows");
   constexpr int ROWS = 2 + K3W * PPW;  // c_k, d_k, then x[wave][i]
@@ -1784,7 +1787,7 @@ __global__ __launch_bounds__(64 * K3W, 4) void flp_psum_part_glds_kernel(Cfg c, 
     if (full) {
 #pragma unroll
       for (int i = 0; i < PPW; i++)
-        glds16(measb + (uint64_t)((k - 1) * chunk + j0 + i) * IL, &ring[sl][2 + wave * PPW + i][0]);
+        glds16<XNT ? 2 : 0>(measb + (uint64_t)((k - 1) * chunk + j0 + i) * IL, &ring[sl][2 + wave * PPW + i][0]);
     }
   };
   // loads a wave issues per call: 1 (coefficient, waves 0/1) + PPW (measurement, full groups)
@@ -2608,6 +2611,11 @@ static void launch_psum_part(const Cfg& c, const Bufs& b, hipStream_t s, uint32_
         hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 3>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
       else
         hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
+      return;
+    }
+    if (b.k3_pf == 24) {  // depth-4 ring, non-temporal measurement loads
+      const uint32_t g2 = grid / c.ngroups * ((c.ngroups + K3W - 1) / K3W);
+      hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4, 0, 1>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
       return;
     }
     if (b.k3_pf == 22 || b.k3_pf == 23) {  // timing probes (wrong results): loads only / products only
