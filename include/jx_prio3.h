@@ -217,7 +217,12 @@ int32_t jx_engine_stream(jx_engine* e, void** stream);
 int32_t jx_engine_timing(jx_engine* e, int32_t enable);
 int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]);
 
-/* Debug knobs (tests only): option 1 = route every report through the slow XOF kernel. */
+/* Debug knobs (tests and measurements): option 1 = route every report through the slow XOF kernel;
+ * 2 = accumulate chunking; 3 = helper K1 variant (0 automatic: the fused two-sponge kernel, the
+ * lane-split kernel for launches under one fused wave per SIMD; 1 / 2 squeeze-only + absorb-only
+ * launches; 3 lane-split; 4 fused with sequential permutations; 5 fused, forced); 4 = ParallelSum FLP
+ * part kernel (1 / 2 / 12 / 13 register-prefetch variants; 20 / 21 LDS-DMA ring of depth 3 / 4, the
+ * default 21; 26 ring with 8 slot groups per workgroup). JX_K1_SPLIT / JX_K3_PF set 3 / 4 at create. */
 int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value);
 
 const char* jx_status_str(int32_t status);

@@ -844,7 +844,7 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
   e->default_chunk = chunk;
   if (const char* env = getenv("JX_K3_PF")) {
     const int v = atoi(env);
-    if (v == 1 || v == 2 || v == 12 || v == 13 || (v >= 20 && v <= 24)) e->k3_pf = (uint32_t)v;  // 22/23: timing probes
+    if (v == 1 || v == 2 || v == 12 || v == 13 || (v >= 20 && v <= 26 && v != 24)) e->k3_pf = (uint32_t)v;  // 22/23/25: timing probes
   }
   *out = e;
   return JX_OK;
@@ -1319,7 +1319,7 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
     return JX_OK;
   }
   if (option == 4) {  // K3 load pipeline: 1 or 2 calls ahead; 12 / 13 = 2 / 3 ahead at 3 waves/SIMD; 20 / 21 LDS-DMA ring
-    if (value != 1 && value != 2 && value != 12 && value != 13 && value != 20 && value != 21 && value != 24)
+    if (value != 1 && value != 2 && value != 12 && value != 13 && value != 20 && value != 21 && value != 26)
       return JX_E_INVALID;
     e->k3_pf = (uint32_t)value;
     return JX_OK;

@@ -907,7 +907,7 @@ __global__ __launch_bounds__(64 * K1_WAVES, 4) void xof_lanes_kernel(Cfg c, Bufs
     tr.i = ti;
     uint32_t carry0 = aux[8], carry1 = aux[9], gmax = aux[10];
     f128 trunc_lo = make128(0, 0);
-    if (WIDE) trunc_lo = make128((uint64_t)aux[11] | ((uint64_t)aux[12] << 32), (uint64_t)aux[13] | ((uint64_t)aux[14] << 32));
+    if constexpr (WIDE) trunc_lo = make128((uint64_t)aux[11] | ((uint64_t)aux[12] << 32), (uint64_t)aux[13] | ((uint64_t)aux[14] << 32));
     auto emit = [&](uint32_t e, uint4 v) {
       if (e >= c.meas_len) return;
       gmax = max(gmax, ge_screen(v));
@@ -954,7 +954,7 @@ __global__ __launch_bounds__(64 * K1_WAVES, 4) void xof_lanes_kernel(Cfg c, Bufs
     aux[8] = carry0;
     aux[9] = carry1;
     aux[10] = gmax;
-    if (WIDE) {
+    if constexpr (WIDE) {
       aux[11] = (uint32_t)trunc_lo.lo;
       aux[12] = (uint32_t)(trunc_lo.lo >> 32);
       aux[13] = (uint32_t)trunc_lo.hi;
@@ -1711,10 +1711,8 @@ __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
   __builtin_amdgcn_s_waitcnt(0x3f70 | (N & 15) | ((N >> 4) << 14));
 }
-// AUX = cache policy: 0 default, 2 non-temporal (streamed data read once)
-template <int AUX = 0>
 __device__ __forceinline__ void glds16(const uint4* src, uint4* lds_row) {
-  __builtin_amdgcn_global_load_lds((const void*)src, (void*)lds_row, 16, 0, AUX);
+  __builtin_amdgcn_global_load_lds((const void*)src, (void*)lds_row, 16, 0, 0);
 }
 
 // K3 with an LDS-DMA ring (k3_pf = 20 / 21: D = 3 / 4). A workgroup is K3W waves = K3W consecutive slot
@@ -1746,21 +1744,22 @@ __device__ __forceinline__ void lds_read4(uint32_t a0, uint32_t a1, uint32_t a2,
       : "memory");
 }
 // PROBE (timing experiments only, results are wrong): 1 = loads and barriers without the limb
-// products, 2 = limb products on whatever the ring holds, without loads
-// XNT: the measurement elements (read once) are loaded non-temporal
-template <int PPW, bool HIST, bool LEADER, int D, int PROBE = 0, int XNT = 0>
-__global__ __launch_bounds__(64 * K3W, 4) void flp_psum_part_glds_kernel(Cfg c, Bufs b) {
+// products, 2 = limb products on whatever the ring holds, without loads, 3 = like 1 but every
+// workgroup streams one contiguous region (8 KiB per call) instead of the staging's call stride
+// W: waves (slot groups) per workgroup
+template <int PPW, bool HIST, bool LEADER, int D, int PROBE = 0, int W = K3W>
+__global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bufs b) {
   static_assert(PPW == 2, "lds_read4 reads c, d and two measurement rows");
-  constexpr int ROWS = 2 + K3W * PPW;  // c_k, d_k, then x[wave][i]
+  constexpr int ROWS = 2 + W * PPW;  // c_k, d_k, then x[wave][i]
   __shared__ uint4 ring[D][ROWS][64];
-  const uint32_t NG = c.ngroups, NW = (NG + K3W - 1) / K3W;
+  const uint32_t NG = c.ngroups, NW = (NG + W - 1) / W;
   const uint32_t bid = blockIdx.x, xcd = bid & 7u, q = bid >> 3;
   const uint32_t wg = q % NW;
   const uint64_t blk = (uint64_t)(q / NW) * 8 + xcd;
   const uint64_t nblk = (b.n + 63) / 64;
   if (blk >= nblk) return;  // uniform over the workgroup
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t g = wg * K3W + wave;
+  const uint32_t g = wg * W + wave;
   const uint32_t C = c.calls, chunk = c.chunk, M = c.meas_len;
   const uint32_t j0 = g * PPW;
   const bool full = g < NG && j0 + PPW <= chunk;  // this wave's PPW slots are all real
@@ -1786,8 +1785,11 @@ __global__ __launch_bounds__(64 * K3W, 4) void flp_psum_part_glds_kernel(Cfg c, 
     if (wave < 2) glds16(coefb + (uint64_t)(COEF_K + 2 * (k - 1) + wave) * IL, &ring[sl][wave][0]);
     if (full) {
 #pragma unroll
-      for (int i = 0; i < PPW; i++)
-        glds16<XNT ? 2 : 0>(measb + (uint64_t)((k - 1) * chunk + j0 + i) * IL, &ring[sl][2 + wave * PPW + i][0]);
+      for (int i = 0; i < PPW; i++) {
+        const uint64_t e = PROBE == 3 ? (uint64_t)wg * kfw * (W * PPW) + (k - 1) * (W * PPW) + wave * PPW + i
+                                      : (uint64_t)((k - 1) * chunk + j0 + i);
+        glds16(measb + e * IL, &ring[sl][2 + wave * PPW + i][0]);
+      }
     }
   };
   // loads a wave issues per call: 1 (coefficient, waves 0/1) + PPW (measurement, full groups)
@@ -1810,7 +1812,7 @@ __global__ __launch_bounds__(64 * K3W, 4) void flp_psum_part_glds_kernel(Cfg c, 
     wait_call(k + D - 2 > kfw);  // near the end fewer calls are in flight: wait for all
     __builtin_amdgcn_s_barrier();
     if (k + D - 1 <= kfw) issue(k + D - 1);
-    if (full && PROBE != 1) {
+    if (full && PROBE != 1 && PROBE != 3) {
       const uint32_t a = ring_base + ((k - 1) % D) * SLOT_BYTES;
       uint4 cv, dv, xv[PPW];
       lds_read4(a, a + ROW_BYTES, a + (2 + wave * PPW) * ROW_BYTES, a + (3 + wave * PPW) * ROW_BYTES, cv, dv, xv[0],
@@ -2613,14 +2615,16 @@ static void launch_psum_part(const Cfg& c, const Bufs& b, hipStream_t s, uint32_
         hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
       return;
     }
-    if (b.k3_pf == 24) {  // depth-4 ring, non-temporal measurement loads
-      const uint32_t g2 = grid / c.ngroups * ((c.ngroups + K3W - 1) / K3W);
-      hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4, 0, 1>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
+    if (b.k3_pf == 26) {  // depth-4 ring, 8 slot groups per workgroup
+      const uint32_t g2 = grid / c.ngroups * ((c.ngroups + 7) / 8);
+      hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4, 0, 8>), dim3(g2), dim3(64 * 8), 0, s, c, b);
       return;
     }
-    if (b.k3_pf == 22 || b.k3_pf == 23) {  // timing probes (wrong results): loads only / products only
+    if (b.k3_pf == 22 || b.k3_pf == 23 || b.k3_pf == 25) {  // timing probes (wrong results)
       const uint32_t g2 = grid / c.ngroups * ((c.ngroups + K3W - 1) / K3W);
-      if (b.k3_pf == 22)
+      if (b.k3_pf == 25)
+        hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4, 3>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
+      else if (b.k3_pf == 22)
         hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4, 1>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
       else
         hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4, 2>), dim3(g2), dim3(64 * K3W), 0, s, c, b);

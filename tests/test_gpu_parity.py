@@ -291,8 +291,8 @@ def test_k1_split_variants(name, split):
         np.testing.assert_array_equal(res.verdicts, want["verdicts"])
 
 
-@pytest.mark.parametrize("pf", [1, 2, 12, 13, 20, 21, 24],
-                         ids=["pf1_occ4", "pf2_occ4", "pf2_occ3", "pf3_occ3", "glds3", "glds4", "glds4_nt"])
+@pytest.mark.parametrize("pf", [1, 2, 12, 13, 20, 21, 26],
+                         ids=["pf1_occ4", "pf2_occ4", "pf2_occ3", "pf3_occ3", "glds3", "glds4", "glds4_w8"])
 @pytest.mark.parametrize("name", ["sumvec_8x1000_88", "histogram_256_16", "sumvec_64x20_9", "sumvec_small"])
 def test_k3_pipeline_variants(name, pf):
     """The deeper-pipelined ParallelSum FLP part kernels (register rings; the LDS-DMA ring of depth 3 / 4
