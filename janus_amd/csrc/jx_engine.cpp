@@ -88,6 +88,18 @@ struct jx_engine {
   uint32_t force_slow = 0;
   uint32_t k1_split = 0;  // helper K1 as squeeze-only + absorb-only launches (JX_K1_SPLIT, debug option 3)
   uint32_t k3_pf = 21;    // K3 load pipeline variant (JX_K3_PF, debug option 4): the depth-4 LDS-DMA ring
+  // Overlapped fused path (multi-launch device calls): K3 + K4 of launch i run on stream2 while K1 of
+  // launch i+1 runs on stream, from a second staging set. Off by default: measured on MI355X
+  // (SumVec 8x1000/88, 5 launches per step) the concurrent kernels slow each other down more than they
+  // hide (K1 26.6 -> 36.1 ms, K3 8.4 -> 23.5 ms per launch; 7.00M -> 6.62M reports/s).
+  // JX_OVERLAP=1 / debug option 5 = 1 turn it on.
+  uint32_t overlap = 0;
+  uint4 *d_meas2 = nullptr, *d_proof2 = nullptr, *d_outs2 = nullptr, *d_coef2 = nullptr;
+  uint32_t* d_flags2 = nullptr;
+  uint4* d_part2 = nullptr;
+  uint64_t cap2 = 0;
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_k1[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr}, ev_join = nullptr;
   std::string err;
 };
 
@@ -403,6 +415,13 @@ static void free_staging(jx_engine* e) {
   e->d_mask = nullptr;
   e->d_seg = nullptr;
   e->cap = 0;
+  void* ptrs2[] = {e->d_meas2, e->d_proof2, e->d_outs2, e->d_coef2, e->d_flags2, e->d_part2};
+  for (void* p : ptrs2)
+    if (p) (void)hipFree(p);
+  e->d_meas2 = e->d_proof2 = e->d_outs2 = e->d_coef2 = nullptr;
+  e->d_flags2 = nullptr;
+  e->d_part2 = nullptr;
+  e->cap2 = 0;
   e->have_batch = false;
   for (uint8_t** p : {&e->d_lis, &e->d_lps_out, &e->d_in_msgs}) {
     if (*p) (void)hipFree(*p);
@@ -462,6 +481,36 @@ static int32_t ensure_capacity(jx_engine* e, uint64_t n) {
   return JX_OK;
 }
 
+// The second staging set of the overlapped fused path (same shapes as the first; cap reports). Returns
+// false, with nothing allocated, when the device cannot hold it: the caller then runs serially.
+static bool ensure_second_set(jx_engine* e) {
+  if (e->cap2 >= e->cap && e->d_meas2) return true;
+  const Cfg& c = e->cfg;
+  const uint64_t cap = e->cap, eb = stage_eb(c);
+  auto A = [&](void** p, size_t bytes) { return hipMalloc(p, bytes ? bytes : 16) == hipSuccess; };
+  bool ok = A((void**)&e->d_meas2, cap * c.meas_len * eb) && A((void**)&e->d_proof2, cap * c.np * c.proof_len * eb) &&
+            ((c.algo != ALGO_COUNT && c.out_is_meas) || A((void**)&e->d_outs2, cap * c.out_len * 16)) &&
+            A((void**)&e->d_coef2, cap * coef_elems(c) * eb) && A((void**)&e->d_flags2, cap * 4) &&
+            A((void**)&e->d_part2, cap * part_bytes(c));
+  if (ok) ok = hipMemsetAsync(e->d_flags2, 0, cap * 4, e->stream) == hipSuccess;
+  if (ok && !e->stream2) ok = hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) == hipSuccess;
+  for (hipEvent_t* ev : {&e->ev_k1[0], &e->ev_k1[1], &e->ev_free[0], &e->ev_free[1], &e->ev_join})
+    if (ok && !*ev) ok = hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    void* ptrs2[] = {e->d_meas2, e->d_proof2, e->d_outs2, e->d_coef2, e->d_flags2, e->d_part2};
+    for (void* p : ptrs2)
+      if (p) (void)hipFree(p);
+    e->d_meas2 = e->d_proof2 = e->d_outs2 = e->d_coef2 = nullptr;
+    e->d_flags2 = nullptr;
+    e->d_part2 = nullptr;
+    e->cap2 = 0;
+    (void)hipGetLastError();  // the failed allocation is not an engine error
+    return false;
+  }
+  e->cap2 = cap;
+  return true;
+}
+
 static int32_t get_segment(jx_engine* e, uint32_t id, Segment** out) {
   auto it = e->segs.find(id);
   if (it == e->segs.end()) {
@@ -504,19 +553,19 @@ static uint64_t launch_chunk(const jx_engine* e, uint64_t n) {
 
 // ---------------------------------------------------------------------------- timing
 
-static hipError_t stage_begin(jx_engine* e, hipEvent_t* ev) {
+static hipError_t stage_begin(jx_engine* e, hipEvent_t* ev, hipStream_t s = nullptr) {
   if (!e->timing) return hipSuccess;
   hipError_t st = hipEventCreate(ev);
   if (st != hipSuccess) return st;
-  return hipEventRecord(*ev, e->stream);
+  return hipEventRecord(*ev, s ? s : e->stream);
 }
-static hipError_t stage_end(jx_engine* e, int stage, hipEvent_t ev0) {
+static hipError_t stage_end(jx_engine* e, int stage, hipEvent_t ev0, hipStream_t s = nullptr) {
   e->launches[stage]++;
   if (!e->timing) return hipSuccess;
   hipEvent_t ev1;
   hipError_t st = hipEventCreate(&ev1);
   if (st != hipSuccess) return st;
-  st = hipEventRecord(ev1, e->stream);
+  st = hipEventRecord(ev1, s ? s : e->stream);
   e->pending.push_back({stage, {ev0, ev1}});
   return st;
 }
@@ -537,11 +586,16 @@ static int32_t drain_timing(jx_engine* e) {
 // ---------------------------------------------------------------------------- core sequencing
 
 // Prepare n <= cap reports whose inputs are at the given device pointers.
+// set: staging set (1 = the overlapped path's second set); parts: 1 = the XOF stage (K1, K1') on sx,
+// 2 = the FLP stage (K3) on sf, 3 = both (default streams: the engine stream).
 static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* his,
                          const uint8_t* lps, uint8_t* verdicts, uint8_t* msgs, const uint8_t* lis = nullptr,
-                         uint8_t* lps_out = nullptr) {
+                         uint8_t* lps_out = nullptr, int set = 0, int parts = 3, hipStream_t sx = nullptr,
+                         hipStream_t sf = nullptr) {
   const Cfg& c = e->cfg;
   const bool leader = lis != nullptr;
+  if (!sx) sx = e->stream;
+  if (!sf) sf = e->stream;
   Bufs b{};
   b.n = n;
   b.nonces = nonces;
@@ -551,12 +605,12 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
   b.lis = lis;
   b.lps_out = lps_out;
   b.leader = leader ? 1u : 0u;
-  b.meas = e->d_meas;
-  b.proof = e->d_proof;
-  b.outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? e->d_meas : e->d_outs;
-  b.coef = e->d_coef;
-  b.flags = e->d_flags;
-  b.part = e->d_part;
+  b.meas = set ? e->d_meas2 : e->d_meas;
+  b.proof = set ? e->d_proof2 : e->d_proof;
+  b.outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? b.meas : (set ? e->d_outs2 : e->d_outs);
+  b.coef = set ? e->d_coef2 : e->d_coef;
+  b.flags = set ? e->d_flags2 : e->d_flags;
+  b.part = set ? e->d_part2 : e->d_part;
   b.verdicts = verdicts;
   b.msgs = msgs;
   b.consts = e->d_consts;
@@ -586,17 +640,21 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
     HIPCHK(e, launch_mp_flp(c, b, e->stream));
     HIPCHK(e, stage_end(e, ST_FLP, ev));
   } else {
-    HIPCHK(e, stage_begin(e, &ev));
-    HIPCHK(e, launch_xof(c, b, e->stream));
-    HIPCHK(e, stage_end(e, ST_XOF, ev));
-    if (!leader) {  // the leader's shares are explicit: no rejection-sampled streams to redo
-      HIPCHK(e, stage_begin(e, &ev));
-      HIPCHK(e, launch_xof_slow(c, b, e->stream));
-      HIPCHK(e, stage_end(e, ST_SLOW, ev));
+    if (parts & 1) {
+      HIPCHK(e, stage_begin(e, &ev, sx));
+      HIPCHK(e, launch_xof(c, b, sx));
+      HIPCHK(e, stage_end(e, ST_XOF, ev, sx));
+      if (!leader) {  // the leader's shares are explicit: no rejection-sampled streams to redo
+        HIPCHK(e, stage_begin(e, &ev, sx));
+        HIPCHK(e, launch_xof_slow(c, b, sx));
+        HIPCHK(e, stage_end(e, ST_SLOW, ev, sx));
+      }
     }
-    HIPCHK(e, stage_begin(e, &ev));
-    HIPCHK(e, launch_flp(c, b, e->stream));
-    HIPCHK(e, stage_end(e, ST_FLP, ev));
+    if (parts & 2) {
+      HIPCHK(e, stage_begin(e, &ev, sf));
+      HIPCHK(e, launch_flp(c, b, sf));
+      HIPCHK(e, stage_end(e, ST_FLP, ev, sf));
+    }
   }
   e->batch_nonces = nonces;
   e->leader_batch = leader;
@@ -622,15 +680,20 @@ static int32_t ensure_leader_capacity(jx_engine* e, uint64_t n) {
 
 // Single-segment accumulate into aggregation seg_id. With d_seg (dense indices), only reports whose
 // index is 0 are taken.
+// st / set / nonces: the overlapped path's stream, staging set and launch nonces (default: the engine
+// stream, set 0 and the resident batch's nonces)
 static int32_t accumulate_core(jx_engine* e, uint64_t n, const uint8_t* verdicts, const uint8_t* d_mask,
-                               const uint32_t* d_seg, uint32_t seg_id, bool dense = false) {
+                               const uint32_t* d_seg, uint32_t seg_id, bool dense = false, hipStream_t st = nullptr,
+                               int set = 0, const uint8_t* nonces = nullptr) {
   const Cfg& c = e->cfg;
   Segment* s = nullptr;
   int32_t rc = get_segment(e, seg_id, &s);
   if (rc) return rc;
+  if (!st) st = e->stream;
   AccArgs a{};
   a.n = n;
-  a.outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? e->d_meas : e->d_outs;
+  uint4* meas = set ? e->d_meas2 : e->d_meas;
+  a.outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? meas : (set ? e->d_outs2 : e->d_outs);
   a.out_len = c.out_len;
   a.verdicts = verdicts;
   a.mask = d_mask;
@@ -641,13 +704,13 @@ static int32_t accumulate_core(jx_engine* e, uint64_t n, const uint8_t* verdicts
   uint64_t nblk = (n + 63) / 64;
   a.blocks_per_chunk = (uint32_t)((nblk + a.nchunks - 1) / a.nchunks);
   if (a.blocks_per_chunk == 0) a.blocks_per_chunk = 1;
-  a.nonces = e->batch_nonces;
+  a.nonces = nonces ? nonces : e->batch_nonces;
   a.checksum = s->checksum;
   a.count = s->count;
   hipEvent_t ev = nullptr;
-  HIPCHK(e, stage_begin(e, &ev));
-  HIPCHK(e, launch_accumulate(c, a, s->agg, e->stream));
-  HIPCHK(e, stage_end(e, ST_ACC, ev));
+  HIPCHK(e, stage_begin(e, &ev, st));
+  HIPCHK(e, launch_accumulate(c, a, s->agg, st));
+  HIPCHK(e, stage_end(e, ST_ACC, ev, st));
   return JX_OK;
 }
 
@@ -842,6 +905,7 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
     if (v >= 64) chunk = v / 64 * 64;
   }
   e->default_chunk = chunk;
+  if (const char* env = getenv("JX_OVERLAP")) e->overlap = atoi(env) != 0;
   if (const char* env = getenv("JX_K3_PF")) {
     const int v = atoi(env);
     if (v == 1 || v == 2 || v == 12 || v == 13 || (v >= 20 && v <= 26 && v != 24)) e->k3_pf = (uint32_t)v;  // 22/23/25: timing probes
@@ -853,7 +917,10 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
 void jx_engine_destroy(jx_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
+  if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (hipEvent_t ev : {e->ev_k1[0], e->ev_k1[1], e->ev_free[0], e->ev_free[1], e->ev_join})
+    if (ev) (void)hipEventDestroy(ev);
   for (auto& p : e->pending) {
     (void)hipEventDestroy(p.second.first);
     (void)hipEventDestroy(p.second.second);
@@ -872,6 +939,7 @@ void jx_engine_destroy(jx_engine* e) {
   if (e->d_lis) (void)hipFree(e->d_lis);
   if (e->d_lps_out) (void)hipFree(e->d_lps_out);
   if (e->d_in_msgs) (void)hipFree(e->d_in_msgs);
+  if (e->stream2) (void)hipStreamDestroy(e->stream2);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1154,6 +1222,40 @@ int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_
   const uint8_t *N = (const uint8_t*)d_nonces, *PS = (const uint8_t*)d_ps, *H = (const uint8_t*)d_his,
                 *L = (const uint8_t*)d_lps;
   const uint32_t* SG = (const uint32_t*)d_segment;
+  // Several launches into one aggregation, when enabled: pipeline them over two streams and two
+  // staging sets. K1 (VALU-bound, every VGPR of its SIMDs) of launch i+1 runs while K3 (bound by the
+  // staging read stream) and K4 of launch i drain on stream2; K3/K4 stay ordered among themselves on
+  // stream2 (one aggregation). Measured slower than the serial path (see `overlap`).
+  const bool generic = c.algo != ALGO_COUNT && c.algo != ALGO_SUMVEC_F64_MULTIPROOF;
+  if (e->overlap && generic && n > chunk && !SG && nsegments == 1 && ensure_second_set(e)) {
+    Segment* seg = nullptr;
+    rc = get_segment(e, ids[0], &seg);  // its zero-fill is queued on stream, before the first K1
+    if (rc) return rc;
+    HIPCHK(e, hipEventRecord(e->ev_join, e->stream));
+    HIPCHK(e, hipStreamWaitEvent(e->stream2, e->ev_join, 0));
+    uint64_t i = 0;
+    for (uint64_t off = 0; off < n; off += chunk, i++) {
+      const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
+      const int set = (int)(i & 1);
+      uint8_t* vout = d_out_verdicts ? (uint8_t*)d_out_verdicts + off : e->d_verdicts;
+      uint8_t* mout = (d_out_prep_msgs && c.jr_len) ? (uint8_t*)d_out_prep_msgs + off * c.seed : e->d_msgs;
+      if (i >= 2) HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_free[set], 0));  // set reused: K3/K4 of i-2 done
+      rc = prep_core(e, m, N + off * 16, PS ? PS + off * c.ps_bytes : nullptr, H + off * c.his_bytes,
+                     L + off * c.lps_bytes, vout, mout, nullptr, nullptr, set, 1, e->stream, e->stream2);
+      if (rc) return rc;
+      HIPCHK(e, hipEventRecord(e->ev_k1[set], e->stream));
+      HIPCHK(e, hipStreamWaitEvent(e->stream2, e->ev_k1[set], 0));
+      rc = prep_core(e, m, N + off * 16, PS ? PS + off * c.ps_bytes : nullptr, H + off * c.his_bytes,
+                     L + off * c.lps_bytes, vout, mout, nullptr, nullptr, set, 2, e->stream, e->stream2);
+      if (rc) return rc;
+      rc = accumulate_core(e, m, vout, nullptr, nullptr, ids[0], false, e->stream2, set, N + off * 16);
+      if (rc) return rc;
+      HIPCHK(e, hipEventRecord(e->ev_free[set], e->stream2));
+    }
+    HIPCHK(e, hipEventRecord(e->ev_join, e->stream2));
+    HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_join, 0));  // callers sync the engine stream
+    return JX_OK;
+  }
   for (uint64_t off = 0; off < n; off += chunk) {
     const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
     uint8_t* vout = d_out_verdicts ? (uint8_t*)d_out_verdicts + off : e->d_verdicts;
@@ -1316,6 +1418,10 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
     // 0: automatic (fused; lane-split below one fused wave per SIMD), 1 / 2: squeeze-only + absorb-only
     // launches (absorb at 3 / 2 waves/SIMD), 3: lane-split, 4: sequential S, J permutations, 5: fused
     e->k1_split = (uint32_t)value;
+    return JX_OK;
+  }
+  if (option == 5) {  // overlapped two-stream fused path for multi-launch device calls (1) or not (0, default)
+    e->overlap = value != 0;
     return JX_OK;
   }
   if (option == 4) {  // K3 load pipeline: 1 or 2 calls ahead; 12 / 13 = 2 / 3 ahead at 3 waves/SIMD; 20 / 21 LDS-DMA ring

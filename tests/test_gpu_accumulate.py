@@ -141,6 +141,45 @@ def test_fused_device_segments_match_oracle():
             assert eng.aggregate_share(s) == _expected(orc, want, nonces, sel)
 
 
+@pytest.mark.parametrize("name,vdaf", [("sumvec", Prio3.sum_vec(2, 50, 9)), ("histogram", Prio3.histogram(40, 5)),
+                                       ("sum", Prio3.sum(7))])
+@pytest.mark.parametrize("overlap", [1, 0], ids=["two_streams", "serial"])
+def test_fused_device_multi_launch_overlap(name, vdaf, overlap):
+    """A fused device call over several launches into one aggregation: the two-stream pipeline (K1 of
+    launch i+1 beside K3 + K4 of launch i, two staging sets, jx_engine_debug option 5) and the serial
+    path give the oracle's verdicts, prep messages and aggregate (five launches: both staging sets are
+    reused)."""
+    import os
+
+    import torch
+
+    vk = bytes(range(16))
+    n = 2300
+    orc, nonces, ps, his, lps = _batch(vdaf, vk, n, seed=11)
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    os.environ["JX_CHUNK_REPORTS"] = "512"
+    try:
+        eng = HelperEngine(vdaf, vk)
+    finally:
+        del os.environ["JX_CHUNK_REPORTS"]
+    with eng:
+        eng.debug(5, overlap)
+        d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
+        d_m = torch.zeros((n, 16), dtype=torch.uint8, device=dev)
+        keep = [T(nonces), T(ps) if ps is not None else None, T(his), T(lps)]
+        eng.prep_and_aggregate_device(keep[0].data_ptr(), keep[1].data_ptr() if keep[1] is not None else None,
+                                      keep[2].data_ptr(), keep[3].data_ptr(), n, d_out_prep_msgs=d_m.data_ptr(),
+                                      d_out_verdicts=d_v.data_ptr())
+        eng.sync()
+        np.testing.assert_array_equal(d_v.cpu().numpy(), want["verdicts"])
+        fin = want["verdicts"] == 0
+        if vdaf.algo_id != O.COUNT:
+            np.testing.assert_array_equal(d_m.cpu().numpy()[fin], want["prep_msgs"][fin])
+        assert eng.aggregate_share(0) == (want["agg"], want["count"], want["checksum"])
+
+
 def test_batch_ids_refuse_interleaved_and_double_accumulate():
     """two interleaved leader jobs of the same size (init A, init B, finish A) must not
     finish A against B's device state; a batch accumulates at most once."""
