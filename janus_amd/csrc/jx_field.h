@@ -241,6 +241,25 @@ JX_HD void acc_add(acc192& a, uint64_t lo, uint64_t hi, uint32_t top) {
   a.w1 = addc64(a.w1, hi, c);
   a.w2 += (uint64_t)top + c;
 }
+// reduce192 for a top word w2 < 2^32 (the output-share truncation: V < 2^(128 + bits)), branch-free:
+// one fold of w2 (2^128 == 28*2^64 - 1), one fold of its carry, one conditional subtraction of p.
+JX_HD f128 reduce192_small(uint64_t w0, uint64_t w1, uint64_t w2) {
+  uint32_t b = 0;
+  uint64_t a0 = subb64(w0, w2, b);
+  uint32_t c = 0;
+  uint64_t a1 = addc64(w1, w2 * 28u, c);  // w1 + 28 w2 (28 w2 < 2^37)
+  uint32_t b1 = b;
+  a1 = subb64(a1, 0, b1);  // - the borrow of w0 - w2; w1 + 28 w2 - b >= 0, so c - b1 is 0 or 1
+  const uint64_t k = (uint64_t)(c - b1);
+  uint32_t b2 = 0;
+  a0 = subb64(a0, k, b2);  // k * 2^128 == k * (28 * 2^64 - 1); a1 < 2^37 here when k = 1: no carry
+  a1 = a1 + 28u * k - b2;
+  f128 v = make128(a0, a1);
+  uint32_t br = 0;
+  const uint64_t lo = subb64(v.lo, P128_LO, br);
+  const uint64_t hi = subb64(v.hi, P128_HI, br);
+  return ge_p128(v) ? make128(lo, hi) : v;  // v < 2^128 < 2p: one subtraction at most
+}
 JX_HD void acc_add128(acc192& a, f128 v) { acc_add(a, v.lo, v.hi, 0); }
 JX_HD f128 acc_reduce(const acc192& a) { return reduce192(a.w0, a.w1, a.w2); }
 

@@ -275,7 +275,7 @@ __device__ __forceinline__ f128 truncw_value(const TruncW& t) {
   const uint64_t w0 = addc64(t.T[0], t.T[1] << 32, c);
   const uint64_t w1 = addc64(t.T[2], (t.T[1] >> 32) | (t.T[3] << 32), c);
   const uint64_t w2 = (t.T[3] >> 32) + c;
-  return reduce192(w0, w1, w2);
+  return reduce192_small(w0, w1, w2);  // V < 2^(128 + bits), bits <= 32
 }
 // Conservative ">= p" screen for a sampled Field128 element: true for every x >= p (and for
 // the 2^-59-probable x in [2^128 - 2^69, p), which the slow kernel then redoes exactly).

@@ -38,6 +38,7 @@ void ht_f128(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
   st(out, r);
 }
 void ht_reduce192(const uint64_t w[3], uint8_t* out) { st(out, reduce192(w[0], w[1], w[2])); }
+void ht_reduce192_small(const uint64_t w[3], uint8_t* out) { st(out, reduce192_small(w[0], w[1], w[2])); }
 void ht_mont_lazy(const uint8_t* a, const uint8_t* b, uint64_t out[3]) {
   uint64_t lo, hi;
   uint32_t top;

@@ -1,0 +1,35 @@
+"""bench.py's roofline bookkeeping on the CPU: the Keccak instruction-mix ceiling, and the PMC
+summary it reads being refused when it was taken on other kernel sources."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_keccak_mix_ceiling():
+    # 190 instructions per round at the measured per-instruction rates
+    n = sum(c for c, _ in bench.KECCAK_ROUND_MIX.values())
+    assert n == 190 == bench.OPS_PER_PERM // 12
+    assert abs(bench.keccak_mix_ceiling_tops() - 52.11) < 0.05
+    assert bench.keccak_mix_ceiling_tops() < bench.VALU_PEAK_TOPS
+
+
+def test_pmc_summary_refused_on_other_sources(tmp_path, monkeypatch):
+    summary = {"workload": {"reports_per_launch": 1000, "sources_digest": "not-these-sources"},
+               "kernels": {"jx::xof_kernel<0, false>": {"hbm_read_bytes": 1e9, "hbm_write_bytes": 1e9,
+                                                       "clock_GHz": 2.1}}}
+    p = tmp_path / "s.json"
+    p.write_text(json.dumps(summary))
+    monkeypatch.setattr(bench, "PMC_SUMMARY", str(p))
+    traffic, _, note = bench.pmc_traffic("jx::xof_kernel<0, false>", 500)
+    assert traffic is None and "other kernel sources" in note
+    assert bench.pmc_clock("jx::xof_kernel<0, false>") is None
+    summary["workload"]["sources_digest"] = bench.sources_digest()
+    p.write_text(json.dumps(summary))
+    traffic, _, _ = bench.pmc_traffic("jx::xof_kernel<0, false>", 500)
+    assert traffic == 1_000_000_000  # 2e9 bytes over 1000 reports, scaled to 500
+    assert bench.pmc_clock("jx::xof_kernel<0, false>") == 2.1

@@ -28,6 +28,7 @@ def ht():
     vp = ctypes.c_void_p
     L.ht_f128.argtypes = [ctypes.c_int, vp, vp, vp]
     L.ht_reduce192.argtypes = [vp, vp]
+    L.ht_reduce192_small.argtypes = [vp, vp]
     L.ht_wide_dot.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp]
     L.ht_x25519.argtypes = [vp, vp, vp]
     L.ht_fe.argtypes = [ctypes.c_int, vp, vp, vp]
@@ -102,6 +103,22 @@ def test_reduce192(ht):
         w = (ctypes.c_uint64 * 3)(v & (2**64 - 1), (v >> 64) & (2**64 - 1), v >> 128)
         out = ctypes.create_string_buffer(16)
         ht.ht_reduce192(w, out)
+        assert int.from_bytes(out.raw, "little") == v % P128, hex(v)
+
+
+def test_reduce192_small(ht):
+    """The branch-free reduction of the output-share truncation (top word < 2^32)."""
+    rnd = random.Random(14)
+    cases = [0, 1, P128 - 1, P128, 2**128 - 1, 2**128, 2**160 - 1, 2**128 + 2**64 - 1, (2**32 - 1) << 128,
+             ((2**32 - 1) << 128) + 2**128 - 1, ((2**32 - 1) << 128) | 1, P128 * 255, 2**136 - 1]
+    cases += [rnd.randrange(2**(128 + rnd.randrange(0, 33))) for _ in range(3000)]
+    # tops whose fold carries: w1 close to 2^64
+    cases += [(rnd.randrange(1, 2**32) << 128) | ((2**64 - rnd.randrange(1, 2**40)) << 64) | rnd.randrange(2**64)
+              for _ in range(500)]
+    for v in cases:
+        w = (ctypes.c_uint64 * 3)(v & (2**64 - 1), (v >> 64) & (2**64 - 1), v >> 128)
+        out = ctypes.create_string_buffer(16)
+        ht.ht_reduce192_small(w, out)
         assert int.from_bytes(out.raw, "little") == v % P128, hex(v)
 
 
