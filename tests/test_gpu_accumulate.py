@@ -121,7 +121,7 @@ def test_fused_device_segments_match_oracle():
     dense = rng.integers(0, 6, size=n).astype(np.uint32)  # 5 = out of range: skipped
     ids = [7, 70, 700, 7000, 70000]
     dev = torch.device("cuda", 0)
-    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    T = lambda a: torch.from_numpy(np.array(a, copy=True)).to(dev)  # noqa: E731  (writable copy)
     d_seg = T(dense.astype(np.int32))
     import os
     os.environ["JX_CHUNK_REPORTS"] = "512"  # several launches: the segment array is offset per launch
@@ -158,7 +158,7 @@ def test_fused_device_multi_launch_overlap(name, vdaf, overlap):
     orc, nonces, ps, his, lps = _batch(vdaf, vk, n, seed=11)
     want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
     dev = torch.device("cuda", 0)
-    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    T = lambda a: torch.from_numpy(np.array(a, copy=True)).to(dev)  # noqa: E731  (writable copy)
     os.environ["JX_CHUNK_REPORTS"] = "512"
     try:
         eng = HelperEngine(vdaf, vk)
@@ -232,7 +232,7 @@ def test_device_leader_ping_pong_with_peer_verdicts():
     sh = [orc.shard(meas[i], nonces[i].tobytes(), rands[i].tobytes()) for i in range(n)]
     ps, lis, his = (np.frombuffer(b"".join(s[k] for s in sh), np.uint8).reshape(n, -1) for k in range(3))
     dev = torch.device("cuda", 0)
-    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    T = lambda a: torch.from_numpy(np.array(a, copy=True)).to(dev)  # noqa: E731  (writable copy)
     d_n, d_ps, d_lis, d_his = T(nonces), T(ps), T(lis), T(his)
     d_lps = torch.zeros((n, vdaf.prep_share_len), dtype=torch.uint8, device=dev)
     d_hv = torch.zeros(n, dtype=torch.uint8, device=dev)
