@@ -1130,7 +1130,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_leader_kernel(Cfg c, Bufs b
   const uint32_t b_last = ML / 168;
 
   uint32_t buf[42];  // block m of the explicit measurement share (words past the share read as 0)
-  auto load_block = [&](uint32_t m) {
+  auto load_block = [&](uint32_t m) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < 21; q++) {
       const uint32_t off = 168 * m + 8 * q;
@@ -1140,6 +1140,19 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_leader_kernel(Cfg c, Bufs b
       buf[2 * q + 1] = v.y;
     }
   };
+  // a block wholly inside the share: no per-word guard, so nothing consumes the loaded words before
+  // the next iteration and the loads stay in flight under the permutation (a guard's select would
+  // make the compiler wait for them before it)
+  auto load_block_full = [&](uint32_t m) __attribute__((always_inline)) {
+    const uint2* src = reinterpret_cast<const uint2*>(ls + 168 * m);
+#pragma unroll
+    for (int q = 0; q < 21; q++) {
+      const uint2 v = src[q];
+      buf[2 * q] = v.x;
+      buf[2 * q + 1] = v.y;
+    }
+  };
+  const uint32_t NF = MB / 168;  // blocks 0 .. NF-1 lie wholly inside the share
   uint32_t carry0 = 0, carry1 = 0, unused_screen = 0;
   bool bad = false;
   TruncW tr;
@@ -1149,11 +1162,11 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_leader_kernel(Cfg c, Bufs b
   f128 trunc_lo = make128(0, 0);
   uint4* const mp = b.meas + il_idx(blk, c.meas_len, 0, lane);
   uint4* const op = b.outs + il_idx(blk, c.out_len, 0, lane);
-  auto emit = [&](uint32_t e, uint4 v) {
+  auto emit = [&](uint32_t e, uint4 v) __attribute__((always_inline)) {
     if (e < c.meas_len) bad |= ge_exact(v);
     emit_meas<WIDE>(c, mp, op, e, v, unused_screen, tr, trunc_lo);
   };
-  auto emit_block = [&](uint32_t m) {
+  auto emit_block = [&](uint32_t m) __attribute__((always_inline)) {
     const uint32_t e0 = 21 * (m >> 1);
     if ((m & 1) == 0) {
 #pragma unroll
@@ -1185,7 +1198,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_leader_kernel(Cfg c, Bufs b
   uint32_t J[50], prev[11];
   // J's message words of block m from prev (block m-1) and buf (block m, if present); block 0 starts
   // with the header
-  auto message = [&](uint32_t m, bool have, uint32_t* jw) {
+  auto message = [&](uint32_t m, bool have, uint32_t* jw) __attribute__((always_inline)) {
     const uint32_t s0 = have ? buf[0] : 0u;
     if (m == 0) {
 #pragma unroll
@@ -1231,10 +1244,12 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_leader_kernel(Cfg c, Bufs b
 #pragma unroll
       for (int w = 0; w < 11; w++) prev[w] = buf[31 + w];
     }
-    if (1 < NM) load_block(1);
+    if (1 < NF)
+      load_block_full(1);
+    else if (1 < NM)
+      load_block(1);
     keccak_p12(J);
-#pragma unroll 1
-    for (uint32_t m = 1; m < b_last; m++) {  // m < b_last <= NM: block m holds measurement bytes
+    auto step = [&](uint32_t m) __attribute__((always_inline)) {  // block m < b_last <= NM holds measurement bytes
       emit_block(m);
       uint32_t jw[42];
       message(m, true, jw);
@@ -1242,6 +1257,17 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_leader_kernel(Cfg c, Bufs b
       for (int w = 0; w < 42; w++) J[w] ^= jw[w];
 #pragma unroll
       for (int w = 0; w < 11; w++) prev[w] = buf[31 + w];
+    };
+    uint32_t m = 1;
+#pragma unroll 1
+    for (; m < b_last && m + 1 < NF; m++) {  // the next block is wholly inside the share
+      step(m);
+      load_block_full(m + 1);
+      keccak_p12(J);
+    }
+#pragma unroll 1
+    for (; m < b_last; m++) {
+      step(m);
       if (m + 1 < NM) load_block(m + 1);
       keccak_p12(J);
     }
