@@ -159,6 +159,55 @@ def make_pool(vdaf, vk, K, seed=0x5EED, threads=16):
     return orc, nonces, ps, his, lps, want
 
 
+def pool_cache_path(vdaf, vk, K, seed=0x5EED) -> str:
+    import hashlib
+
+    key = hashlib.sha256(f"{vdaf.algo_id}/{vdaf.bits}/{vdaf.length}/{vdaf.chunk_length}/{K}/{seed}/{vk.hex()}/"
+                         "pool-v1".encode()).hexdigest()[:16]
+    return os.path.join(os.environ.get("JX_POOL_CACHE", "/tmp"), f"janus_amd_bench_pool_{key}.npz")
+
+
+def load_or_make_pool(vdaf, vk, K, threads, local_rank: int, wait_s: float = 900.0):
+    """The synthetic pool, generated once per node: local rank 0 runs the C oracle and writes the pool
+    (inputs + the oracle's verdicts and aggregate) atomically to a cache file; the other ranks wait for
+    the file and read it. An 8-rank start therefore costs one generation, not eight."""
+    from oracle import oracle as O
+
+    path = pool_cache_path(vdaf, vk, K)
+    if not os.path.exists(path):
+        if local_rank == 0:
+            orc, nonces, ps, his, lps, want = make_pool(vdaf, vk, K, threads=threads)
+            tmp = f"{path}.{os.getpid()}.tmp.npz"
+            np.savez(tmp, nonces=nonces, ps=ps, his=his, lps=lps, verdicts=want["verdicts"],
+                     agg=np.frombuffer(want["agg"], np.uint8), count=np.array([want["count"]], np.int64))
+            os.replace(tmp, path)
+            return orc, nonces, ps, his, lps, want, "generated"
+        t0 = time.perf_counter()
+        while not os.path.exists(path):
+            if time.perf_counter() - t0 > wait_s:
+                sys.exit(f"bench.py: rank {local_rank} waited {wait_s:.0f}s for the pool file {path}")
+            time.sleep(0.5)
+    d = np.load(path)  # allow_pickle=False: plain arrays this script wrote
+    orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
+    want = {"verdicts": d["verdicts"], "agg": d["agg"].tobytes(), "count": int(d["count"][0])}
+    return orc, d["nonces"], d["ps"], d["his"], d["lps"], want, "cached"
+
+
+def cpu_threads() -> dict:
+    """Host threads for the CPU baseline: the CPUs this process may run on (affinity), capped by the
+    cgroup CPU quota when one is set (a GPU box's share of a larger machine)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    use = min(aff, quota) if quota else aff
+    return {"affinity_cpus": aff, "cgroup_quota_cpus": quota, "threads": use}
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -250,6 +299,9 @@ def main():
     ap.add_argument("--bits", type=int, default=8)
     ap.add_argument("--length", type=int, default=1000)
     ap.add_argument("--chunk", type=int, default=88)
+    ap.add_argument("--no-dist", dest="dist", action="store_false",
+                    help="at N=1, skip the RCCL (nccl) process group and the shard-record all-gather + device merge "
+                         "that every step otherwise ends with (by default the N=1 step carries the N>1 step's work)")
     args = ap.parse_args()
     ensure_world(args.gpus)
 
@@ -266,16 +318,23 @@ def main():
     assert world == args.gpus  # ensure_world
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    use_dist = world > 1 or args.dist
+    if use_dist:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     vdaf = Prio3.sum_vec(args.bits, args.length, args.chunk)
     vk = bytes(range(16))
-    threads = min(16, os.cpu_count() or 1)
+    cpu = cpu_threads()
+    threads = min(16, cpu["threads"])  # pool generation (the oracle) per node
     t0 = time.perf_counter()
-    orc, nonces, ps, his, lps, want = make_pool(vdaf, vk, args.pool, threads=threads)
-    log(f"pool of {args.pool} reports generated in {time.perf_counter() - t0:.1f}s; "
-        f"{int(want['count'])} valid")
+    orc, nonces, ps, his, lps, want, how = load_or_make_pool(vdaf, vk, args.pool, threads, local_rank)
+    startup_s = time.perf_counter() - t0
+    log(f"pool of {args.pool} reports {how} in {startup_s:.1f}s; {int(want['count'])} valid")
 
     R = args.reports_per_gpu
     reps = -(-R // args.pool)
@@ -288,7 +347,7 @@ def main():
     d_verdicts = torch.empty(R, dtype=torch.uint8, device=dev)
     d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
     eng = HelperEngine(vdaf, vk, device=local_rank)
-    combiner = ShardCombiner(eng) if world > 1 else None
+    combiner = ShardCombiner(eng) if use_dist else None
 
     def step():
         eng.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(), d_lps.data_ptr(), R,
@@ -300,18 +359,18 @@ def main():
     for _ in range(args.warmup):
         step()
     eng.timing(True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t
     kt = eng.timing_read()
-    if world > 1:
+    if use_dist:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
@@ -330,7 +389,7 @@ def main():
     exp_count = total_steps * (q * want["count"] + head["count"])
     verified = agg == exp and count == exp_count
     verdict_ok = bool(np.array_equal(d_verdicts.cpu().numpy(), np.tile(want["verdicts"], reps)[:R]))
-    if world > 1:
+    if combiner is not None:
         c_agg, c_count, _ = combiner.result()
         exp_c = b"".join(((x * world) % P128).to_bytes(16, "little") for x in acc)
         verified = verified and c_agg == exp_c and c_count == world * exp_count
@@ -374,7 +433,11 @@ def main():
         "config": {"workload": f"Prio3SumVec bits={args.bits} length={args.length} chunk_length={args.chunk}: "
                                "helper prep_init + prep_shares_to_prep + prep_next + aggregate",
                    "reports_per_gpu": R, "global_reports_per_step": R * world,
-                   "parallelism": f"report-sharded x{world} (RCCL all-gather + device mod-p combine)"},
+                   "parallelism": f"report-sharded x{world} (RCCL all-gather + device mod-p combine)",
+                   "combine_timed": combiner is not None,
+                   "combine_note": "every step ends with the shard-record RCCL all-gather + device merge"
+                   if combiner is not None else "N=1 with --no-dist: no combine in the step"},
+        "startup": {"pool": how, "seconds": round(startup_s, 1)},
         "roofline": {"bound": "valu", "kernel": dominant, "achieved": round(ach, 3), "peak": round(VALU_PEAK_TOPS, 2),
                      "unit": "TOP/s int32 instruction issue (2280 per Keccak-p[1600,12]; DESIGN.md §5)",
                      "frac": round(ach / VALU_PEAK_TOPS, 4),
@@ -407,11 +470,12 @@ def main():
         "verified": bool(verified and verdict_ok),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(orc, vdaf, vk, nonces, ps, his, lps, args.cpu_seconds, threads)
+        out["cpu_baseline"] = cpu_baseline(orc, vdaf, vk, nonces, ps, his, lps, args.cpu_seconds, cpu["threads"])
+        out["cpu_baseline"].update(cpu)
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

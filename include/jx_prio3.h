@@ -19,8 +19,10 @@
  *  - Every function returns int32 status: 0 = OK, < 0 = engine error (JX_E_*).
  *    Per-report preparation failures are NOT errors: they are verdict bytes.
  *  - The caller owns every host buffer; it is borrowed for the duration of the call.
- *  - An engine owns its device memory and one HIP stream on one device. Engines are
- *    not re-entrant: serialize calls per engine; use one engine per GPU.
+ *  - An engine owns its device memory and one HIP stream on one device. Every entry point takes the
+ *    engine's mutex for the duration of the call, so one engine per GPU can serve concurrent
+ *    aggregation jobs from several host threads; the device work of the calls is serialized on the
+ *    engine stream. What a job keeps between calls (its prepared reports) is a batch handle.
  *  - Byte layouts are the DAP/VDAF encodings (fixed stride per report):
  *      nonces               n x 16   (report ids; VDAF nonce, aggregator.rs:1951)
  *      public_shares        n x PS   (Prio3PublicShare: joint-rand parts, 0 or 32 B)
@@ -104,18 +106,48 @@ int32_t jx_engine_sizes(const jx_engine* e, uint32_t* public_share, uint32_t* he
 /* Reserve staging for `reports` reports (two-phase API needs n <= capacity; grows on demand). */
 int32_t jx_engine_set_capacity(jx_engine* e, uint64_t reports);
 
+/* ---- Resident prepared batches (one per aggregation job in flight).
+ * Every prepare call (jx_helper_prep_batch, jx_leader_prep_init_*) creates a NEW resident batch and
+ * returns its handle (batch id, never reused, never 0); it does not disturb other resident batches,
+ * so any number of aggregation jobs can be prepared, finished and aggregated interleaved on one
+ * engine (Janus steps max_concurrent_job_workers jobs at once, aggregator/src/binary_utils/
+ * job_driver.rs:116-138; the leader holds each job's prepare state across the helper round trip,
+ * aggregation_job_driver.rs:396-416 -> :540-701). A batch holds its output shares, verdicts, prep
+ * messages (leader: the corrected joint-rand seeds) and report ids in HBM until it is released
+ * (jx_batch_release) or accumulated into the running aggregations (jx_accumulate*, which releases it).
+ * Calls naming a released or unknown batch return JX_E_STATE; a report count other than the
+ * batch's returns JX_E_INVALID. */
+
 /* Batched helper_initialized + evaluate for n reports (host buffers).
  * out_verdicts[n] receives JX_FINISHED or a failure code; out_prep_msgs[n x PM] the outbound
  * Finish{prep_msg} payload (meaningful where verdict == JX_FINISHED); out_output_shares
- * (nullable) the output shares. Output shares stay resident for jx_accumulate: the engine holds
- * one prepared batch at a time, named by a batch id (jx_engine_batch_id); any later prepare call
- * replaces it, and jx_leader_prep_finish_* / jx_accumulate* refuse (JX_E_STATE) a batch id that no
- * longer names the resident batch instead of mixing two batches. */
+ * (nullable) the output shares; *out_batch_id (nullable) the new batch's handle. */
 int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
                              const uint8_t* helper_input_shares, const uint8_t* leader_prep_shares,
-                             uint8_t* out_prep_msgs, uint8_t* out_verdicts, uint8_t* out_output_shares);
-/* Id of the resident prepared batch (0: none, or already accumulated). */
+                             uint8_t* out_prep_msgs, uint8_t* out_verdicts, uint8_t* out_output_shares,
+                             uint64_t* out_batch_id);
+/* Handle of the most recently prepared batch if it is still resident (0 otherwise). */
 int32_t jx_engine_batch_id(const jx_engine* e, uint64_t* batch_id);
+/* Resident batches and the device bytes they hold (either pointer nullable). */
+int32_t jx_engine_batches(const jx_engine* e, uint64_t* resident, uint64_t* device_bytes);
+/* Drop a resident batch (its device memory returns to the engine). */
+int32_t jx_batch_release(jx_engine* e, uint64_t batch_id);
+
+/* Per-job batch-aggregation deltas (the retry-safe accumulation contract).
+ * Aggregates the finished reports of batch `batch_id` (helper; leader after finish) with
+ * accept_mask[i] != 0 (nullable = all) into nsegments ZEROED aggregations, report i into aggregation
+ * segment_index[i] (nullable = all into 0; indices >= nsegments are skipped), and writes them as
+ * nsegments back-to-back shard records (encoded aggregate share OUT x FB || report count u64 LE ||
+ * ReportIdChecksum 32 B, see jx_shard_record_bytes) to out_records. Nothing in the engine changes: the
+ * batch stays resident and the running aggregations are untouched, so the call can be repeated with
+ * the same or another mask (a retried run_tx closure, aggregator_core/src/datastore.rs:225-282) and the
+ * host merges each record into the batch-aggregation row it read at its shard `ord`
+ * (BatchAggregation::merged_with, aggregation_job_writer.rs:527,615-690). */
+int32_t jx_batch_aggregate_records(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t* accept_mask,
+                                   const uint32_t* segment_index, uint32_t nsegments, uint8_t* out_records);
+/* Same with device arrays and a device output (asynchronous on the engine stream). */
+int32_t jx_batch_aggregate_records_device(jx_engine* e, uint64_t batch_id, uint64_t n, const void* d_accept_mask,
+                                          const void* d_segment_index, uint32_t nsegments, void* d_out_records);
 
 /* ---- Leader role: the leader side of the same ping-pong exchange.
  * jx_leader_prep_init_batch replaces the per-report vdaf.leader_initialized(verify_key, agg_param,
@@ -125,13 +157,12 @@ int32_t jx_engine_batch_id(const jx_engine* e, uint64_t* batch_id);
  * jx_engine_leader_sizes). out_prep_shares[n x LPS] receives the prep_share that goes into
  * PingPongMessage::Initialize; out_verdicts[n]: JX_FINISHED (0) = initialized, or
  * JX_PREPARE_INIT_FAILURE (an input-share element >= p, or t a P-th root of unity). The prepare
- * state (output share + corrected joint-rand seed) stays on the device.
+ * state (output share + corrected joint-rand seed) stays on the device in the new batch.
  * jx_leader_prep_finish_batch replaces leader_continued on the helper's Finish{prep_msg}
  * (aggregation_job_driver.rs:588-602): prepare_next fails (JX_PREPARE_NEXT_FAILURE) unless prep_msg
  * equals the corrected seed. prep_msgs: n x PM (PM = 0: nullable). out_output_shares nullable.
- * *out_batch_id names the leader batch; finish and accumulate must pass it back (JX_E_STATE when
- * another prepare call has replaced the batch in between, e.g. two interleaved aggregation jobs).
- * After finish, jx_accumulate aggregates the leader's finished output shares. */
+ * *out_batch_id names the leader batch; finish, records and accumulate pass it back. A batch is
+ * finished once (a second finish returns JX_E_STATE); its records / accumulation need the finish. */
 int32_t jx_engine_leader_sizes(const jx_engine* e, uint32_t* leader_input_share);
 int32_t jx_leader_prep_init_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
                                   const uint8_t* leader_input_shares, uint8_t* out_prep_shares, uint8_t* out_verdicts,
@@ -139,7 +170,7 @@ int32_t jx_leader_prep_init_batch(jx_engine* e, uint64_t n, const uint8_t* nonce
 int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t* prep_msgs,
                                     uint8_t* out_verdicts, uint8_t* out_output_shares);
 /* Device-pointer leader role (inputs resident in HBM; asynchronous on the engine stream, n <= the
- * engine capacity, grown on demand; the nonces must stay valid until the batch is accumulated).
+ * engine capacity, grown on demand; the report ids are copied into the batch).
  * d_out_verdicts nullable. Finish: d_peer_verdicts (nullable) are the helper's verdicts; a report
  * the helper rejected gets JX_HELPER_STEP_FAILURE. */
 int32_t jx_leader_prep_init_device(jx_engine* e, uint64_t n, const void* d_nonces, const void* d_public_shares,
@@ -149,17 +180,18 @@ int32_t jx_leader_prep_finish_device(jx_engine* e, uint64_t batch_id, uint64_t n
                                      const void* d_peer_verdicts, void* d_out_verdicts);
 
 /* Accumulate the output shares of the resident batch `batch_id` (helper, or leader after finish) into
- * batch aggregations (BatchAggregation::merged_with, aggregation_job_writer.rs:608-708): report i is
- * added iff verdict == FINISHED and accept_mask[i] != 0 (accept_mask nullable = all), into
- * aggregation `segment[i]` (any u32 batch-aggregation id; segment nullable = 0). Adds to the
- * aggregate share, the report count and the ReportIdChecksum (XOR of SHA-256(report id)). Any
- * number of segments is handled in one pass over the batch (device counting sort by segment). A
- * batch is accumulated at most once (a second call returns JX_E_STATE). */
+ * the engine's running batch aggregations (the engine as one shard, §8e): report i is added iff
+ * verdict == FINISHED and accept_mask[i] != 0 (accept_mask nullable = all), into aggregation
+ * `segment[i]` (any u32 batch-aggregation id; segment nullable = 0). Adds to the aggregate share, the
+ * report count and the ReportIdChecksum (XOR of SHA-256(report id)). Any number of segments is handled
+ * in one pass over the batch (device counting sort by segment). The batch is released: it is
+ * accumulated at most once (a second call returns JX_E_STATE). */
 int32_t jx_accumulate(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t* accept_mask,
                       const uint32_t* segment);
 /* Same with device arrays: d_accept_mask (nullable) and d_segment (nullable = all reports into
  * segment_ids[0]) holding, per report, an index into the host array segment_ids[nsegments]; reports
- * whose index is >= nsegments are skipped. Asynchronous on the engine stream. */
+ * whose index is >= nsegments are skipped. segment_ids must not repeat an id (JX_E_INVALID).
+ * Asynchronous on the engine stream. */
 int32_t jx_accumulate_device(jx_engine* e, uint64_t batch_id, uint64_t n, const void* d_accept_mask,
                              const void* d_segment, const uint32_t* segment_ids, uint32_t nsegments);
 
@@ -172,7 +204,8 @@ int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces
 
 /* Same with DEVICE pointers (inputs already resident in HBM, e.g. from a torch tensor).
  * Report i goes to aggregation segment_ids[d_segment[i]] (d_segment nullable: all into
- * segment_ids[0]; indices >= nsegments are skipped); every finished report is added.
+ * segment_ids[0]; indices >= nsegments are skipped; ids must not repeat); every finished report is
+ * added. No batch is created (staging holds one launch at a time).
  * d_out_prep_msgs / d_out_verdicts are device pointers (nullable). Asynchronous on the engine
  * stream; call jx_engine_sync before reading results. */
 int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_nonces, const void* d_public_shares,
@@ -218,11 +251,9 @@ int32_t jx_engine_timing(jx_engine* e, int32_t enable);
 int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]);
 
 /* Debug knobs (tests and measurements): option 1 = route every report through the slow XOF kernel;
- * 2 = accumulate chunking; 3 = helper K1 variant (0 automatic: the fused two-sponge kernel, the
- * lane-split kernel for launches under one fused wave per SIMD; 1 / 2 squeeze-only + absorb-only
- * launches; 3 lane-split; 4 fused with sequential permutations; 5 fused, forced); 4 = ParallelSum FLP
- * part kernel (1 / 2 / 12 / 13 register-prefetch variants; 20 / 21 LDS-DMA ring of depth 3 / 4, the
- * default 21; 26 ring with 8 slot groups per workgroup). JX_K1_SPLIT / JX_K3_PF set 3 / 4 at create. */
+ * 2 = accumulate chunking; 3 = helper K1 kernel (0 automatic: the fused two-sponge kernel, the
+ * lane-split kernel for launches under one fused wave per SIMD; 3 lane-split; 5 fused, forced);
+ * 5 = overlapped two-stream fused path. JX_K1_SPLIT sets option 3 at create. */
 int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value);
 
 const char* jx_status_str(int32_t status);

@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(_HERE, "lib", "libjanus_prio3.so")
 # Every symbol include/jx_prio3.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
     "jx_engine_create", "jx_engine_create_ex", "jx_engine_destroy", "jx_engine_sizes", "jx_engine_set_capacity",
-    "jx_helper_prep_batch", "jx_engine_batch_id", "jx_engine_leader_sizes", "jx_leader_prep_init_batch",
+    "jx_helper_prep_batch", "jx_engine_batch_id", "jx_engine_batches", "jx_batch_release",
+    "jx_batch_aggregate_records", "jx_batch_aggregate_records_device", "jx_engine_leader_sizes", "jx_leader_prep_init_batch",
     "jx_leader_prep_finish_batch", "jx_leader_prep_init_device", "jx_leader_prep_finish_device",
     "jx_accumulate", "jx_accumulate_device", "jx_helper_prep_aggregate", "jx_helper_prep_aggregate_device",
     "jx_aggregate_read", "jx_aggregate_checksum", "jx_aggregate_reset", "jx_aggregate_export_device",
@@ -60,8 +61,12 @@ def load():
         "jx_engine_destroy": (None, [vp]),
         "jx_engine_sizes": (i32, [vp, P(u32), P(u32), P(u32), P(u32), P(u32), P(u32)]),
         "jx_engine_set_capacity": (i32, [vp, u64]),
-        "jx_helper_prep_batch": (i32, [vp, u64, u8p, u8p, u8p, u8p, u8p, u8p, u8p]),
+        "jx_helper_prep_batch": (i32, [vp, u64, u8p, u8p, u8p, u8p, u8p, u8p, u8p, P(u64)]),
         "jx_engine_batch_id": (i32, [vp, P(u64)]),
+        "jx_engine_batches": (i32, [vp, P(u64), P(u64)]),
+        "jx_batch_release": (i32, [vp, u64]),
+        "jx_batch_aggregate_records": (i32, [vp, u64, u64, u8p, u8p, u32, u8p]),
+        "jx_batch_aggregate_records_device": (i32, [vp, u64, u64, vp, vp, u32, vp]),
         "jx_engine_leader_sizes": (i32, [vp, P(u32)]),
         "jx_leader_prep_init_batch": (i32, [vp, u64, u8p, u8p, u8p, u8p, u8p, P(u64)]),
         "jx_leader_prep_finish_batch": (i32, [vp, u64, u64, u8p, u8p, u8p]),

@@ -11,8 +11,11 @@ reference:
   * answers PrepareStepResult::Continue{Finish{prep_msg}} or Reject(error) (:1969-1993),
   * later fails replayed reports with ReportReplayed (:2101-2136) and accumulates the
     rest into batch aggregations (aggregation_job_writer.rs:608-708).
-Here the per-report prio call is one engine batch call and accumulation is one masked,
-segmented device reduction.
+Here the per-report prio call is one engine batch call that leaves a resident batch (one
+per aggregation job in flight), and accumulation is one masked, segmented device reduction:
+with a BatchAggregationWriter, into per-batch-identifier deltas merged inside a retryable
+datastore transaction (aggregation_job_writer.rs:476-553, 608-708); without one, into the
+engine's running aggregations.
 """
 from __future__ import annotations
 
@@ -34,23 +37,32 @@ class AggregateInitOutcome:
     step_failures: Counter = field(default_factory=Counter)  # janus_step_failures{type=...}
 
 
+def _dense(seg_of_row: list[int]) -> tuple[np.ndarray, list[int]]:
+    """Dense per-row indices into the list of distinct batch identifiers (first-seen order)."""
+    ids: dict[int, int] = {}
+    idx = np.array([ids.setdefault(int(s), len(ids)) for s in seg_of_row], np.uint32)
+    return idx, list(ids)
+
+
 def handle_aggregate_init(engine: HelperEngine, prepare_inits: list[PrepareInit], input_shares: list[bytes],
                           segments: list[int] | None = None, replayed: set[bytes] | None = None,
-                          writer=None) -> AggregateInitOutcome:
+                          writer=None, extra_report_times: list[tuple[int, int]] = (),
+                          inject_tx_failures: int = 0) -> AggregateInitOutcome:
     """Prepare and aggregate one AggregationJobInitializeReq worth of reports.
 
     input_shares[i] is the HPKE-decrypted PlaintextInputShare payload of report i (the
     encoded Prio3 helper input share). segments[i] names the batch aggregation the report
     belongs to (batch identifier; default 0). replayed holds report ids the datastore
-    already saw (check_other_report_aggregation_exists). writer (a
-    batch_aggregation.BatchAggregationWriter) records the host-side half of each batch
-    aggregation: every report's timestamp, failed ones included, and the job counters (a
-    one-round Prio3 helper job is written already finished: neither counter moves)."""
+    already saw (check_other_report_aggregation_exists).
+
+    writer (a batch_aggregation.BatchAggregationWriter): the job's batch aggregations are
+    written in one retryable transaction (a one-round Prio3 helper job is written already
+    finished: neither job counter moves); every report's timestamp widens its batch's
+    interval, failed ones included (extra_report_times: report aggregations of the request
+    that never reached this call, e.g. HPKE failures). Reports landing in an already
+    collected batch fail with BatchCollected. The engine batch is released afterwards.
+    Without a writer the finished reports go into the engine's running aggregations."""
     n = len(prepare_inits)
-    if writer is not None:
-        segs = segments if segments else [0] * n
-        writer.observe_report_aggregations(segs, [p.report_share.metadata.time for p in prepare_inits])
-        writer.observe_job(segs, initial_write=True, terminal=True)
     if len(input_shares) != n:
         raise ValueError("one input share per PrepareInit")
     ids = [p.report_share.metadata.report_id for p in prepare_inits]
@@ -88,6 +100,7 @@ def handle_aggregate_init(engine: HelperEngine, prepare_inits: list[PrepareInit]
         lps = np.frombuffer(b"".join(prepare_inits[i].message.prep_share for i in batch_idx), np.uint8)
         res = engine.helper_initialized_batch(nonces, ps, his, lps)
         accept = np.zeros(m, np.uint8)
+        row_seg = [int(segments[i]) if segments else 0 for i in batch_idx]
         seg = np.zeros(m, np.uint32)
         for j, i in enumerate(batch_idx):
             verdict = int(res.verdicts[j])
@@ -102,7 +115,25 @@ def handle_aggregate_init(engine: HelperEngine, prepare_inits: list[PrepareInit]
             accept[j] = 1
             seg[j] = segments[i] if segments else 0
             finished[i] = True
-        engine.accumulate(m, accept, seg, batch_id=res.batch_id)
+        if writer is None:
+            engine.accumulate(m, accept, seg, batch_id=res.batch_id)
+    if writer is not None:
+        times = [(int(segments[i]) if segments else 0, p.report_share.metadata.time)
+                 for i, p in enumerate(prepare_inits)] + list(extra_report_times)
+        if m:
+            idx, seg_ids = _dense(row_seg)
+            try:
+                collected = writer.write_job(engine, res.batch_id, m, accept, idx, seg_ids, times,
+                                             initial_write=True, terminal=True, inject_failures=inject_tx_failures)
+            finally:
+                engine.release(res.batch_id)
+        else:
+            collected = writer.write_job(engine, 0, 0, None, None, [], times, initial_write=True, terminal=True,
+                                         inject_failures=inject_tx_failures)
+        for j, i in enumerate(batch_idx):  # fail_report_aggregations_for_collected_batches
+            if finished[i] and row_seg[j] in collected:
+                finished[i] = False
+                results[i] = PrepareStepResult(2, error=PrepareError.BatchCollected)
     responses = [PrepareResp(ids[i], results[i]) for i in range(n)]
     return AggregateInitOutcome(responses, finished, failures)
 
@@ -140,10 +171,6 @@ def leader_aggregate_init(engine: HelperEngine, reports: list[LeaderReport], seg
     timestamp."""
     v = engine.vdaf
     n = len(reports)
-    if writer is not None:
-        segs = segments if segments else [0] * n
-        writer.observe_report_aggregations(segs, [r.metadata.time for r in reports])
-        writer.observe_job(segs, initial_write=True, terminal=False)
     failures: Counter = Counter()
     failed: dict[int, PrepareError] = {}
     ok = [i for i, r in enumerate(reports) if len(r.leader_input_share) == engine.leader_input_share_len
@@ -169,6 +196,9 @@ def leader_aggregate_init(engine: HelperEngine, reports: list[LeaderReport], seg
             stepped.append(i)
     step = LeaderStep(inits, stepped, failed, len(ok), failures, res if ok else None)
     step._batch_index = {i: j for j, i in enumerate(ok)}  # report index -> engine batch row
+    step._times = [(int(segments[i]) if segments else 0, r.metadata.time) for i, r in enumerate(reports)]
+    if writer is not None:  # InitialWrite of the in-progress job: no finished report yet
+        writer.write_job(engine, 0, 0, None, None, [], step._times, initial_write=True, terminal=False)
     return step
 
 
@@ -176,10 +206,9 @@ def leader_process_helper_response(engine: HelperEngine, step: LeaderStep, prepa
                                    segments: list[int] | None = None, writer=None) -> AggregateInitOutcome:
     """Finish the leader's reports from the helper's AggregationJobResp and accumulate the
     finished ones (process_response_from_helper, aggregation_job_driver.rs:540-701). writer: the
-    job is updated into a terminal state (aggregation_jobs_terminated + 1 per batch identifier)."""
-    if writer is not None:
-        nrep = max([*step.stepped, *step.failed, -1]) + 1
-        writer.observe_job(segments if segments else [0] * nrep, initial_write=False, terminal=True)
+    job is updated into a terminal state (aggregation_jobs_terminated + 1 per batch identifier),
+    its finished reports merged as deltas in one retryable transaction, and the engine batch is
+    released. Without a writer they go into the engine's running aggregations."""
     if len(prepare_resps) != len(step.stepped) or any(
             resp.report_id != step.prepare_inits[k].report_share.metadata.report_id
             for k, resp in enumerate(prepare_resps)):
@@ -209,6 +238,8 @@ def leader_process_helper_response(engine: HelperEngine, step: LeaderStep, prepa
                 msgs[row, :pm] = np.frombuffer(res.message.prep_msg, np.uint8)
             continued[row] = True
     if step.n == 0:  # no report reached the engine: nothing to continue or accumulate
+        if writer is not None:
+            writer.write_job(engine, 0, 0, None, None, [], step._times, initial_write=False, terminal=True)
         responses = [PrepareResp(step.prepare_inits[k].report_share.metadata.report_id,
                                  PrepareStepResult(2, error=results[i])) for k, i in enumerate(step.stepped)]
         return AggregateInitOutcome(responses, finished, failures)
@@ -226,7 +257,22 @@ def leader_process_helper_response(engine: HelperEngine, step: LeaderStep, prepa
         accept[row] = 1
         seg[row] = segments[i] if segments else 0
         finished[i] = True
-    engine.accumulate(step.n, accept, seg, batch_id=step.init.batch_id)
+    if writer is None:
+        engine.accumulate(step.n, accept, seg, batch_id=step.init.batch_id)
+    else:
+        row_seg = [0] * step.n
+        for i, row in step._batch_index.items():
+            row_seg[row] = int(segments[i]) if segments else 0
+        idx, seg_ids = _dense(row_seg)
+        try:
+            collected = writer.write_job(engine, step.init.batch_id, step.n, accept, idx, seg_ids, step._times,
+                                         initial_write=False, terminal=True)
+        finally:
+            engine.release(step.init.batch_id)
+        for i, row in step._batch_index.items():
+            if finished[i] and row_seg[row] in collected:
+                finished[i] = False
+                results[i] = PrepareError.BatchCollected
     responses = [PrepareResp(step.prepare_inits[k].report_share.metadata.report_id,
                              PrepareStepResult(1) if results[i] is None else
                              PrepareStepResult(2, error=results[i]))
@@ -288,12 +334,11 @@ def handle_aggregate_init_encrypted(engine: HelperEngine, opener, hpke_config_id
             continue
         payloads[i] = pis.payload
     keep = [i for i in range(n) if i in payloads]
-    if writer is not None:  # every report aggregation of the request, including the ones that failed to open
-        segs = segments if segments else [0] * n
-        writer.observe_report_aggregations(segs, [p.report_share.metadata.time for p in prepare_inits])
-        writer.observe_job(segs, initial_write=True, terminal=True)
+    # every report aggregation of the request is written, including the ones that failed to open
+    dropped = [(int(segments[i]) if segments else 0, prepare_inits[i].report_share.metadata.time)
+               for i in range(n) if i not in payloads]
     inner = handle_aggregate_init(engine, [prepare_inits[i] for i in keep], [payloads[i] for i in keep],
-                                  [segments[i] for i in keep] if segments else None, replayed)
+                                  [segments[i] for i in keep] if segments else None, replayed, writer, dropped)
     failures.update(inner.step_failures)
     by_row = dict(zip(keep, range(len(keep))))
     finished = np.zeros(n, bool)

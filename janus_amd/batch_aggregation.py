@@ -99,38 +99,99 @@ class BatchAggregation:
         return replace(self, state=SCRUBBED, aggregate_share=None)
 
 
+class Datastore:
+    """In-memory stand-in for the batch_aggregations table and Datastore::run_tx
+    (aggregator_core/src/datastore.rs:225-282): rows keyed by (batch identifier, ord). A transaction
+    runs its closure on a snapshot of the committed rows; a serialization failure discards the
+    snapshot and runs the closure again, so the closure must be pure (Janus's writer is copy-on-write
+    for exactly this reason, aggregation_job_writer.rs:497-500). `inject_failures` makes the first k
+    attempts fail after the closure ran (tests)."""
+
+    def __init__(self):
+        self.rows: dict[tuple[int, int], BatchAggregation] = {}
+        self.attempts = 0
+
+    def run_tx(self, fn, inject_failures: int = 0):
+        tries = 0
+        while True:
+            tx = dict(self.rows)
+            result = fn(tx)
+            tries += 1
+            self.attempts += 1
+            if tries <= inject_failures:
+                continue  # rolled back: nothing of this attempt is kept
+            self.rows = tx
+            return result
+
+
 @dataclass
 class BatchAggregationWriter:
-    """The batch-aggregation bookkeeping of AggregationJobWriter for one engine: the device holds the
-    per-segment share / count / checksum; this object holds the per-segment interval and job counters
-    and assembles BatchAggregation rows (segment = batch identifier)."""
+    """AggregationJobWriter's batch-aggregation half for one engine (aggregation_job_writer.rs:
+    476-553, 608-708). Per aggregation job, the engine turns the job's resident batch into one delta
+    per batch identifier (share, count, checksum of the job's finished reports:
+    jx_batch_aggregate_records, which changes nothing on the engine); inside a datastore transaction
+    the writer reads the rows at a random shard `ord` in [0, shard_count) and merges each delta into
+    the row it read (merged_with), together with the host-side bookkeeping: the client timestamp
+    interval over every report aggregation of the job (failed ones included) and the job counters.
+    Rows that are collected or scrubbed are not updated, and their reports fail with BatchCollected.
+    A retried transaction recomputes everything from the resident batch, so a retry writes exactly
+    what one attempt would."""
     field_bytes: int = 16
-    ord: int = 0
-    intervals: dict[int, Interval] = field(default_factory=dict)
-    jobs_created: dict[int, int] = field(default_factory=dict)
-    jobs_terminated: dict[int, int] = field(default_factory=dict)
+    shard_count: int = 1
+    datastore: Datastore = field(default_factory=Datastore)
+    seed: int = 0
 
-    def observe_report_aggregations(self, segments, times) -> None:
-        """Every report aggregation written for a batch identifier widens its client timestamp
-        interval, whatever its state (aggregation_job_writer.rs:641-663)."""
-        for s, t in zip(segments, times):
+    def __post_init__(self):
+        import random
+        self._rng = random.Random(self.seed)
+
+    def write_job(self, engine, batch_id: int, n: int, accept, segment_index, segment_ids: list[int],
+                  report_times: list[tuple[int, int]], initial_write: bool, terminal: bool,
+                  inject_failures: int = 0) -> set[int]:
+        """Write one aggregation job's batch aggregations. accept / segment_index: per row of the
+        engine batch (None: no engine batch, e.g. a job whose reports all failed before the
+        engine); segment_ids[k]: the batch identifier of dense index k; report_times: (batch
+        identifier, client time) of every report aggregation the job writes. Returns the batch
+        identifiers that were already collected (their reports fail with BatchCollected)."""
+        ids = list(dict.fromkeys(int(s) for s in segment_ids))
+        intervals: dict[int, Interval] = {}
+        for s, t in report_times:
             s = int(s)
-            self.intervals[s] = self.intervals.get(s, Interval.EMPTY).merge(Interval.from_time(int(t)))
+            intervals[s] = intervals.get(s, Interval.EMPTY).merge(Interval.from_time(int(t)))
+            if s not in ids:
+                ids.append(s)
+        dense = {s: k for k, s in enumerate(segment_ids)}
+        created = 1 if initial_write and not terminal else 0
+        terminated = 1 if not initial_write and terminal else 0
 
-    def observe_job(self, segments, initial_write: bool, terminal: bool) -> None:
-        """One aggregation job touching `segments`: InitialWrite of an in-progress job counts as
-        created, UpdateWrite into a terminal state as terminated (aggregation_job_writer.rs:335-420)."""
-        for s in set(int(x) for x in segments):
-            if initial_write and not terminal:
-                self.jobs_created[s] = self.jobs_created.get(s, 0) + 1
-            elif not initial_write and terminal:
-                self.jobs_terminated[s] = self.jobs_terminated.get(s, 0) + 1
+        def closure(tx) -> set[int]:
+            ord_ = self._rng.randrange(self.shard_count)
+            recs = (engine.aggregate_records(batch_id, n, accept, segment_index, len(segment_ids))
+                    if batch_id and n and segment_ids else [])
+            collected = set()
+            for s in ids:
+                row = tx.get((s, ord_))
+                if row is not None and row.state != AGGREGATING:
+                    collected.add(s)
+                    continue
+                share, cnt, cs = recs[dense[s]] if s in dense and recs else (None, 0, bytes(32))
+                delta = BatchAggregation(s, ord_, intervals.get(s, Interval.EMPTY), AGGREGATING,
+                                         share if cnt else None, cnt, cs, created, terminated, self.field_bytes)
+                tx[(s, ord_)] = delta if row is None else row.merged_with(delta)
+            return collected
 
-    def batch_aggregation(self, engine, segment: int) -> BatchAggregation:
-        agg, count, checksum = engine.aggregate_share(segment)
-        return BatchAggregation(segment, self.ord, self.intervals.get(segment, Interval.EMPTY), AGGREGATING,
-                                agg if count else None, count, checksum, self.jobs_created.get(segment, 0),
-                                self.jobs_terminated.get(segment, 0), self.field_bytes)
+        return self.datastore.run_tx(closure, inject_failures)
+
+    def batch_aggregation(self, segment: int) -> BatchAggregation:
+        """The batch identifier's rows merged over every shard ord (as collection merges them,
+        aggregate_share.rs:55-96)."""
+        rows = [r for (s, _), r in sorted(self.datastore.rows.items()) if s == segment]
+        if not rows:
+            return BatchAggregation(segment, field_bytes=self.field_bytes)
+        out = rows[0]
+        for r in rows[1:]:
+            out = out.merged_with(r)
+        return out
 
     def segments(self) -> list[int]:
-        return sorted(set(self.intervals) | set(self.jobs_created) | set(self.jobs_terminated))
+        return sorted({s for s, _ in self.datastore.rows})

@@ -1,9 +1,11 @@
 // jx_engine.cpp — host side of the C ABI in include/jx_prio3.h.
 //
-// Owns device staging, constant tables and per-segment batch aggregations; sequences
-// the K1 (XOF) -> K1' (slow path) -> K3 (FLP) -> K4 (accumulate) launches on one HIP
-// stream per engine. There is no CPU compute path: if the device or the kernels are
-// unavailable every entry point fails with an error status.
+// Owns device staging, constant tables, resident prepared batches and per-segment batch
+// aggregations; sequences the K1 (XOF) -> K1' (slow path) -> K3 (FLP) -> K4 (accumulate) launches
+// on one HIP stream per engine. Every entry point takes the engine mutex for the duration of the
+// call only, so concurrent aggregation jobs can share an engine (each holds a batch handle). There
+// is no CPU compute path: if the device or the kernels are unavailable every entry point fails with
+// an error status.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -14,6 +16,7 @@
 #include <set>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/jx_prio3.h"
@@ -25,10 +28,39 @@ using namespace jx;
 
 namespace {
 
+// One batch aggregation's device state (aggregate share, report count, ReportIdChecksum).
 struct Segment {
   uint4* agg = nullptr;                 // [out_len] canonical
   uint32_t* checksum = nullptr;         // [8]
   unsigned long long* count = nullptr;  // [1]
+};
+
+// A resident prepared batch: one aggregation job's reports after prepare_init, holding what
+// prepare_next and the accumulation need once the prepare call has returned. Staging (measurement
+// and proof shares, coefficients, FLP partials) is per-call scratch shared by every batch; the
+// output shares, verdicts, prep messages (leader: the corrected joint-rand seeds, its prepare state)
+// and report ids live here until jx_batch_release / jx_accumulate. Any number of batches can be
+// resident, so the aggregation jobs Janus steps concurrently (max_concurrent_job_workers,
+// aggregator/src/binary_utils/job_driver.rs:116-138; a leader job holds its prepare state across
+// the helper round trip, aggregation_job_driver.rs:396-416 -> :540-701) each keep their own.
+struct Batch {
+  uint64_t n = 0;
+  bool leader = false;
+  bool finished = false;      // leader: prepare_next has run (once)
+  void* mem = nullptr;        // one allocation: outs | verdicts | msgs | nonces
+  size_t bytes = 0;
+  uint4* outs = nullptr;      // interleaved [n/64][out_len][64] (Histogram: the measurement share)
+  uint8_t* verdicts = nullptr;
+  uint8_t* msgs = nullptr;
+  uint8_t* nonces = nullptr;  // report ids, for the checksums
+};
+
+// What an accumulation reads: output shares, verdicts, report ids of n reports.
+struct AccSrc {
+  uint64_t n;
+  const uint4* outs;
+  const uint8_t* verdicts;
+  const uint8_t* nonces;
 };
 
 enum { ST_XOF = 0, ST_FLP = 1, ST_ACC = 2, ST_SLOW = 3, NST = 4 };
@@ -39,6 +71,7 @@ struct jx_engine {
   Cfg cfg{};
   int device = 0;
   hipStream_t stream = nullptr;
+  std::mutex mu;  // held by every entry point for the duration of the call
   uint64_t cap = 0;  // reports (multiple of 64)
   uint64_t default_chunk = 0;
   uint64_t round_reports = 0;  // reports that fill every K1 wave slot once (0: unknown)
@@ -48,24 +81,26 @@ struct jx_engine {
   uint4 *d_meas = nullptr, *d_proof = nullptr, *d_outs = nullptr, *d_coef = nullptr, *d_consts = nullptr;
   uint32_t* d_flags = nullptr;
   uint4* d_part = nullptr;
-  uint8_t *d_verdicts = nullptr, *d_msgs = nullptr;
+  uint8_t *d_verdicts = nullptr, *d_msgs = nullptr;  // the fused paths' per-launch results
   // accumulation scratch: partials + selection bytes
   uint64_t* d_partials = nullptr;
   uint32_t acc_chunks = 0;  // report chunks of the accumulate kernel (0: acc_nchunks picks)
-  uint8_t* d_tmp = nullptr;  // output-share transpose / aggregate encode
+  uint8_t* d_tmp = nullptr;  // output-share transpose / aggregate encode / records
   size_t tmp_bytes = 0;
   uint8_t* d_mask = nullptr;
   uint32_t* d_seg = nullptr;
-  // leader role staging (allocated on first leader call): input shares, outbound prep
-  // shares, inbound prep messages; the corrected seeds (prepare state) live in d_msgs
+  // leader role staging (allocated on first leader call): input shares, outbound prep shares,
+  // inbound prep messages
   uint8_t *d_lis = nullptr, *d_lps_out = nullptr, *d_in_msgs = nullptr;
   uint64_t leader_cap = 0;
-  bool leader_batch = false;
-  std::map<uint32_t, Segment> segs;
-  uint64_t last_n = 0;
-  bool have_batch = false;
-  // every prepared batch gets a generation id; finish / accumulate name the batch they mean
-  uint64_t batch_gen = 0, batch_id = 0;
+  std::map<uint32_t, Segment> segs;  // running batch aggregations (the engine as one shard)
+  // resident prepared batches by handle; handles are never reused
+  std::map<uint64_t, Batch> batches;
+  uint64_t batch_gen = 0, last_batch = 0;
+  std::multimap<size_t, void*> batch_pool;  // released batch allocations, reused by later batches
+  // per-call batch-aggregation deltas (jx_batch_aggregate_records): agg [ns][out_len] | count [ns] | checksum [ns][8]
+  uint8_t* d_delta = nullptr;
+  size_t delta_bytes = 0;
   // segmented accumulation scratch (allocated on first use)
   uint32_t* d_segx = nullptr;  // cnt, off, cursor [SEG_MAX each], ioff [SEG_MAX + 1], nitems [2]
   uint32_t* d_perm = nullptr;
@@ -75,31 +110,21 @@ struct jx_engine {
   uint64_t spart_wmax = 0;
   void** d_ptrs = nullptr;  // [3][nptrs]: aggs, counts, checksums of the call's segments
   uint64_t ptrs_cap = 0;
-  std::vector<void*> h_ptrs;
+  // pinned host copies of the pointer table, double-buffered: buffer k is rewritten only after the
+  // upload that last read it has completed (ev_ptrs[k]), so no call waits for its own work
+  void** h_ptrs[2] = {nullptr, nullptr};
+  uint64_t h_ptrs_cap[2] = {0, 0};
+  hipEvent_t ev_ptrs[2] = {nullptr, nullptr};
+  int ptrs_k = 0;
   std::vector<uint32_t> h_dense;
   uint32_t* d_err = nullptr;  // combine kernels: non-canonical input seen (reported by jx_engine_sync)
-  // the nonces of the resident batch (device pointer; engine copy or caller's)
-  const uint8_t* batch_nonces = nullptr;
   // timing
   bool timing = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
   double ms[NST] = {0, 0, 0, 0};
   uint64_t launches[NST] = {0, 0, 0, 0};
   uint32_t force_slow = 0;
-  uint32_t k1_split = 0;  // helper K1 as squeeze-only + absorb-only launches (JX_K1_SPLIT, debug option 3)
-  uint32_t k3_pf = 21;    // K3 load pipeline variant (JX_K3_PF, debug option 4): the depth-4 LDS-DMA ring
-  // Overlapped fused path (multi-launch device calls): K3 + K4 of launch i run on stream2 while K1 of
-  // launch i+1 runs on stream, from a second staging set. Off by default: measured on MI355X
-  // (SumVec 8x1000/88, 5 launches per step) the concurrent kernels slow each other down more than they
-  // hide (K1 26.6 -> 36.1 ms, K3 8.4 -> 23.5 ms per launch; 7.00M -> 6.62M reports/s).
-  // JX_OVERLAP=1 / debug option 5 = 1 turn it on.
-  uint32_t overlap = 0;
-  uint4 *d_meas2 = nullptr, *d_proof2 = nullptr, *d_outs2 = nullptr, *d_coef2 = nullptr;
-  uint32_t* d_flags2 = nullptr;
-  uint4* d_part2 = nullptr;
-  uint64_t cap2 = 0;
-  hipStream_t stream2 = nullptr;
-  hipEvent_t ev_k1[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr}, ev_join = nullptr;
+  uint32_t k1_split = 0;  // helper K1: 0 automatic, 3 lane-split, 5 fused (JX_K1_SPLIT, debug option 3)
   std::string err;
 };
 
@@ -114,6 +139,8 @@ static int32_t fail(jx_engine* e, int32_t code, const std::string& msg) {
       return fail((e), _st == hipErrorOutOfMemory ? JX_E_NOMEM : JX_E_HIP,                                \
                   std::string(#call) + ": " + hipGetErrorString(_st));                                    \
   } while (0)
+#define LOCK(e) std::lock_guard<std::mutex> _lk((e)->mu)
+
 
 // ---------------------------------------------------------------------------- host field helpers
 
@@ -415,14 +442,6 @@ static void free_staging(jx_engine* e) {
   e->d_mask = nullptr;
   e->d_seg = nullptr;
   e->cap = 0;
-  void* ptrs2[] = {e->d_meas2, e->d_proof2, e->d_outs2, e->d_coef2, e->d_flags2, e->d_part2};
-  for (void* p : ptrs2)
-    if (p) (void)hipFree(p);
-  e->d_meas2 = e->d_proof2 = e->d_outs2 = e->d_coef2 = nullptr;
-  e->d_flags2 = nullptr;
-  e->d_part2 = nullptr;
-  e->cap2 = 0;
-  e->have_batch = false;
   for (uint8_t** p : {&e->d_lis, &e->d_lps_out, &e->d_in_msgs}) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
@@ -436,6 +455,8 @@ static uint64_t coef_elems(const Cfg& c) { return c.algo == ALGO_SUMVEC_F64_MULT
 static uint64_t part_bytes(const Cfg& c) {
   return c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? 24ull * c.np * c.ngroups : 64ull * c.ngt;
 }
+// the output shares alias the measurement-share staging (Histogram: output = measurement share)
+static bool outs_alias_meas(const Cfg& c) { return c.out_is_meas && c.algo != ALGO_COUNT; }
 
 static uint64_t per_report_bytes(const Cfg& c) {
   uint64_t b = (uint64_t)stage_eb(c) * (c.meas_len + (uint64_t)c.np * c.proof_len + coef_elems(c));
@@ -455,6 +476,7 @@ static uint32_t acc_nchunks(const jx_engine* e) {
 
 static int32_t ensure_capacity(jx_engine* e, uint64_t n) {
   if (n <= e->cap) return JX_OK;
+  HIPCHK(e, hipStreamSynchronize(e->stream));  // queued work may still read the old staging
   free_staging(e);
   const Cfg& c = e->cfg;
   uint64_t cap = (n + 63) / 64 * 64;
@@ -466,7 +488,7 @@ static int32_t ensure_capacity(jx_engine* e, uint64_t n) {
   const uint64_t eb = stage_eb(c);
   HIPCHK(e, A((void**)&e->d_meas, cap * c.meas_len * eb));
   HIPCHK(e, A((void**)&e->d_proof, cap * c.np * c.proof_len * eb));
-  if (c.algo == ALGO_COUNT || !c.out_is_meas) HIPCHK(e, A((void**)&e->d_outs, cap * c.out_len * 16));
+  if (!outs_alias_meas(c)) HIPCHK(e, A((void**)&e->d_outs, cap * c.out_len * 16));
   HIPCHK(e, A((void**)&e->d_coef, cap * coef_elems(c) * eb));
   HIPCHK(e, A((void**)&e->d_flags, cap * 4));
   HIPCHK(e, A((void**)&e->d_part, cap * part_bytes(c)));
@@ -481,35 +503,8 @@ static int32_t ensure_capacity(jx_engine* e, uint64_t n) {
   return JX_OK;
 }
 
-// The second staging set of the overlapped fused path (same shapes as the first; cap reports). Returns
-// false, with nothing allocated, when the device cannot hold it: the caller then runs serially.
-static bool ensure_second_set(jx_engine* e) {
-  if (e->cap2 >= e->cap && e->d_meas2) return true;
-  const Cfg& c = e->cfg;
-  const uint64_t cap = e->cap, eb = stage_eb(c);
-  auto A = [&](void** p, size_t bytes) { return hipMalloc(p, bytes ? bytes : 16) == hipSuccess; };
-  bool ok = A((void**)&e->d_meas2, cap * c.meas_len * eb) && A((void**)&e->d_proof2, cap * c.np * c.proof_len * eb) &&
-            ((c.algo != ALGO_COUNT && c.out_is_meas) || A((void**)&e->d_outs2, cap * c.out_len * 16)) &&
-            A((void**)&e->d_coef2, cap * coef_elems(c) * eb) && A((void**)&e->d_flags2, cap * 4) &&
-            A((void**)&e->d_part2, cap * part_bytes(c));
-  if (ok) ok = hipMemsetAsync(e->d_flags2, 0, cap * 4, e->stream) == hipSuccess;
-  if (ok && !e->stream2) ok = hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) == hipSuccess;
-  for (hipEvent_t* ev : {&e->ev_k1[0], &e->ev_k1[1], &e->ev_free[0], &e->ev_free[1], &e->ev_join})
-    if (ok && !*ev) ok = hipEventCreateWithFlags(ev, hipEventDisableTiming) == hipSuccess;
-  if (!ok) {
-    void* ptrs2[] = {e->d_meas2, e->d_proof2, e->d_outs2, e->d_coef2, e->d_flags2, e->d_part2};
-    for (void* p : ptrs2)
-      if (p) (void)hipFree(p);
-    e->d_meas2 = e->d_proof2 = e->d_outs2 = e->d_coef2 = nullptr;
-    e->d_flags2 = nullptr;
-    e->d_part2 = nullptr;
-    e->cap2 = 0;
-    (void)hipGetLastError();  // the failed allocation is not an engine error
-    return false;
-  }
-  e->cap2 = cap;
-  return true;
-}
+// the fused paths' output shares (engine staging)
+static uint4* staging_outs(jx_engine* e) { return outs_alias_meas(e->cfg) ? e->d_meas : e->d_outs; }
 
 static int32_t get_segment(jx_engine* e, uint32_t id, Segment** out) {
   auto it = e->segs.find(id);
@@ -529,6 +524,7 @@ static int32_t get_segment(jx_engine* e, uint32_t id, Segment** out) {
 
 static int32_t ensure_tmp(jx_engine* e, size_t bytes) {
   if (bytes <= e->tmp_bytes) return JX_OK;
+  HIPCHK(e, hipStreamSynchronize(e->stream));
   if (e->d_tmp) (void)hipFree(e->d_tmp);
   e->d_tmp = nullptr;
   e->tmp_bytes = 0;
@@ -537,35 +533,86 @@ static int32_t ensure_tmp(jx_engine* e, size_t bytes) {
   return JX_OK;
 }
 
-// Reports per launch for an n-report fused call: the fewest launches that fit the staging
-// budget (default_chunk), split evenly (multiple of 64) so every launch has the same shape.
-// When the chunk is a whole number of K1 rounds (round_reports), launches are full chunks and
-// only the last one carries a partial round (1.25M SumVec reports: 4 x 262,144 + 201,424
-// instead of 4 x 312,500). Measured on MI355X: K1 time per report is unchanged (its waves do
-// not finish in lockstep rounds), the step went 188.4 -> 184.6 ms, within run-to-run noise.
-static uint64_t launch_chunk(const jx_engine* e, uint64_t n) {
-  if (n <= e->default_chunk) return n;
-  if (e->round_reports && e->default_chunk % e->round_reports == 0) return e->default_chunk;
-  const uint64_t launches = (n + e->default_chunk - 1) / e->default_chunk;
-  const uint64_t per = (n + launches - 1) / launches;
-  return (per + 63) / 64 * 64;
+// ---------------------------------------------------------------------------- resident batches
+
+static size_t align256(size_t v) { return (v + 255) / 256 * 256; }
+
+// A new resident batch of n reports (handle in *id). Allocations of released batches are reused when
+// they fit (stream-ordered: every use of a batch is on the engine stream).
+static int32_t batch_new(jx_engine* e, uint64_t n, bool leader, uint64_t* id, Batch** out) {
+  const Cfg& c = e->cfg;
+  const uint64_t cap = (n + 63) / 64 * 64;
+  const size_t o_outs = 0, o_ver = align256((size_t)cap * c.out_len * 16), o_msg = o_ver + align256(cap),
+               o_non = o_msg + align256((size_t)cap * c.seed), bytes = o_non + align256(cap * 16);
+  Batch b;
+  b.n = n;
+  b.leader = leader;
+  auto it = e->batch_pool.lower_bound(bytes);
+  if (it != e->batch_pool.end() && it->first <= 2 * bytes + (1u << 20)) {
+    b.mem = it->second;
+    b.bytes = it->first;
+    e->batch_pool.erase(it);
+  } else {
+    HIPCHK(e, hipMalloc(&b.mem, bytes ? bytes : 256));
+    b.bytes = bytes;
+  }
+  uint8_t* m = (uint8_t*)b.mem;
+  b.outs = (uint4*)(m + o_outs);
+  b.verdicts = m + o_ver;
+  b.msgs = m + o_msg;
+  b.nonces = m + o_non;
+  *id = ++e->batch_gen;
+  e->last_batch = *id;
+  *out = &e->batches.emplace(*id, b).first->second;
+  return JX_OK;
 }
+
+// Keep at most this many bytes of released batch allocations for reuse.
+static constexpr size_t BATCH_POOL_MAX = 8ull << 30;
+
+static void batch_free(jx_engine* e, std::map<uint64_t, Batch>::iterator it) {
+  Batch& b = it->second;
+  size_t pooled = 0;
+  for (auto& kv : e->batch_pool) pooled += kv.first;
+  if (b.mem) {
+    if (pooled + b.bytes <= BATCH_POOL_MAX) {
+      e->batch_pool.emplace(b.bytes, b.mem);
+    } else {
+      (void)hipStreamSynchronize(e->stream);  // queued work may still read it
+      (void)hipFree(b.mem);
+    }
+  }
+  if (e->last_batch == it->first) e->last_batch = 0;
+  e->batches.erase(it);
+}
+
+static int32_t find_batch(jx_engine* e, uint64_t id, uint64_t n, const char* what, Batch** out) {
+  auto it = e->batches.find(id);
+  if (id == 0 || it == e->batches.end())
+    return fail(e, JX_E_STATE, std::string(what) + ": batch id names no resident prepared batch (released or never made)");
+  if (it->second.n != n)
+    return fail(e, JX_E_INVALID, std::string(what) + ": report count differs from the batch's");
+  *out = &it->second;
+  return JX_OK;
+}
+
+static AccSrc batch_src(const Batch& b) { return AccSrc{b.n, b.outs, b.verdicts, b.nonces}; }
 
 // ---------------------------------------------------------------------------- timing
 
-static hipError_t stage_begin(jx_engine* e, hipEvent_t* ev, hipStream_t s = nullptr) {
+static hipError_t stage_begin(jx_engine* e, hipEvent_t* ev) {
   if (!e->timing) return hipSuccess;
   hipError_t st = hipEventCreate(ev);
   if (st != hipSuccess) return st;
-  return hipEventRecord(*ev, s ? s : e->stream);
+  return hipEventRecord(*ev, e->stream);
 }
-static hipError_t stage_end(jx_engine* e, int stage, hipEvent_t ev0, hipStream_t s = nullptr) {
+static hipError_t stage_end(jx_engine* e, int stage, hipEvent_t ev0) {
   e->launches[stage]++;
   if (!e->timing) return hipSuccess;
   hipEvent_t ev1;
   hipError_t st = hipEventCreate(&ev1);
   if (st != hipSuccess) return st;
-  st = hipEventRecord(ev1, s ? s : e->stream);
+  st = hipEventRecord(ev1, e->stream);
   e->pending.push_back({stage, {ev0, ev1}});
   return st;
 }
@@ -585,17 +632,14 @@ static int32_t drain_timing(jx_engine* e) {
 
 // ---------------------------------------------------------------------------- core sequencing
 
-// Prepare n <= cap reports whose inputs are at the given device pointers.
-// set: staging set (1 = the overlapped path's second set); parts: 1 = the XOF stage (K1, K1') on sx,
-// 2 = the FLP stage (K3) on sf, 3 = both (default streams: the engine stream).
+// Prepare n <= cap reports whose inputs are at the given device pointers; the output shares go to
+// outs (a batch's buffer, or the staging of the fused paths), verdicts and prep messages / leader
+// seeds to verdicts / msgs.
 static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* his,
-                         const uint8_t* lps, uint8_t* verdicts, uint8_t* msgs, const uint8_t* lis = nullptr,
-                         uint8_t* lps_out = nullptr, int set = 0, int parts = 3, hipStream_t sx = nullptr,
-                         hipStream_t sf = nullptr) {
+                         const uint8_t* lps, uint8_t* verdicts, uint8_t* msgs, uint4* outs,
+                         const uint8_t* lis = nullptr, uint8_t* lps_out = nullptr) {
   const Cfg& c = e->cfg;
   const bool leader = lis != nullptr;
-  if (!sx) sx = e->stream;
-  if (!sf) sf = e->stream;
   Bufs b{};
   b.n = n;
   b.nonces = nonces;
@@ -605,12 +649,12 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
   b.lis = lis;
   b.lps_out = lps_out;
   b.leader = leader ? 1u : 0u;
-  b.meas = set ? e->d_meas2 : e->d_meas;
-  b.proof = set ? e->d_proof2 : e->d_proof;
-  b.outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? b.meas : (set ? e->d_outs2 : e->d_outs);
-  b.coef = set ? e->d_coef2 : e->d_coef;
-  b.flags = set ? e->d_flags2 : e->d_flags;
-  b.part = set ? e->d_part2 : e->d_part;
+  b.meas = outs_alias_meas(c) ? outs : e->d_meas;
+  b.proof = e->d_proof;
+  b.outs = outs;
+  b.coef = e->d_coef;
+  b.flags = e->d_flags;
+  b.part = e->d_part;
   b.verdicts = verdicts;
   b.msgs = msgs;
   b.consts = e->d_consts;
@@ -621,7 +665,6 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
   // (FixedPointBoundedL2VecSum 16 x 10000, 24,576 reports: 153 -> 92 ms on MI355X).
   const bool wide = c.bits > 32 && (c.algo == ALGO_SUM || c.algo == ALGO_SUMVEC);
   if (e->k1_split == 0 && !leader && !wide && e->round_reports && 2 * n < e->round_reports) b.k1_split = 3;
-  b.k3_pf = e->k3_pf;
   hipEvent_t ev = nullptr;
   if (c.algo == ALGO_COUNT) {
     HIPCHK(e, stage_begin(e, &ev));
@@ -640,24 +683,18 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
     HIPCHK(e, launch_mp_flp(c, b, e->stream));
     HIPCHK(e, stage_end(e, ST_FLP, ev));
   } else {
-    if (parts & 1) {
-      HIPCHK(e, stage_begin(e, &ev, sx));
-      HIPCHK(e, launch_xof(c, b, sx));
-      HIPCHK(e, stage_end(e, ST_XOF, ev, sx));
-      if (!leader) {  // the leader's shares are explicit: no rejection-sampled streams to redo
-        HIPCHK(e, stage_begin(e, &ev, sx));
-        HIPCHK(e, launch_xof_slow(c, b, sx));
-        HIPCHK(e, stage_end(e, ST_SLOW, ev, sx));
-      }
+    HIPCHK(e, stage_begin(e, &ev));
+    HIPCHK(e, launch_xof(c, b, e->stream));
+    HIPCHK(e, stage_end(e, ST_XOF, ev));
+    if (!leader) {  // the leader's shares are explicit: no rejection-sampled streams to redo
+      HIPCHK(e, stage_begin(e, &ev));
+      HIPCHK(e, launch_xof_slow(c, b, e->stream));
+      HIPCHK(e, stage_end(e, ST_SLOW, ev));
     }
-    if (parts & 2) {
-      HIPCHK(e, stage_begin(e, &ev, sf));
-      HIPCHK(e, launch_flp(c, b, sf));
-      HIPCHK(e, stage_end(e, ST_FLP, ev, sf));
-    }
+    HIPCHK(e, stage_begin(e, &ev));
+    HIPCHK(e, launch_flp(c, b, e->stream));
+    HIPCHK(e, stage_end(e, ST_FLP, ev));
   }
-  e->batch_nonces = nonces;
-  e->leader_batch = leader;
   return JX_OK;
 }
 
@@ -665,6 +702,7 @@ static int32_t ensure_leader_capacity(jx_engine* e, uint64_t n) {
   int32_t rc = ensure_capacity(e, n);
   if (rc) return rc;
   if (n <= e->leader_cap && e->d_lis) return JX_OK;
+  HIPCHK(e, hipStreamSynchronize(e->stream));
   for (uint8_t** p : {&e->d_lis, &e->d_lps_out, &e->d_in_msgs}) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
@@ -678,39 +716,64 @@ static int32_t ensure_leader_capacity(jx_engine* e, uint64_t n) {
   return JX_OK;
 }
 
-// Single-segment accumulate into aggregation seg_id. With d_seg (dense indices), only reports whose
-// index is 0 are taken.
-// st / set / nonces: the overlapped path's stream, staging set and launch nonces (default: the engine
-// stream, set 0 and the resident batch's nonces)
-static int32_t accumulate_core(jx_engine* e, uint64_t n, const uint8_t* verdicts, const uint8_t* d_mask,
-                               const uint32_t* d_seg, uint32_t seg_id, bool dense = false, hipStream_t st = nullptr,
-                               int set = 0, const uint8_t* nonces = nullptr) {
+// Accumulate the finished (and, with d_mask, accepted) reports of src into one aggregation. With
+// d_dense (dense per-report indices), only reports whose index is 0 are taken.
+static int32_t accumulate_one(jx_engine* e, const AccSrc& src, const uint8_t* d_mask, const uint32_t* d_dense,
+                              const Segment& t) {
   const Cfg& c = e->cfg;
-  Segment* s = nullptr;
-  int32_t rc = get_segment(e, seg_id, &s);
-  if (rc) return rc;
-  if (!st) st = e->stream;
   AccArgs a{};
-  a.n = n;
-  uint4* meas = set ? e->d_meas2 : e->d_meas;
-  a.outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? meas : (set ? e->d_outs2 : e->d_outs);
+  a.n = src.n;
+  a.outs = src.outs;
   a.out_len = c.out_len;
-  a.verdicts = verdicts;
+  a.verdicts = src.verdicts;
   a.mask = d_mask;
-  a.seg = d_seg;
-  a.seg_id = dense ? 0u : seg_id;
+  a.seg = d_dense;
+  a.seg_id = 0;
   a.partials = e->d_partials;
   a.nchunks = acc_nchunks(e);
-  uint64_t nblk = (n + 63) / 64;
+  uint64_t nblk = (src.n + 63) / 64;
   a.blocks_per_chunk = (uint32_t)((nblk + a.nchunks - 1) / a.nchunks);
   if (a.blocks_per_chunk == 0) a.blocks_per_chunk = 1;
-  a.nonces = nonces ? nonces : e->batch_nonces;
-  a.checksum = s->checksum;
-  a.count = s->count;
+  a.nonces = src.nonces;
+  a.checksum = t.checksum;
+  a.count = t.count;
   hipEvent_t ev = nullptr;
-  HIPCHK(e, stage_begin(e, &ev, st));
-  HIPCHK(e, launch_accumulate(c, a, s->agg, st));
-  HIPCHK(e, stage_end(e, ST_ACC, ev, st));
+  HIPCHK(e, stage_begin(e, &ev));
+  HIPCHK(e, launch_accumulate(c, a, t.agg, e->stream));
+  HIPCHK(e, stage_end(e, ST_ACC, ev));
+  return JX_OK;
+}
+
+// Upload the device pointer table (aggs, counts, checksums) of `targets` into d_ptrs. The pinned host
+// copy is double-buffered and reused only once the upload that last read it has completed, so the
+// host never waits for the call's own kernels.
+static int32_t upload_targets(jx_engine* e, const std::vector<Segment>& targets) {
+  const uint64_t S = targets.size();
+  if (e->ptrs_cap < S) {
+    HIPCHK(e, hipStreamSynchronize(e->stream));  // kernels may still read the old table
+    if (e->d_ptrs) (void)hipFree(e->d_ptrs);
+    e->d_ptrs = nullptr;
+    HIPCHK(e, hipMalloc((void**)&e->d_ptrs, 3 * S * sizeof(void*)));
+    e->ptrs_cap = S;
+  }
+  const int k = e->ptrs_k;
+  e->ptrs_k ^= 1;
+  if (!e->ev_ptrs[k]) HIPCHK(e, hipEventCreateWithFlags(&e->ev_ptrs[k], hipEventDisableTiming));
+  else HIPCHK(e, hipEventSynchronize(e->ev_ptrs[k]));
+  if (e->h_ptrs_cap[k] < S) {
+    if (e->h_ptrs[k]) (void)hipHostFree(e->h_ptrs[k]);
+    e->h_ptrs[k] = nullptr;
+    HIPCHK(e, hipHostMalloc((void**)&e->h_ptrs[k], 3 * S * sizeof(void*), hipHostMallocDefault));
+    e->h_ptrs_cap[k] = S;
+  }
+  void** h = e->h_ptrs[k];
+  for (uint64_t t = 0; t < S; t++) {
+    h[t] = targets[t].agg;
+    h[S + t] = targets[t].count;
+    h[2 * S + t] = targets[t].checksum;
+  }
+  HIPCHK(e, hipMemcpyAsync(e->d_ptrs, h, 3 * S * sizeof(void*), hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipEventRecord(e->ev_ptrs[k], e->stream));
   return JX_OK;
 }
 
@@ -722,15 +785,14 @@ static uint32_t seg_items_len(const jx_engine* e, uint64_t n) {
   return (uint32_t)(L < 64 ? 64 : L);
 }
 
-// Accumulate the finished, accepted reports of a prepared batch into the aggregations named by a
-// dense per-report segment index d_dense[r] in [0, ids.size()) (segment ids[d]); one pass per
-// SEG_MAX segments. The device pointer table is uploaded once per call.
-static int32_t accumulate_segmented(jx_engine* e, uint64_t n, const uint8_t* verdicts, const uint8_t* d_mask,
-                                    const uint32_t* d_dense, const std::vector<uint32_t>& ids) {
+// Accumulate the finished, accepted reports of src into the aggregations named by a dense per-report
+// index d_dense[r] in [0, S) (S = segments of the table uploaded by upload_targets; indices >= S are
+// skipped); one pass per SEG_MAX segments.
+static int32_t accumulate_many(jx_engine* e, const AccSrc& src, const uint8_t* d_mask, const uint32_t* d_dense,
+                               uint64_t S) {
   const Cfg& c = e->cfg;
-  const uint64_t S = ids.size();
+  const uint64_t n = src.n;
   if (S == 0 || n == 0) return JX_OK;
-  HIPCHK(e, hipStreamSynchronize(e->stream));  // h_ptrs may still feed an earlier async upload
   // per-pass segments: SEG_MAX, or fewer when the per-item partials would exceed ~512 MiB
   const uint32_t L = seg_items_len(e, n);
   const uint64_t items_n = (n + L - 1) / L;
@@ -740,6 +802,7 @@ static int32_t accumulate_segmented(jx_engine* e, uint64_t n, const uint8_t* ver
   if (ns_max > SEG_MAX) ns_max = SEG_MAX;
   const uint64_t wmax = items_n + (S < ns_max ? S : ns_max);
   if (!e->d_segx) HIPCHK(e, hipMalloc((void**)&e->d_segx, (4 * SEG_MAX + 3) * sizeof(uint32_t)));
+  if (e->perm_cap < n || e->spart_wmax < wmax) HIPCHK(e, hipStreamSynchronize(e->stream));
   if (e->perm_cap < n) {
     if (e->d_perm) (void)hipFree(e->d_perm);
     e->d_perm = nullptr;
@@ -755,37 +818,21 @@ static int32_t accumulate_segmented(jx_engine* e, uint64_t n, const uint8_t* ver
     HIPCHK(e, hipMalloc((void**)&e->d_spart, wmax * per_item));
     e->spart_wmax = wmax;
   }
-  if (e->ptrs_cap < S) {
-    if (e->d_ptrs) (void)hipFree(e->d_ptrs);
-    e->d_ptrs = nullptr;
-    HIPCHK(e, hipMalloc((void**)&e->d_ptrs, 3 * S * sizeof(void*)));
-    e->ptrs_cap = S;
-  }
-  e->h_ptrs.assign(3 * S, nullptr);
-  for (uint64_t t = 0; t < S; t++) {
-    Segment* sg = nullptr;
-    int32_t rc = get_segment(e, ids[t], &sg);
-    if (rc) return rc;
-    e->h_ptrs[t] = sg->agg;
-    e->h_ptrs[S + t] = sg->count;
-    e->h_ptrs[2 * S + t] = sg->checksum;
-  }
-  HIPCHK(e, hipMemcpyAsync(e->d_ptrs, e->h_ptrs.data(), 3 * S * sizeof(void*), hipMemcpyHostToDevice, e->stream));
   uint64_t grid = (n + 255) / 256;
   if (grid > SELECT_WGS) grid = SELECT_WGS;
   for (uint64_t s0 = 0; s0 < S; s0 += ns_max) {
     const uint32_t ns = (uint32_t)(S - s0 < ns_max ? S - s0 : ns_max);
     SegArgs a{};
     a.n = n;
-    a.outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? e->d_meas : e->d_outs;
+    a.outs = src.outs;
     a.out_len = c.out_len;
     a.fb = c.fb;
-    a.verdicts = verdicts;
+    a.verdicts = src.verdicts;
     a.mask = d_mask;
     a.seg = d_dense;
     a.s0 = (uint32_t)s0;
     a.ns = ns;
-    a.nonces = e->batch_nonces;
+    a.nonces = src.nonces;
     a.cnt = e->d_segx;
     a.off = e->d_segx + SEG_MAX;
     a.cursor = e->d_segx + 2 * SEG_MAX;
@@ -823,18 +870,70 @@ static void densify(const uint32_t* seg, uint64_t n, std::vector<uint32_t>& dens
   }
 }
 
-// Accumulate the resident batch into segment_ids[d_dense[r]] (d_dense nullable: all into
-// segment_ids[0]). One segment takes the coalesced select/accumulate path.
-static int32_t accumulate_any(jx_engine* e, uint64_t n, const uint8_t* verdicts, const uint8_t* d_mask,
-                              const uint32_t* d_dense, const std::vector<uint32_t>& ids) {
-  if (ids.size() == 1 || !d_dense) return accumulate_core(e, n, verdicts, d_mask, d_dense, ids[0], d_dense != nullptr);
-  return accumulate_segmented(e, n, verdicts, d_mask, d_dense, ids);
+// The running aggregations named by a caller's segment-id table. A repeated id would make two
+// segmented-reduce rows update one aggregation without atomics: refused.
+static int32_t segment_targets(jx_engine* e, const uint32_t* ids, uint64_t nids, std::vector<Segment>& out) {
+  std::unordered_set<uint32_t> seen;
+  out.clear();
+  for (uint64_t t = 0; t < nids; t++) {
+    if (!seen.insert(ids[t]).second)
+      return fail(e, JX_E_INVALID, "segment_ids holds a repeated batch-aggregation id");
+    Segment* s = nullptr;
+    int32_t rc = get_segment(e, ids[t], &s);
+    if (rc) return rc;
+    out.push_back(*s);
+  }
+  return JX_OK;
 }
 
-static int32_t check_batch(jx_engine* e, uint64_t batch_id, uint64_t n, const char* what) {
-  if (batch_id == 0 || batch_id != e->batch_id || !e->have_batch || n != e->last_n)
-    return fail(e, JX_E_STATE, std::string(what) + ": batch id / size does not name the resident prepared batch");
+// Accumulate src into targets[d_dense[r]] (d_dense nullable: all into targets[0]). One target takes the
+// coalesced select/accumulate path; several upload their pointer table (unless `uploaded`).
+static int32_t accumulate_into(jx_engine* e, const AccSrc& src, const uint8_t* d_mask, const uint32_t* d_dense,
+                               const std::vector<Segment>& targets, bool uploaded = false) {
+  if (src.n == 0 || targets.empty()) return JX_OK;
+  if (targets.size() == 1 || !d_dense) return accumulate_one(e, src, d_mask, d_dense, targets[0]);
+  if (!uploaded) {
+    int32_t rc = upload_targets(e, targets);
+    if (rc) return rc;
+  }
+  return accumulate_many(e, src, d_mask, d_dense, targets.size());
+}
+
+// Per-call delta aggregations (zeroed): ns contiguous segment states in d_delta.
+static int32_t delta_targets(jx_engine* e, uint32_t ns, std::vector<Segment>& out) {
+  const size_t agg_b = (size_t)ns * e->cfg.out_len * 16, bytes = agg_b + (size_t)ns * 8 + (size_t)ns * 32;
+  if (bytes > e->delta_bytes) {
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->d_delta) (void)hipFree(e->d_delta);
+    e->d_delta = nullptr;
+    e->delta_bytes = 0;
+    HIPCHK(e, hipMalloc((void**)&e->d_delta, bytes));
+    e->delta_bytes = bytes;
+  }
+  HIPCHK(e, hipMemsetAsync(e->d_delta, 0, bytes, e->stream));
+  out.resize(ns);
+  for (uint32_t s = 0; s < ns; s++) {
+    out[s].agg = (uint4*)e->d_delta + (size_t)s * e->cfg.out_len;
+    out[s].count = (unsigned long long*)(e->d_delta + agg_b) + s;
+    out[s].checksum = (uint32_t*)(e->d_delta + agg_b + (size_t)ns * 8) + 8 * s;
+  }
   return JX_OK;
+}
+
+static uint32_t record_bytes(const Cfg& c) { return c.out_len * c.fb + 40u; }
+
+// Reports per launch for an n-report fused call: the fewest launches that fit the staging
+// budget (default_chunk), split evenly (multiple of 64) so every launch has the same shape.
+// When the chunk is a whole number of K1 rounds (round_reports), launches are full chunks and
+// only the last one carries a partial round (1.25M SumVec reports: 4 x 262,144 + 201,424
+// instead of 4 x 312,500). Measured on MI355X: K1 time per report is unchanged (its waves do
+// not finish in lockstep rounds), the step went 188.4 -> 184.6 ms, within run-to-run noise.
+static uint64_t launch_chunk(const jx_engine* e, uint64_t n) {
+  if (n <= e->default_chunk) return n;
+  if (e->round_reports && e->default_chunk % e->round_reports == 0) return e->default_chunk;
+  const uint64_t launches = (n + e->default_chunk - 1) / e->default_chunk;
+  const uint64_t per = (n + launches - 1) / launches;
+  return (per + 63) / 64 * 64;
 }
 
 // ---------------------------------------------------------------------------- C ABI
@@ -880,7 +979,7 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
   const uint64_t per = per_report_bytes(e->cfg);
   if (const char* env = getenv("JX_K1_SPLIT")) {
     const int v = atoi(env);
-    if (v >= 0 && v <= 5) e->k1_split = (uint32_t)v;
+    if (v == 0 || v == 3 || v == 5) e->k1_split = (uint32_t)v;
   }
   e->round_reports = k1_round_reports(e->cfg, device, e->k1_split);
   uint64_t budget = 48ull << 30;
@@ -905,11 +1004,6 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
     if (v >= 64) chunk = v / 64 * 64;
   }
   e->default_chunk = chunk;
-  if (const char* env = getenv("JX_OVERLAP")) e->overlap = atoi(env) != 0;
-  if (const char* env = getenv("JX_K3_PF")) {
-    const int v = atoi(env);
-    if (v == 1 || v == 2 || v == 12 || v == 13 || (v >= 20 && v <= 26 && v != 24)) e->k3_pf = (uint32_t)v;  // 22/23/25: timing probes
-  }
   *out = e;
   return JX_OK;
 }
@@ -917,10 +1011,7 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
 void jx_engine_destroy(jx_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
-  if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  for (hipEvent_t ev : {e->ev_k1[0], e->ev_k1[1], e->ev_free[0], e->ev_free[1], e->ev_join})
-    if (ev) (void)hipEventDestroy(ev);
   for (auto& p : e->pending) {
     (void)hipEventDestroy(p.second.first);
     (void)hipEventDestroy(p.second.second);
@@ -931,15 +1022,18 @@ void jx_engine_destroy(jx_engine* e) {
     (void)hipFree(kv.second.checksum);
     (void)hipFree(kv.second.count);
   }
+  for (auto& kv : e->batches)
+    if (kv.second.mem) (void)hipFree(kv.second.mem);
+  for (auto& kv : e->batch_pool) (void)hipFree(kv.second);
   if (e->d_consts) (void)hipFree(e->d_consts);
   if (e->d_tmp) (void)hipFree(e->d_tmp);
   for (void* q : {(void*)e->d_segx, (void*)e->d_perm, (void*)e->d_items, (void*)e->d_spart, (void*)e->d_ptrs,
-                  (void*)e->d_err})
+                  (void*)e->d_err, (void*)e->d_delta})
     if (q) (void)hipFree(q);
-  if (e->d_lis) (void)hipFree(e->d_lis);
-  if (e->d_lps_out) (void)hipFree(e->d_lps_out);
-  if (e->d_in_msgs) (void)hipFree(e->d_in_msgs);
-  if (e->stream2) (void)hipStreamDestroy(e->stream2);
+  for (int k = 0; k < 2; k++) {
+    if (e->h_ptrs[k]) (void)hipHostFree(e->h_ptrs[k]);
+    if (e->ev_ptrs[k]) (void)hipEventDestroy(e->ev_ptrs[k]);
+  }
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -959,55 +1053,101 @@ int32_t jx_engine_sizes(const jx_engine* e, uint32_t* ps, uint32_t* his, uint32_
 
 int32_t jx_engine_set_capacity(jx_engine* e, uint64_t reports) {
   if (!e) return JX_E_INVALID;
+  LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
   return ensure_capacity(e, reports);
 }
 
-int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
-                             const uint8_t* helper_input_shares, const uint8_t* leader_prep_shares,
-                             uint8_t* out_prep_msgs, uint8_t* out_verdicts, uint8_t* out_output_shares) {
-  if (!e || !nonces || !helper_input_shares || !leader_prep_shares || !out_verdicts) return JX_E_INVALID;
-  const Cfg& c = e->cfg;
-  if (c.ps_bytes && !public_shares) return JX_E_INVALID;
-  e->have_batch = false;
-  e->batch_id = 0;
-  if (n == 0) {
-    e->have_batch = true;
-    e->leader_batch = false;
-    e->last_n = 0;
-    e->batch_id = ++e->batch_gen;
-    return JX_OK;
+// Release batch `id` when a prepare call fails after creating it.
+static int32_t drop_on_error(jx_engine* e, uint64_t id, int32_t rc) {
+  if (rc) {
+    auto it = e->batches.find(id);
+    if (it != e->batches.end()) batch_free(e, it);
   }
-  HIPCHK(e, hipSetDevice(e->device));
+  return rc;
+}
+
+static int32_t copy_out_shares(jx_engine* e, const uint4* outs, uint64_t n, uint8_t* dst) {
+  const Cfg& c = e->cfg;
+  int32_t rc = ensure_tmp(e, n * c.out_len * c.fb);
+  if (rc) return rc;
+  HIPCHK(e, launch_transpose_out(c, outs, n, e->d_tmp, e->stream));
+  HIPCHK(e, hipMemcpyAsync(dst, e->d_tmp, n * c.out_len * c.fb, hipMemcpyDeviceToHost, e->stream));
+  return JX_OK;
+}
+
+static int32_t helper_prep_batch_locked(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps,
+                                        const uint8_t* his, const uint8_t* lps, uint8_t* out_msgs, uint8_t* out_verdicts,
+                                        uint8_t* out_shares, uint64_t id, Batch* B) {
+  const Cfg& c = e->cfg;
   int32_t rc = ensure_capacity(e, n);
   if (rc) return rc;
-  HIPCHK(e, hipMemcpyAsync(e->d_nonces, nonces, n * 16, hipMemcpyHostToDevice, e->stream));
-  if (c.ps_bytes) HIPCHK(e, hipMemcpyAsync(e->d_ps, public_shares, n * c.ps_bytes, hipMemcpyHostToDevice, e->stream));
-  HIPCHK(e, hipMemcpyAsync(e->d_his, helper_input_shares, n * c.his_bytes, hipMemcpyHostToDevice, e->stream));
-  HIPCHK(e, hipMemcpyAsync(e->d_lps, leader_prep_shares, n * c.lps_bytes, hipMemcpyHostToDevice, e->stream));
-  rc = prep_core(e, n, e->d_nonces, e->d_ps, e->d_his, e->d_lps, e->d_verdicts, e->d_msgs);
+  HIPCHK(e, hipMemcpyAsync(B->nonces, nonces, n * 16, hipMemcpyHostToDevice, e->stream));
+  if (c.ps_bytes) HIPCHK(e, hipMemcpyAsync(e->d_ps, ps, n * c.ps_bytes, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipMemcpyAsync(e->d_his, his, n * c.his_bytes, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipMemcpyAsync(e->d_lps, lps, n * c.lps_bytes, hipMemcpyHostToDevice, e->stream));
+  rc = prep_core(e, n, B->nonces, e->d_ps, e->d_his, e->d_lps, B->verdicts, B->msgs, B->outs);
   if (rc) return rc;
-  HIPCHK(e, hipMemcpyAsync(out_verdicts, e->d_verdicts, n, hipMemcpyDeviceToHost, e->stream));
-  if (out_prep_msgs && c.jr_len)
-    HIPCHK(e, hipMemcpyAsync(out_prep_msgs, e->d_msgs, n * c.seed, hipMemcpyDeviceToHost, e->stream));
-  if (out_output_shares) {
-    const uint32_t fb = c.fb;
-    rc = ensure_tmp(e, n * c.out_len * fb);
+  HIPCHK(e, hipMemcpyAsync(out_verdicts, B->verdicts, n, hipMemcpyDeviceToHost, e->stream));
+  if (out_msgs && c.jr_len)
+    HIPCHK(e, hipMemcpyAsync(out_msgs, B->msgs, n * c.seed, hipMemcpyDeviceToHost, e->stream));
+  if (out_shares) {
+    rc = copy_out_shares(e, B->outs, n, out_shares);
     if (rc) return rc;
-    const uint4* outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? e->d_meas : e->d_outs;
-    HIPCHK(e, launch_transpose_out(c, outs, n, e->d_tmp, e->stream));
-    HIPCHK(e, hipMemcpyAsync(out_output_shares, e->d_tmp, n * c.out_len * fb, hipMemcpyDeviceToHost, e->stream));
   }
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  e->last_n = n;
-  e->have_batch = true;
-  e->batch_id = ++e->batch_gen;
+  (void)id;
   return drain_timing(e);
+}
+
+int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
+                             const uint8_t* helper_input_shares, const uint8_t* leader_prep_shares,
+                             uint8_t* out_prep_msgs, uint8_t* out_verdicts, uint8_t* out_output_shares,
+                             uint64_t* out_batch_id) {
+  if (out_batch_id) *out_batch_id = 0;
+  if (!e || (n && (!nonces || !helper_input_shares || !leader_prep_shares || !out_verdicts))) return JX_E_INVALID;
+  LOCK(e);
+  const Cfg& c = e->cfg;
+  if (n && c.ps_bytes && !public_shares) return JX_E_INVALID;
+  HIPCHK(e, hipSetDevice(e->device));
+  uint64_t id = 0;
+  Batch* B = nullptr;
+  int32_t rc = batch_new(e, n, false, &id, &B);
+  if (rc) return rc;
+  if (n) {
+    rc = helper_prep_batch_locked(e, n, nonces, public_shares, helper_input_shares, leader_prep_shares, out_prep_msgs,
+                                  out_verdicts, out_output_shares, id, B);
+    if (rc) return drop_on_error(e, id, rc);
+  }
+  if (out_batch_id) *out_batch_id = id;
+  return JX_OK;
 }
 
 int32_t jx_engine_batch_id(const jx_engine* e, uint64_t* batch_id) {
   if (!e || !batch_id) return JX_E_INVALID;
-  *batch_id = e->have_batch ? e->batch_id : 0;
+  LOCK(const_cast<jx_engine*>(e));
+  *batch_id = e->batches.count(e->last_batch) ? e->last_batch : 0;
+  return JX_OK;
+}
+
+int32_t jx_engine_batches(const jx_engine* e, uint64_t* resident, uint64_t* device_bytes) {
+  if (!e) return JX_E_INVALID;
+  LOCK(const_cast<jx_engine*>(e));
+  uint64_t bytes = 0;
+  for (auto& kv : e->batches) bytes += kv.second.bytes;
+  if (resident) *resident = e->batches.size();
+  if (device_bytes) *device_bytes = bytes;
+  return JX_OK;
+}
+
+int32_t jx_batch_release(jx_engine* e, uint64_t batch_id) {
+  if (!e) return JX_E_INVALID;
+  LOCK(e);
+  auto it = e->batches.find(batch_id);
+  if (batch_id == 0 || it == e->batches.end())
+    return fail(e, JX_E_STATE, "release: batch id names no resident prepared batch");
+  HIPCHK(e, hipSetDevice(e->device));
+  batch_free(e, it);
   return JX_OK;
 }
 
@@ -1020,90 +1160,104 @@ int32_t jx_engine_leader_sizes(const jx_engine* e, uint32_t* leader_input_share)
 int32_t jx_leader_prep_init_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
                                   const uint8_t* leader_input_shares, uint8_t* out_prep_shares,
                                   uint8_t* out_verdicts, uint64_t* out_batch_id) {
-  if (!e || !nonces || !leader_input_shares || !out_prep_shares || !out_verdicts) return JX_E_INVALID;
-  const Cfg& c = e->cfg;
-  if (c.ps_bytes && !public_shares) return JX_E_INVALID;
-  e->have_batch = false;
-  e->batch_id = 0;
   if (out_batch_id) *out_batch_id = 0;
-  if (n == 0) {
-    e->have_batch = true;
-    e->leader_batch = true;
-    e->last_n = 0;
-    e->batch_id = ++e->batch_gen;
-    if (out_batch_id) *out_batch_id = e->batch_id;
-    return JX_OK;
-  }
+  if (!e || (n && (!nonces || !leader_input_shares || !out_prep_shares || !out_verdicts))) return JX_E_INVALID;
+  LOCK(e);
+  const Cfg& c = e->cfg;
+  if (n && c.ps_bytes && !public_shares) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
-  int32_t rc = ensure_leader_capacity(e, n);
+  uint64_t id = 0;
+  Batch* B = nullptr;
+  int32_t rc = batch_new(e, n, true, &id, &B);
   if (rc) return rc;
-  HIPCHK(e, hipMemcpyAsync(e->d_nonces, nonces, n * 16, hipMemcpyHostToDevice, e->stream));
-  if (c.ps_bytes) HIPCHK(e, hipMemcpyAsync(e->d_ps, public_shares, n * c.ps_bytes, hipMemcpyHostToDevice, e->stream));
-  HIPCHK(e, hipMemcpyAsync(e->d_lis, leader_input_shares, n * c.lis_bytes, hipMemcpyHostToDevice, e->stream));
-  rc = prep_core(e, n, e->d_nonces, e->d_ps, nullptr, nullptr, e->d_verdicts, e->d_msgs, e->d_lis, e->d_lps_out);
-  if (rc) return rc;
-  HIPCHK(e, hipMemcpyAsync(out_verdicts, e->d_verdicts, n, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(e, hipMemcpyAsync(out_prep_shares, e->d_lps_out, n * c.lps_bytes, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(e, hipStreamSynchronize(e->stream));
-  e->last_n = n;
-  e->have_batch = true;
-  e->batch_id = ++e->batch_gen;
-  if (out_batch_id) *out_batch_id = e->batch_id;
-  return drain_timing(e);
+  if (n) {
+    auto run = [&]() -> int32_t {
+      int32_t r = ensure_leader_capacity(e, n);
+      if (r) return r;
+      HIPCHK(e, hipMemcpyAsync(B->nonces, nonces, n * 16, hipMemcpyHostToDevice, e->stream));
+      if (c.ps_bytes)
+        HIPCHK(e, hipMemcpyAsync(e->d_ps, public_shares, n * c.ps_bytes, hipMemcpyHostToDevice, e->stream));
+      HIPCHK(e, hipMemcpyAsync(e->d_lis, leader_input_shares, n * c.lis_bytes, hipMemcpyHostToDevice, e->stream));
+      r = prep_core(e, n, B->nonces, e->d_ps, nullptr, nullptr, B->verdicts, B->msgs, B->outs, e->d_lis, e->d_lps_out);
+      if (r) return r;
+      HIPCHK(e, hipMemcpyAsync(out_verdicts, B->verdicts, n, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipMemcpyAsync(out_prep_shares, e->d_lps_out, n * c.lps_bytes, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+      return drain_timing(e);
+    };
+    rc = run();
+    if (rc) return drop_on_error(e, id, rc);
+  }
+  if (out_batch_id) *out_batch_id = id;
+  return JX_OK;
 }
 
 int32_t jx_leader_prep_init_device(jx_engine* e, uint64_t n, const void* d_nonces, const void* d_public_shares,
                                    const void* d_leader_input_shares, void* d_out_prep_shares, void* d_out_verdicts,
                                    uint64_t* out_batch_id) {
-  if (!e || !d_nonces || !d_leader_input_shares || !d_out_prep_shares || !out_batch_id) return JX_E_INVALID;
-  const Cfg& c = e->cfg;
-  if (c.ps_bytes && !d_public_shares) return JX_E_INVALID;
-  e->have_batch = false;
-  e->batch_id = 0;
+  if (!out_batch_id) return JX_E_INVALID;
   *out_batch_id = 0;
+  if (!e || (n && (!d_nonces || !d_leader_input_shares || !d_out_prep_shares))) return JX_E_INVALID;
+  LOCK(e);
+  const Cfg& c = e->cfg;
+  if (n && c.ps_bytes && !d_public_shares) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
+  uint64_t id = 0;
+  Batch* B = nullptr;
+  int32_t rc = batch_new(e, n, true, &id, &B);
+  if (rc) return rc;
   if (n) {
-    int32_t rc = ensure_capacity(e, n);
-    if (rc) return rc;
-    rc = prep_core(e, n, (const uint8_t*)d_nonces, (const uint8_t*)d_public_shares, nullptr, nullptr, e->d_verdicts,
-                   e->d_msgs, (const uint8_t*)d_leader_input_shares, (uint8_t*)d_out_prep_shares);
-    if (rc) return rc;
-    if (d_out_verdicts) HIPCHK(e, hipMemcpyAsync(d_out_verdicts, e->d_verdicts, n, hipMemcpyDeviceToDevice, e->stream));
+    auto run = [&]() -> int32_t {
+      int32_t r = ensure_capacity(e, n);
+      if (r) return r;
+      HIPCHK(e, hipMemcpyAsync(B->nonces, d_nonces, n * 16, hipMemcpyDeviceToDevice, e->stream));
+      r = prep_core(e, n, B->nonces, (const uint8_t*)d_public_shares, nullptr, nullptr, B->verdicts, B->msgs, B->outs,
+                    (const uint8_t*)d_leader_input_shares, (uint8_t*)d_out_prep_shares);
+      if (r) return r;
+      if (d_out_verdicts) HIPCHK(e, hipMemcpyAsync(d_out_verdicts, B->verdicts, n, hipMemcpyDeviceToDevice, e->stream));
+      return JX_OK;
+    };
+    rc = run();
+    if (rc) return drop_on_error(e, id, rc);
   }
-  e->leader_batch = true;
-  e->last_n = n;
-  e->have_batch = true;
-  e->batch_id = ++e->batch_gen;
-  *out_batch_id = e->batch_id;
+  *out_batch_id = id;
+  return JX_OK;
+}
+
+static int32_t leader_batch(jx_engine* e, uint64_t batch_id, uint64_t n, Batch** B) {
+  int32_t rc = find_batch(e, batch_id, n, "leader finish", B);
+  if (rc) return rc;
+  if (!(*B)->leader) return fail(e, JX_E_STATE, "leader finish: the batch is a helper batch");
+  if ((*B)->finished) return fail(e, JX_E_STATE, "leader finish: the batch was already finished");
   return JX_OK;
 }
 
 int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t* prep_msgs,
                                     uint8_t* out_verdicts, uint8_t* out_output_shares) {
-  if (!e || !out_verdicts) return JX_E_INVALID;
+  if (!e || (n && !out_verdicts)) return JX_E_INVALID;
+  LOCK(e);
   const Cfg& c = e->cfg;
-  int32_t rc0 = check_batch(e, batch_id, n, "leader finish");
-  if (rc0) return rc0;
-  if (!e->leader_batch) return fail(e, JX_E_STATE, "leader finish: the resident batch is a helper batch");
-  if (c.jr_len && !prep_msgs) return JX_E_INVALID;
+  Batch* B = nullptr;
+  int32_t rc = leader_batch(e, batch_id, n, &B);
+  if (rc) return rc;
+  if (n && c.jr_len && !prep_msgs) return JX_E_INVALID;
+  B->finished = true;
   if (n == 0) return JX_OK;
   HIPCHK(e, hipSetDevice(e->device));
+  rc = ensure_leader_capacity(e, n);
+  if (rc) return rc;
   if (c.jr_len) {
     HIPCHK(e, hipMemcpyAsync(e->d_in_msgs, prep_msgs, n * c.seed, hipMemcpyHostToDevice, e->stream));
     Bufs b{};
     b.n = n;
-    b.verdicts = e->d_verdicts;
-    b.msgs = e->d_msgs;
+    b.verdicts = B->verdicts;
+    b.msgs = B->msgs;
     HIPCHK(e, launch_leader_finish(c, b, e->d_in_msgs, nullptr, e->stream));
   }
-  HIPCHK(e, hipMemcpyAsync(out_verdicts, e->d_verdicts, n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(out_verdicts, B->verdicts, n, hipMemcpyDeviceToHost, e->stream));
   if (out_output_shares) {
-    const uint32_t fb = c.fb;
-    int32_t rc = ensure_tmp(e, n * c.out_len * fb);
+    rc = copy_out_shares(e, B->outs, n, out_output_shares);
     if (rc) return rc;
-    const uint4* outs = (c.out_is_meas && c.algo != ALGO_COUNT) ? e->d_meas : e->d_outs;
-    HIPCHK(e, launch_transpose_out(c, outs, n, e->d_tmp, e->stream));
-    HIPCHK(e, hipMemcpyAsync(out_output_shares, e->d_tmp, n * c.out_len * fb, hipMemcpyDeviceToHost, e->stream));
   }
   HIPCHK(e, hipStreamSynchronize(e->stream));
   return JX_OK;
@@ -1112,74 +1266,170 @@ int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t batch_id, uint64_t n,
 int32_t jx_leader_prep_finish_device(jx_engine* e, uint64_t batch_id, uint64_t n, const void* d_prep_msgs,
                                      const void* d_peer_verdicts, void* d_out_verdicts) {
   if (!e) return JX_E_INVALID;
+  LOCK(e);
   const Cfg& c = e->cfg;
-  int32_t rc = check_batch(e, batch_id, n, "leader finish");
+  Batch* B = nullptr;
+  int32_t rc = leader_batch(e, batch_id, n, &B);
   if (rc) return rc;
-  if (!e->leader_batch) return fail(e, JX_E_STATE, "leader finish: the resident batch is a helper batch");
-  if (c.jr_len && !d_prep_msgs) return JX_E_INVALID;
+  if (n && c.jr_len && !d_prep_msgs) return JX_E_INVALID;
+  B->finished = true;
   if (n == 0) return JX_OK;
   HIPCHK(e, hipSetDevice(e->device));
   Bufs b{};
   b.n = n;
-  b.verdicts = e->d_verdicts;
-  b.msgs = e->d_msgs;
+  b.verdicts = B->verdicts;
+  b.msgs = B->msgs;
   HIPCHK(e, launch_leader_finish(c, b, (const uint8_t*)d_prep_msgs, (const uint8_t*)d_peer_verdicts, e->stream));
-  if (d_out_verdicts) HIPCHK(e, hipMemcpyAsync(d_out_verdicts, e->d_verdicts, n, hipMemcpyDeviceToDevice, e->stream));
+  if (d_out_verdicts) HIPCHK(e, hipMemcpyAsync(d_out_verdicts, B->verdicts, n, hipMemcpyDeviceToDevice, e->stream));
+  return JX_OK;
+}
+
+// A batch ready to accumulate: helper batches at once, leader batches after prepare_next.
+static int32_t ready_batch(jx_engine* e, uint64_t batch_id, uint64_t n, const char* what, Batch** B) {
+  int32_t rc = find_batch(e, batch_id, n, what, B);
+  if (rc) return rc;
+  if ((*B)->leader && !(*B)->finished)
+    return fail(e, JX_E_STATE, std::string(what) + ": leader batch not finished (jx_leader_prep_finish_*)");
   return JX_OK;
 }
 
 int32_t jx_accumulate(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t* accept_mask,
                       const uint32_t* segment) {
   if (!e) return JX_E_INVALID;
-  int32_t rc = check_batch(e, batch_id, n, "accumulate");
+  LOCK(e);
+  Batch* B = nullptr;
+  int32_t rc = ready_batch(e, batch_id, n, "accumulate", &B);
   if (rc) return rc;
-  e->have_batch = false;  // a batch is accumulated at most once
-  e->batch_id = 0;
-  if (n == 0) return JX_OK;
   HIPCHK(e, hipSetDevice(e->device));
-  const uint8_t* dm = nullptr;
-  if (accept_mask) {
-    HIPCHK(e, hipMemcpyAsync(e->d_mask, accept_mask, n, hipMemcpyHostToDevice, e->stream));
-    dm = e->d_mask;
-  }
-  std::vector<uint32_t> ids{0};
-  const uint32_t* ds = nullptr;
-  if (segment) {
-    densify(segment, n, e->h_dense, ids);
-    if (ids.size() > 1) {
-      HIPCHK(e, hipMemcpyAsync(e->d_seg, e->h_dense.data(), n * 4, hipMemcpyHostToDevice, e->stream));
-      ds = e->d_seg;
+  auto run = [&]() -> int32_t {
+    if (n == 0) return JX_OK;
+    int32_t r = ensure_capacity(e, n);  // mask / index scratch and the accumulate partials
+    if (r) return r;
+    const uint8_t* dm = nullptr;
+    if (accept_mask) {
+      HIPCHK(e, hipMemcpyAsync(e->d_mask, accept_mask, n, hipMemcpyHostToDevice, e->stream));
+      dm = e->d_mask;
     }
-  }
-  rc = accumulate_any(e, n, e->d_verdicts, dm, ds, ids);
+    std::vector<uint32_t> ids{0};
+    const uint32_t* ds = nullptr;
+    if (segment) {
+      densify(segment, n, e->h_dense, ids);
+      if (ids.size() > 1) {
+        HIPCHK(e, hipMemcpyAsync(e->d_seg, e->h_dense.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+        ds = e->d_seg;
+      }
+    }
+    std::vector<Segment> targets;
+    r = segment_targets(e, ids.data(), ids.size(), targets);
+    if (r) return r;
+    r = accumulate_into(e, batch_src(*B), dm, ds, targets);
+    if (r) return r;
+    HIPCHK(e, hipStreamSynchronize(e->stream));  // the host mask / index copies are pageable
+    return drain_timing(e);
+  };
+  rc = run();
   if (rc) return rc;
-  HIPCHK(e, hipStreamSynchronize(e->stream));
-  return drain_timing(e);
+  batch_free(e, e->batches.find(batch_id));  // a batch is accumulated at most once
+  return JX_OK;
 }
 
 int32_t jx_accumulate_device(jx_engine* e, uint64_t batch_id, uint64_t n, const void* d_accept_mask,
                              const void* d_segment, const uint32_t* segment_ids, uint32_t nsegments) {
   if (!e || !segment_ids || nsegments == 0) return JX_E_INVALID;
-  int32_t rc = check_batch(e, batch_id, n, "accumulate");
+  LOCK(e);
+  Batch* B = nullptr;
+  int32_t rc = ready_batch(e, batch_id, n, "accumulate", &B);
   if (rc) return rc;
-  e->have_batch = false;
-  e->batch_id = 0;
-  if (n == 0) return JX_OK;
   HIPCHK(e, hipSetDevice(e->device));
-  std::vector<uint32_t> ids(segment_ids, segment_ids + nsegments);
-  return accumulate_any(e, n, e->d_verdicts, (const uint8_t*)d_accept_mask, (const uint32_t*)d_segment, ids);
+  if (n) {
+    rc = ensure_capacity(e, n);
+    if (rc) return rc;
+    std::vector<Segment> targets;
+    rc = segment_targets(e, segment_ids, nsegments, targets);
+    if (rc) return rc;
+    rc = accumulate_into(e, batch_src(*B), (const uint8_t*)d_accept_mask, (const uint32_t*)d_segment, targets);
+    if (rc) return rc;
+  }
+  batch_free(e, e->batches.find(batch_id));
+  return JX_OK;
+}
+
+// Deltas: accumulate a batch into zeroed per-call aggregations and export them as records. Pure with
+// respect to engine state (the batch stays resident; the running aggregations are not touched).
+static int32_t batch_records(jx_engine* e, Batch* B, const uint8_t* d_mask, const uint32_t* d_index, uint32_t ns,
+                             uint8_t* d_out) {
+  std::vector<Segment> targets;
+  int32_t rc = delta_targets(e, ns, targets);
+  if (rc) return rc;
+  rc = accumulate_into(e, batch_src(*B), d_mask, d_index, targets);
+  if (rc) return rc;
+  HIPCHK(e, launch_record_export(e->cfg, targets[0].agg, targets[0].count, targets[0].checksum, d_out, e->stream, ns));
+  return JX_OK;
+}
+
+int32_t jx_batch_aggregate_records(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t* accept_mask,
+                                   const uint32_t* segment_index, uint32_t nsegments, uint8_t* out_records) {
+  if (!e || !out_records || nsegments == 0) return JX_E_INVALID;
+  LOCK(e);
+  Batch* B = nullptr;
+  int32_t rc = ready_batch(e, batch_id, n, "aggregate records", &B);
+  if (rc) return rc;
+  HIPCHK(e, hipSetDevice(e->device));
+  const uint64_t rb = record_bytes(e->cfg);
+  if (n) {
+    rc = ensure_capacity(e, n);
+    if (rc) return rc;
+  }
+  const uint8_t* dm = nullptr;
+  const uint32_t* di = nullptr;
+  if (n && accept_mask) {
+    HIPCHK(e, hipMemcpyAsync(e->d_mask, accept_mask, n, hipMemcpyHostToDevice, e->stream));
+    dm = e->d_mask;
+  }
+  if (n && segment_index) {
+    HIPCHK(e, hipMemcpyAsync(e->d_seg, segment_index, n * 4, hipMemcpyHostToDevice, e->stream));
+    di = e->d_seg;
+  }
+  rc = ensure_tmp(e, rb * nsegments);
+  if (rc) return rc;
+  rc = batch_records(e, B, dm, di, nsegments, e->d_tmp);
+  if (rc) return rc;
+  HIPCHK(e, hipMemcpyAsync(out_records, e->d_tmp, rb * nsegments, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return drain_timing(e);
+}
+
+int32_t jx_batch_aggregate_records_device(jx_engine* e, uint64_t batch_id, uint64_t n, const void* d_accept_mask,
+                                          const void* d_segment_index, uint32_t nsegments, void* d_out_records) {
+  if (!e || !d_out_records || nsegments == 0) return JX_E_INVALID;
+  LOCK(e);
+  Batch* B = nullptr;
+  int32_t rc = ready_batch(e, batch_id, n, "aggregate records", &B);
+  if (rc) return rc;
+  HIPCHK(e, hipSetDevice(e->device));
+  if (n) {
+    rc = ensure_capacity(e, n);
+    if (rc) return rc;
+  }
+  return batch_records(e, B, (const uint8_t*)d_accept_mask, (const uint32_t*)d_segment_index, nsegments,
+                       (uint8_t*)d_out_records);
 }
 
 int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
                                  const uint8_t* helper_input_shares, const uint8_t* leader_prep_shares,
                                  uint32_t segment, uint8_t* out_prep_msgs, uint8_t* out_verdicts) {
   if (!e || !nonces || !helper_input_shares || !leader_prep_shares) return JX_E_INVALID;
+  LOCK(e);
   const Cfg& c = e->cfg;
   if (c.ps_bytes && !public_shares) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
   const uint64_t chunk = launch_chunk(e, n);
   int32_t rc = ensure_capacity(e, chunk);
   if (rc) return rc;
+  Segment* seg = nullptr;
+  rc = get_segment(e, segment, &seg);
+  if (rc) return rc;
+  const std::vector<Segment> targets{*seg};
   for (uint64_t off = 0; off < n; off += chunk) {
     const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
     HIPCHK(e, hipMemcpyAsync(e->d_nonces, nonces + off * 16, m * 16, hipMemcpyHostToDevice, e->stream));
@@ -1190,9 +1440,9 @@ int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces
                              hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemcpyAsync(e->d_lps, leader_prep_shares + off * c.lps_bytes, m * c.lps_bytes,
                              hipMemcpyHostToDevice, e->stream));
-    rc = prep_core(e, m, e->d_nonces, e->d_ps, e->d_his, e->d_lps, e->d_verdicts, e->d_msgs);
+    rc = prep_core(e, m, e->d_nonces, e->d_ps, e->d_his, e->d_lps, e->d_verdicts, e->d_msgs, staging_outs(e));
     if (rc) return rc;
-    rc = accumulate_core(e, m, e->d_verdicts, nullptr, nullptr, segment);
+    rc = accumulate_into(e, AccSrc{m, staging_outs(e), e->d_verdicts, e->d_nonces}, nullptr, nullptr, targets);
     if (rc) return rc;
     if (out_verdicts)
       HIPCHK(e, hipMemcpyAsync(out_verdicts + off, e->d_verdicts, m, hipMemcpyDeviceToHost, e->stream));
@@ -1200,8 +1450,6 @@ int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces
       HIPCHK(e, hipMemcpyAsync(out_prep_msgs + off * c.seed, e->d_msgs, m * c.seed, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
   }
-  e->have_batch = false;  // staging no longer holds one whole batch
-  e->batch_id = 0;
   return drain_timing(e);
 }
 
@@ -1210,60 +1458,34 @@ int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_
                                         const uint32_t* segment_ids, uint32_t nsegments, void* d_out_prep_msgs,
                                         void* d_out_verdicts) {
   if (!e || !d_nonces || !d_his || !d_lps || !segment_ids || nsegments == 0) return JX_E_INVALID;
+  LOCK(e);
   const Cfg& c = e->cfg;
   if (c.ps_bytes && !d_ps) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
   const uint64_t chunk = launch_chunk(e, n);
   int32_t rc = ensure_capacity(e, chunk);
   if (rc) return rc;
-  e->have_batch = false;
-  e->batch_id = 0;
-  const std::vector<uint32_t> ids(segment_ids, segment_ids + nsegments);
+  std::vector<Segment> targets;
+  rc = segment_targets(e, segment_ids, nsegments, targets);
+  if (rc) return rc;
   const uint8_t *N = (const uint8_t*)d_nonces, *PS = (const uint8_t*)d_ps, *H = (const uint8_t*)d_his,
                 *L = (const uint8_t*)d_lps;
   const uint32_t* SG = (const uint32_t*)d_segment;
-  // Several launches into one aggregation, when enabled: pipeline them over two streams and two
-  // staging sets. K1 (VALU-bound, every VGPR of its SIMDs) of launch i+1 runs while K3 (bound by the
-  // staging read stream) and K4 of launch i drain on stream2; K3/K4 stay ordered among themselves on
-  // stream2 (one aggregation). Measured slower than the serial path (see `overlap`).
-  const bool generic = c.algo != ALGO_COUNT && c.algo != ALGO_SUMVEC_F64_MULTIPROOF;
-  if (e->overlap && generic && n > chunk && !SG && nsegments == 1 && ensure_second_set(e)) {
-    Segment* seg = nullptr;
-    rc = get_segment(e, ids[0], &seg);  // its zero-fill is queued on stream, before the first K1
+  // the pointer table is uploaded once for every launch of the call (no per-launch host sync)
+  const bool many = SG && targets.size() > 1;
+  if (many) {
+    rc = upload_targets(e, targets);
     if (rc) return rc;
-    HIPCHK(e, hipEventRecord(e->ev_join, e->stream));
-    HIPCHK(e, hipStreamWaitEvent(e->stream2, e->ev_join, 0));
-    uint64_t i = 0;
-    for (uint64_t off = 0; off < n; off += chunk, i++) {
-      const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
-      const int set = (int)(i & 1);
-      uint8_t* vout = d_out_verdicts ? (uint8_t*)d_out_verdicts + off : e->d_verdicts;
-      uint8_t* mout = (d_out_prep_msgs && c.jr_len) ? (uint8_t*)d_out_prep_msgs + off * c.seed : e->d_msgs;
-      if (i >= 2) HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_free[set], 0));  // set reused: K3/K4 of i-2 done
-      rc = prep_core(e, m, N + off * 16, PS ? PS + off * c.ps_bytes : nullptr, H + off * c.his_bytes,
-                     L + off * c.lps_bytes, vout, mout, nullptr, nullptr, set, 1, e->stream, e->stream2);
-      if (rc) return rc;
-      HIPCHK(e, hipEventRecord(e->ev_k1[set], e->stream));
-      HIPCHK(e, hipStreamWaitEvent(e->stream2, e->ev_k1[set], 0));
-      rc = prep_core(e, m, N + off * 16, PS ? PS + off * c.ps_bytes : nullptr, H + off * c.his_bytes,
-                     L + off * c.lps_bytes, vout, mout, nullptr, nullptr, set, 2, e->stream, e->stream2);
-      if (rc) return rc;
-      rc = accumulate_core(e, m, vout, nullptr, nullptr, ids[0], false, e->stream2, set, N + off * 16);
-      if (rc) return rc;
-      HIPCHK(e, hipEventRecord(e->ev_free[set], e->stream2));
-    }
-    HIPCHK(e, hipEventRecord(e->ev_join, e->stream2));
-    HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_join, 0));  // callers sync the engine stream
-    return JX_OK;
   }
   for (uint64_t off = 0; off < n; off += chunk) {
     const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
     uint8_t* vout = d_out_verdicts ? (uint8_t*)d_out_verdicts + off : e->d_verdicts;
     uint8_t* mout = (d_out_prep_msgs && c.jr_len) ? (uint8_t*)d_out_prep_msgs + off * c.seed : e->d_msgs;
     rc = prep_core(e, m, N + off * 16, PS ? PS + off * c.ps_bytes : nullptr, H + off * c.his_bytes,
-                   L + off * c.lps_bytes, vout, mout);
+                   L + off * c.lps_bytes, vout, mout, staging_outs(e));
     if (rc) return rc;
-    rc = accumulate_any(e, m, vout, nullptr, SG ? SG + off : nullptr, ids);
+    rc = accumulate_into(e, AccSrc{m, staging_outs(e), vout, N + off * 16}, nullptr, SG ? SG + off : nullptr, targets,
+                         many);
     if (rc) return rc;
   }
   return JX_OK;
@@ -1271,6 +1493,7 @@ int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_
 
 int32_t jx_aggregate_read(jx_engine* e, uint32_t segment, uint8_t* out_agg, uint64_t* count) {
   if (!e) return JX_E_INVALID;
+  LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
   const Cfg& c = e->cfg;
   const uint32_t fb = c.fb;
@@ -1290,6 +1513,7 @@ int32_t jx_aggregate_read(jx_engine* e, uint32_t segment, uint8_t* out_agg, uint
 
 int32_t jx_aggregate_checksum(jx_engine* e, uint32_t segment, uint8_t out_checksum[32]) {
   if (!e || !out_checksum) return JX_E_INVALID;
+  LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
   Segment* s = nullptr;
   int32_t rc = get_segment(e, segment, &s);
@@ -1301,6 +1525,7 @@ int32_t jx_aggregate_checksum(jx_engine* e, uint32_t segment, uint8_t out_checks
 
 int32_t jx_aggregate_reset(jx_engine* e) {
   if (!e) return JX_E_INVALID;
+  LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
   for (auto& kv : e->segs) {
     HIPCHK(e, hipMemsetAsync(kv.second.agg, 0, (size_t)e->cfg.out_len * 16, e->stream));
@@ -1313,6 +1538,7 @@ int32_t jx_aggregate_reset(jx_engine* e) {
 
 int32_t jx_aggregate_export_device(jx_engine* e, uint32_t segment, void* d_dst) {
   if (!e || !d_dst) return JX_E_INVALID;
+  LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
   Segment* s = nullptr;
   int32_t rc = get_segment(e, segment, &s);
@@ -1331,6 +1557,7 @@ static int32_t ensure_err(jx_engine* e) {
 
 int32_t jx_aggregate_combine_device(jx_engine* e, const void* d_parts, uint32_t nparts, void* d_out) {
   if (!e || !d_parts || !d_out || nparts == 0) return JX_E_INVALID;
+  LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
   int32_t rc = ensure_err(e);
   if (rc) return rc;
@@ -1340,6 +1567,7 @@ int32_t jx_aggregate_combine_device(jx_engine* e, const void* d_parts, uint32_t 
 
 int32_t jx_shard_record_export_device(jx_engine* e, uint32_t segment, void* d_dst) {
   if (!e || !d_dst) return JX_E_INVALID;
+  LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
   Segment* s = nullptr;
   int32_t rc = get_segment(e, segment, &s);
@@ -1350,6 +1578,7 @@ int32_t jx_shard_record_export_device(jx_engine* e, uint32_t segment, void* d_ds
 
 int32_t jx_shard_record_combine_device(jx_engine* e, const void* d_records, uint32_t nrecords, void* d_out) {
   if (!e || !d_records || !d_out || nrecords == 0) return JX_E_INVALID;
+  LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
   int32_t rc = ensure_err(e);
   if (rc) return rc;
@@ -1359,12 +1588,13 @@ int32_t jx_shard_record_combine_device(jx_engine* e, const void* d_records, uint
 
 int32_t jx_shard_record_bytes(const jx_engine* e, uint32_t* bytes) {
   if (!e || !bytes) return JX_E_INVALID;
-  *bytes = e->cfg.out_len * e->cfg.fb + 40u;
+  *bytes = record_bytes(e->cfg);
   return JX_OK;
 }
 
 int32_t jx_engine_sync(jx_engine* e) {
   if (!e) return JX_E_INVALID;
+  LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   if (e->d_err) {
@@ -1386,6 +1616,7 @@ int32_t jx_engine_stream(jx_engine* e, void** stream) {
 
 int32_t jx_engine_timing(jx_engine* e, int32_t enable) {
   if (!e) return JX_E_INVALID;
+  LOCK(e);
   int32_t rc = drain_timing(e);
   if (rc) return rc;
   e->timing = enable != 0;
@@ -1398,6 +1629,7 @@ int32_t jx_engine_timing(jx_engine* e, int32_t enable) {
 
 int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]) {
   if (!e) return JX_E_INVALID;
+  LOCK(e);
   int32_t rc = drain_timing(e);
   if (rc) return rc;
   for (int i = 0; i < NST; i++) {
@@ -1409,29 +1641,20 @@ int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]) {
 
 int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
   if (!e) return JX_E_INVALID;
+  LOCK(e);
   if (option == 1) {
     e->force_slow = value != 0;
     return JX_OK;
   }
-  if (option == 3) {  // helper K1 variant
-    if (value < 0 || value > 5) return JX_E_INVALID;
-    // 0: automatic (fused; lane-split below one fused wave per SIMD), 1 / 2: squeeze-only + absorb-only
-    // launches (absorb at 3 / 2 waves/SIMD), 3: lane-split, 4: sequential S, J permutations, 5: fused
+  if (option == 3) {  // helper K1 kernel
+    if (value != 0 && value != 3 && value != 5) return JX_E_INVALID;
+    // 0: automatic (fused; lane-split below one fused wave per SIMD), 3: lane-split, 5: fused
     e->k1_split = (uint32_t)value;
-    return JX_OK;
-  }
-  if (option == 5) {  // overlapped two-stream fused path for multi-launch device calls (1) or not (0, default)
-    e->overlap = value != 0;
-    return JX_OK;
-  }
-  if (option == 4) {  // K3 load pipeline: 1 or 2 calls ahead; 12 / 13 = 2 / 3 ahead at 3 waves/SIMD; 20 / 21 LDS-DMA ring
-    if (value != 1 && value != 2 && value != 12 && value != 13 && value != 20 && value != 21 && value != 26)
-      return JX_E_INVALID;
-    e->k3_pf = (uint32_t)value;
     return JX_OK;
   }
   if (option == 2) {  // accumulate chunking (tests)
     if (value < 1 || value > 4096) return JX_E_INVALID;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
     free_staging(e);
     e->acc_chunks = (uint32_t)value;
     return JX_OK;

@@ -104,8 +104,7 @@ struct Bufs {
   uint8_t* msgs;
   const uint4* consts;
   uint32_t force_slow;  // debug: route every report through the slow XOF kernel
-  uint32_t k1_split;    // helper K1 as two launches (squeeze-only, absorb-only) instead of one
-  uint32_t k3_pf;       // ParallelSum FLP part kernel: calls of loads in flight (1..3)
+  uint32_t k1_split;    // helper K1 kernel: 3 = lane-split (xof_lanes_kernel), otherwise the fused kernel
 };
 
 struct AccArgs {
@@ -168,8 +167,9 @@ hipError_t launch_flp(const Cfg& c, const Bufs& b, hipStream_t s);
 hipError_t launch_accumulate(const Cfg& c, const AccArgs& a, uint4* agg, hipStream_t s);
 hipError_t launch_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, uint32_t* err,
                           hipStream_t s);
+// ns records of contiguous segment state (agg [ns][out_len], count [ns], checksum [ns][8])
 hipError_t launch_record_export(const Cfg& c, const uint4* agg, const unsigned long long* count,
-                                const uint32_t* checksum, uint8_t* dst, hipStream_t s);
+                                const uint32_t* checksum, uint8_t* dst, hipStream_t s, uint32_t ns = 1);
 hipError_t launch_record_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, uint32_t* err,
                                  hipStream_t s);
 hipError_t launch_transpose_out(const Cfg& c, const uint4* outs, uint64_t n, uint8_t* dst, hipStream_t s);

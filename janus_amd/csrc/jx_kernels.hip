@@ -496,32 +496,15 @@ __device__ __forceinline__ bool ge_exact(uint4 v) {
   return v.w == 0xFFFFFFFFu && (v.z > 0xFFFFFFE4u || (v.z == 0xFFFFFFE4u && (v.x | v.y) != 0u));
 }
 
-// K1 for one role. HELPER (agg_id 1, aggregator.rs:1947): the measurement and proof shares are
-// expanded from seeds by TurboSHAKE128 and the squeeze runs alongside the joint_rand_part absorb.
-// LEADER (agg_id 0, leader_initialized, aggregation_job_driver.rs:345): the shares are explicit in
-// the leader input share (meas || proofs || k_blind, decoded here: elements >= p fail) and only the
-// joint_rand_part absorb runs through Keccak.
-//
-// Split helper variant (K1_SQUEEZE then K1_ABSORB, Cfg-independent engine switch): the squeeze of
-// the measurement + proof shares (one sponge per lane, <= 128 VGPRs: 4 waves/SIMD) and the
-// joint_rand_part absorb of the staged measurement share + the XOF tail (3 waves/SIMD) run as two
-// launches instead of one 2-sponge kernel at 2 waves/SIMD; +128 KB/report of staging reads.
+// K1, helper (agg_id 1, aggregator.rs:1947), large launches: the measurement and proof shares are
+// expanded from seeds by TurboSHAKE128 and the squeeze runs alongside the joint_rand_part absorb, one
+// report per lane with both sponges in VGPRs (2 waves/SIMD). The leader (agg_id 0) has its own
+// one-sponge kernel (xof_leader_kernel); launches under one fused wave per SIMD take the lane-split
+// kernel (xof_lanes_kernel). Variants measured slower and removed: squeeze-only +
+// absorb-only launches, sequential S/J permutations at 3 waves/SIMD.
 constexpr uint32_t K1_WAVES = 4;  // waves (64-report blocks) per K1 workgroup
-// K1_ABSORB2: the absorb-only launch built for 2 waves/SIMD (no spills) instead of 3
-// K1_SEQ: the fused kernel with the S and J permutations one after the other (not interleaved), built
-// for 3 waves/SIMD
-enum : int { K1_FUSED = 0, K1_LEADER = 1, K1_SQUEEZE = 2, K1_ABSORB = 3, K1_ABSORB2 = 4, K1_SEQ = 5 };
-template <int MODE>
-struct K1Occ {  // min waves per SIMD the register budget is built for
-  static constexpr int value =
-      MODE == K1_SQUEEZE ? 4 : (MODE == K1_ABSORB || MODE == K1_SEQ ? 3 : (MODE == K1_ABSORB2 ? 2 : 1));
-};
-template <int MODE, bool WIDE = false>
-__global__ __launch_bounds__(64 * K1_WAVES, K1Occ<MODE>::value) void xof_kernel(Cfg c, Bufs b) {
-  constexpr bool LEADER = MODE == K1_LEADER;
-  constexpr bool SQUEEZE_ONLY = MODE == K1_SQUEEZE;
-  constexpr bool ABSORB_ONLY = MODE == K1_ABSORB || MODE == K1_ABSORB2;
-  constexpr bool LOADS = LEADER || ABSORB_ONLY;  // measurement words are loaded, not squeezed
+template <bool WIDE = false>
+__global__ __launch_bounds__(64 * K1_WAVES, 1) void xof_kernel(Cfg c, Bufs b) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t blk = (uint64_t)blockIdx.x * K1_WAVES + (threadIdx.x >> 6);
   const uint64_t nblk = (b.n + 63) / 64;
@@ -529,9 +512,7 @@ __global__ __launch_bounds__(64 * K1_WAVES, K1Occ<MODE>::value) void xof_kernel(
   const uint64_t r0 = blk * 64 + lane;
   const uint64_t r = r0 < b.n ? r0 : b.n - 1;
 
-  const uint8_t* hs = LEADER ? nullptr : b.his + (uint64_t)c.his_bytes * r;
-  const uint4* const mstage = b.meas + il_idx(blk, c.meas_len, 0, lane);
-  const uint8_t* ls = LEADER ? b.lis + (uint64_t)c.lis_bytes * r : nullptr;
+  const uint8_t* hs = b.his + (uint64_t)c.his_bytes * r;
   uint32_t flags = 0;
   const uint32_t MB = c.meas_len * 16;
   const uint32_t ML = 42 + MB;
@@ -539,58 +520,14 @@ __global__ __launch_bounds__(64 * K1_WAVES, K1Occ<MODE>::value) void xof_kernel(
   const uint32_t b_last = ML / 168;      // last absorbed block (b_last <= NM)
 
   // ---- measurement share fused with the joint_rand_part absorb --------------------
-  // S: block m of the measurement share. Helper: XOF(k_meas, DST(1), [1]) squeezed 168 bytes
-  //    per block; leader: bytes [168m, 168m + 168) of its explicit share.
+  // S: XOF(k_meas, DST(1), [1]) squeezed 168 bytes (block m of the measurement share) per block.
   // J: XOF(k_blind, DST(7), [agg_id] || nonce || enc(meas_share))   (absorbing those bytes)
   // J's message block m is meas bytes [168m - 42, 168m + 126): the 42-byte header makes it a
-  // 16-bit funnel shift (v_alignbit_b32) of the words of blocks m-1 and m. On the helper, after
-  // block m is consumed S (-> block m+1) and J (absorb block m) permute together: two
-  // independent streams (keccak_p12_x2).
+  // 16-bit funnel shift (v_alignbit_b32) of the words of blocks m-1 and m. After block m is
+  // consumed S (-> block m+1) and J (absorb block m) permute together: two independent streams
+  // (keccak_p12_x2).
   uint32_t S[50], J[50];
-  // leader: load block m of the explicit share; absorb-only: of the staged share (words past the
-  // share's end read as 0). Block m = bytes [168m, 168m + 168): elements 21(m/2) + 0..10 (even m,
-  // the last one's low half) or + 10..20 (odd m, the first one's high half).
-  auto load_block = [&](uint32_t m) {
-    if (ABSORB_ONLY) {
-      const uint32_t e0 = 21 * (m >> 1) + ((m & 1) ? 10 : 0);
-      uint4 v[11];
-#pragma unroll
-      for (int q = 0; q < 11; q++) v[q] = e0 + q < c.meas_len ? mstage[(uint64_t)(e0 + q) * IL] : make_uint4(0, 0, 0, 0);
-      if ((m & 1) == 0) {
-#pragma unroll
-        for (int q = 0; q < 10; q++) {
-          S[4 * q] = v[q].x;
-          S[4 * q + 1] = v[q].y;
-          S[4 * q + 2] = v[q].z;
-          S[4 * q + 3] = v[q].w;
-        }
-        S[40] = v[10].x;
-        S[41] = v[10].y;
-      } else {
-        S[0] = v[0].z;
-        S[1] = v[0].w;
-#pragma unroll
-        for (int q = 0; q < 10; q++) {
-          S[2 + 4 * q] = v[q + 1].x;
-          S[3 + 4 * q] = v[q + 1].y;
-          S[4 + 4 * q] = v[q + 1].z;
-          S[5 + 4 * q] = v[q + 1].w;
-        }
-      }
-      return;
-    }
-#pragma unroll
-    for (int q = 0; q < 21; q++) {
-      const uint32_t off = 168 * m + 8 * q;
-      uint2 v = make_uint2(0, 0);
-      if (off < MB) v = *reinterpret_cast<const uint2*>(ls + off);
-      S[2 * q] = v.x;
-      S[2 * q + 1] = v.y;
-    }
-  };
-  if (LOADS) {
-    load_block(0);
-  } else {
+  {
     uint32_t kmeas[4];
     load16(hs, kmeas);
     Block m;
@@ -604,11 +541,11 @@ __global__ __launch_bounds__(64 * K1_WAVES, K1Occ<MODE>::value) void xof_kernel(
   {
     uint32_t nonce[4], kblind[4];
     load16(b.nonces + 16 * r, nonce);
-    load16(LEADER ? ls + MB + 16 * c.proof_len : hs + 32, kblind);
+    load16(hs + 32, kblind);
     Block h;
     blk_zero(h);
     int pos = blk_xof_prefix(h, c.dst_id, 7, kblind);
-    blk_put_byte(h, pos, LEADER ? 0 : 1);  // agg_id
+    blk_put_byte(h, pos, 1);  // agg_id
 #pragma unroll
     for (int i = 0; i < 4; i++) blk_put_word(h, pos + 1 + 4 * i, nonce[i]);
 #pragma unroll
@@ -616,8 +553,7 @@ __global__ __launch_bounds__(64 * K1_WAVES, K1Occ<MODE>::value) void xof_kernel(
   }
   uint32_t prev[11];
   uint32_t carry0 = 0, carry1 = 0;
-  uint32_t gmax = 0;  // helper: running ge_screen over every sampled element
-  bool bad = false;   // leader: an explicit element is >= p
+  uint32_t gmax = 0;  // running ge_screen over every sampled element
   TruncW tr;
   truncw_zero(tr);
   tr.j = 0;
@@ -625,18 +561,9 @@ __global__ __launch_bounds__(64 * K1_WAVES, K1Occ<MODE>::value) void xof_kernel(
   f128 trunc_lo = make128(0, 0);
   uint4* const mp = b.meas + il_idx(blk, c.meas_len, 0, lane);
   uint4* const op = b.outs + il_idx(blk, c.out_len, 0, lane);
-  uint32_t unused_screen = 0;
-  auto emit = [&](uint32_t e, uint4 v) {
-    if (LEADER) {
-      if (e < c.meas_len) bad |= ge_exact(v);
-      emit_meas<WIDE>(c, mp, op, e, v, unused_screen, tr, trunc_lo);
-    } else {
-      emit_meas<WIDE>(c, mp, op, e, v, gmax, tr, trunc_lo);
-    }
-  };
+  auto emit = [&](uint32_t e, uint4 v) { emit_meas<WIDE>(c, mp, op, e, v, gmax, tr, trunc_lo); };
   // emit the measurement elements of block m (10 or 11, by parity)
   auto emit_block = [&](uint32_t m) {
-    if (ABSORB_ONLY) return;  // staged by the squeeze-only launch
     const uint32_t e0 = 21 * (m >> 1);
     if ((m & 1) == 0) {
 #pragma unroll
@@ -705,31 +632,15 @@ __global__ __launch_bounds__(64 * K1_WAVES, K1Occ<MODE>::value) void xof_kernel(
     for (int w = 0; w < 42; w++) J[w] ^= jw[w];
     keccak_p12(J);
   };
-  // advance to block m+1: helper squeezes (together with J's permutation), leader loads
+  // advance to block m+1: S squeezes together with J's permutation
   auto advance = [&](uint32_t m) {
-    if (LOADS) {
-      if (m + 1 < NM) load_block(m + 1);
-      keccak_p12(J);
-    } else if (m + 1 < NM && MODE == K1_SEQ) {
-      keccak_p12(S);
-      keccak_p12(J);
-    } else if (m + 1 < NM) {
+    if (m + 1 < NM)
       keccak_p12_x2(S, J);
-    } else {
+    else
       keccak_p12(J);
-    }
   };
-  if (SQUEEZE_ONLY) {  // K1a: the measurement-share squeeze alone (one sponge per lane)
-    emit_block(0);
-#pragma unroll 1
-    for (uint32_t m = 1; m < NM; m++) {
-      keccak_p12(S);
-      emit_block(m);
-    }
-  }
   // blocks m = 0 .. b_last (b_last <= NM); blocks m < NM hold measurement bytes. Block 0 is
   // peeled so that the 42-byte header is dead inside the main loop.
-  else {
   emit_block(0);
   if (b_last == 0) {
     absorb_last(0, true);
@@ -746,83 +657,49 @@ __global__ __launch_bounds__(64 * K1_WAVES, K1Occ<MODE>::value) void xof_kernel(
     if (have) emit_block(b_last);
     absorb_last(b_last, have);
   }
-  }
   uint32_t own_part[4] = {J[0], J[1], J[2], J[3]};
 
-  // ---- proof share ------------------------------------------------------------------
+  // ---- proof share: XOF(k_proofs, DST(2), [PROOFS=1, agg_id=1]) ----------------------
   uint4* const pp = b.proof + il_idx(blk, c.proof_len, 0, lane);
-  if (LEADER) {
-    const uint4* src = reinterpret_cast<const uint4*>(ls + MB);
-#pragma unroll 1
-    for (uint32_t e = 0; e < c.proof_len; e++) {
-      const uint4 v = src[e];
-      bad |= ge_exact(v);
-      pp[(uint64_t)e * IL] = v;
-    }
-  } else if (!ABSORB_ONLY) {  // XOF(k_proofs, DST(2), [PROOFS=1, agg_id=1])
-    {
-      uint32_t kproof[4];
-      load16(hs + 16, kproof);
-      Block m;
-      blk_zero(m);
-      int pos = blk_xof_prefix(m, c.dst_id, 2, kproof);
-      blk_put_byte(m, pos, 1);
-      blk_put_byte(m, pos + 1, 1);
-      blk_pad(m, pos + 2);
-      sponge_oneblock(S, m);
-    }
-    const uint32_t NP = (c.proof_len * 16 + 167) / 168;
-#pragma unroll 1
-    for (uint32_t m = 0; m < NP; m++) {
-      if (m > 0) keccak_p12(S);
-      const uint32_t e0 = 21 * (m >> 1);
-      if ((m & 1) == 0) {
-#pragma unroll
-        for (int ci = 0; ci < 10; ci++)
-          emit_proof(c, pp, e0 + ci, make_uint4(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]), gmax);
-        carry0 = S[40];
-        carry1 = S[41];
-      } else {
-        emit_proof(c, pp, e0 + 10, make_uint4(carry0, carry1, S[0], S[1]), gmax);
-#pragma unroll
-        for (int ci = 0; ci < 10; ci++)
-          emit_proof(c, pp, e0 + 11 + ci, make_uint4(S[2 + 4 * ci], S[3 + 4 * ci], S[4 + 4 * ci], S[5 + 4 * ci]),
-                     gmax);
-      }
-    }
-    if (gmax == 0xFFFFFFFFu) flags |= FLAG_SLOW;
+  {
+    uint32_t kproof[4];
+    load16(hs + 16, kproof);
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.dst_id, 2, kproof);
+    blk_put_byte(m, pos, 1);
+    blk_put_byte(m, pos + 1, 1);
+    blk_pad(m, pos + 2);
+    sponge_oneblock(S, m);
   }
-  if (SQUEEZE_ONLY) {  // the absorb-only launch finishes the report (and ORs these flags in)
-    if (b.force_slow) flags |= FLAG_SLOW;
-    if (r0 < b.n) b.flags[r0] = flags;
-    return;
+  const uint32_t NP = (c.proof_len * 16 + 167) / 168;
+#pragma unroll 1
+  for (uint32_t m = 0; m < NP; m++) {
+    if (m > 0) keccak_p12(S);
+    const uint32_t e0 = 21 * (m >> 1);
+    if ((m & 1) == 0) {
+#pragma unroll
+      for (int ci = 0; ci < 10; ci++)
+        emit_proof(c, pp, e0 + ci, make_uint4(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]), gmax);
+      carry0 = S[40];
+      carry1 = S[41];
+    } else {
+      emit_proof(c, pp, e0 + 10, make_uint4(carry0, carry1, S[0], S[1]), gmax);
+#pragma unroll
+      for (int ci = 0; ci < 10; ci++)
+        emit_proof(c, pp, e0 + 11 + ci, make_uint4(S[2 + 4 * ci], S[3 + 4 * ci], S[4 + 4 * ci], S[5 + 4 * ci]), gmax);
+    }
   }
+  if (gmax == 0xFFFFFFFFu) flags |= FLAG_SLOW;
 
   uint32_t nonce[4];
   load16(b.nonces + 16 * r, nonce);
-  if (LEADER) {
-    // corrected seed = XOF(0, DST(6), own part || helper's part from the public share): the
-    // leader's prepare state (written to msgs), and own part goes out in the prep share
-    uint32_t part_h[4];
-    load16(b.ps + (uint64_t)c.ps_bytes * r + 16, part_h);
-    flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, own_part, own_part, part_h, flags, false);
-    if (flags & FLAG_SLOW)  // a rejected joint/query randomness sample (~2^-120): redo exactly
-      flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, own_part, own_part, part_h, flags & ~FLAG_SLOW, true);
-    if (bad) flags |= FLAG_INPUT_FAIL;
-    if (r0 < b.n) {
-      *reinterpret_cast<uint4*>(b.lps_out + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16) =
-          make_uint4(own_part[0], own_part[1], own_part[2], own_part[3]);
-      b.flags[r0] = flags;
-    }
-  } else {
-    uint32_t part_l[4], lead_part[4];
-    load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
-    load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
-    if (ABSORB_ONLY) flags |= b.flags[r];  // the squeeze-only launch's screen
-    flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, part_l, lead_part, own_part, flags, false);
-    if (b.force_slow) flags |= FLAG_SLOW;
-    if (r0 < b.n) b.flags[r0] = flags;
-  }
+  uint32_t part_l[4], lead_part[4];
+  load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
+  load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
+  flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, part_l, lead_part, own_part, flags, false);
+  if (b.force_slow) flags |= FLAG_SLOW;
+  if (r0 < b.n) b.flags[r0] = flags;
 }
 
 // ---------------------------------------------------------------------------- K1, lane-split helper
@@ -1646,10 +1523,10 @@ __device__ __forceinline__ void psum_part_finish(const Cfg& c, const Bufs& b, ui
 // slots, its share of v (sum_m g_m S_m), its share of G(t), and (Histogram) sum of x.
 // Phase 2 (flp_psum_final_kernel): one report per lane; adds the partials, the leader's
 // v and G(t), and decides.
-// PF: calls whose loads are in flight ahead of the one being multiplied (a ring of PF register
-// sets; the HBM latency is several calls' worth of VALU work at 4 waves/SIMD).
-template <int PPW, bool HIST, bool LEADER, int PF = 1, int OCC = 4>
-__global__ __launch_bounds__(64, OCC) void flp_psum_part_kernel(Cfg c, Bufs b) {
+// PF: calls whose loads are in flight ahead of the one being multiplied (1: deeper register
+// prefetch measured no faster). Used for PPW = 1; PPW = 2 takes the LDS-DMA ring kernel below.
+template <int PPW, bool HIST, bool LEADER, int PF = 1>
+__global__ __launch_bounds__(64, 4) void flp_psum_part_kernel(Cfg c, Bufs b) {
   const uint32_t NG = c.ngroups;
   // Workgroup ids are dispatched round-robin over the 8 XCDs; map them so that the NG
   // groups of one block run back to back on one XCD and share its L2 (coefficients,
@@ -1741,7 +1618,7 @@ __device__ __forceinline__ void glds16(const uint4* src, uint4* lds_row) {
   __builtin_amdgcn_global_load_lds((const void*)src, (void*)lds_row, 16, 0, 0);
 }
 
-// K3 with an LDS-DMA ring (k3_pf = 20 / 21: D = 3 / 4). A workgroup is K3W waves = K3W consecutive slot
+// K3 with an LDS-DMA ring of depth D (4). A workgroup is K3W waves = K3W consecutive slot
 // groups of one 64-report block. Per call k, wave 0 streams c_k and wave 1 d_k (one
 // global_load_lds_dwordx4 each: 1 KiB, the block's 64 reports) into ring slot (k-1) % D, and every live
 // wave its own PPW measurement elements; the coefficients are fetched once per K3W groups instead of
@@ -1769,11 +1646,8 @@ __device__ __forceinline__ void lds_read4(uint32_t a0, uint32_t a1, uint32_t a2,
       : "v"(a0), "v"(a1), "v"(a2), "v"(a3)
       : "memory");
 }
-// PROBE (timing experiments only, results are wrong): 1 = loads and barriers without the limb
-// products, 2 = limb products on whatever the ring holds, without loads, 3 = like 1 but every
-// workgroup streams one contiguous region (8 KiB per call) instead of the staging's call stride
 // W: waves (slot groups) per workgroup
-template <int PPW, bool HIST, bool LEADER, int D, int PROBE = 0, int W = K3W>
+template <int PPW, bool HIST, bool LEADER, int D, int W = K3W>
 __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bufs b) {
   static_assert(PPW == 2, "lds_read4 reads c, d and two measurement rows");
   constexpr int ROWS = 2 + W * PPW;  // c_k, d_k, then x[wave][i]
@@ -1806,14 +1680,12 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
   acc_zero(sx);
   // loads of call k into ring slot (k - 1) % D
   auto issue = [&](uint32_t k) {
-    if (PROBE == 2) return;
     const uint32_t sl = (k - 1) % D;
     if (wave < 2) glds16(coefb + (uint64_t)(COEF_K + 2 * (k - 1) + wave) * IL, &ring[sl][wave][0]);
     if (full) {
 #pragma unroll
       for (int i = 0; i < PPW; i++) {
-        const uint64_t e = PROBE == 3 ? (uint64_t)wg * kfw * (W * PPW) + (k - 1) * (W * PPW) + wave * PPW + i
-                                      : (uint64_t)((k - 1) * chunk + j0 + i);
+        const uint64_t e = (uint64_t)((k - 1) * chunk + j0 + i);
         glds16(measb + e * IL, &ring[sl][2 + wave * PPW + i][0]);
       }
     }
@@ -1838,7 +1710,7 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
     wait_call(k + D - 2 > kfw);  // near the end fewer calls are in flight: wait for all
     __builtin_amdgcn_s_barrier();
     if (k + D - 1 <= kfw) issue(k + D - 1);
-    if (full && PROBE != 1 && PROBE != 3) {
+    if (full) {
       const uint32_t a = ring_base + ((k - 1) % D) * SLOT_BYTES;
       uint4 cv, dv, xv[PPW];
       lds_read4(a, a + ROW_BYTES, a + (2 + wave * PPW) * ROW_BYTES, a + (3 + wave * PPW) * ROW_BYTES, cv, dv, xv[0],
@@ -2428,10 +2300,16 @@ __global__ void combine_kernel(Cfg c, const uint8_t* parts, uint32_t nparts, uin
 
 // shard record = encoded aggregate share || count (u64 LE) || checksum (32 B), see
 // janus_amd/distributed.py. Thread i < out_len writes element i; thread out_len the tail.
+// blockIdx.y = record: ns records from contiguous segment state (agg [ns][out_len], count [ns],
+// checksum [ns][8]) to ns back-to-back records
 __global__ void record_export_kernel(Cfg c, const uint4* agg, const unsigned long long* count,
                                      const uint32_t* checksum, uint8_t* dst) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t fb = c.fb;
+  const uint32_t fb = c.fb, y = blockIdx.y;
+  agg += (uint64_t)y * c.out_len;
+  count += y;
+  checksum += 8 * y;
+  dst += (uint64_t)y * (c.out_len * fb + 40u);
   if (i < c.out_len) {
     uint4 v = agg[i];
     for (uint32_t k = 0; k < fb; k++) {
@@ -2544,32 +2422,16 @@ hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
     hipLaunchKernelGGL((xof_leader_kernel<true>), grid, block, 0, s, c, b);
   else if (b.leader)
     hipLaunchKernelGGL((xof_leader_kernel<false>), grid, block, 0, s, c, b);
-  else if (b.k1_split == 5) {  // the fused kernel, forced (tests; the engine picks lanes for small launches)
-    if (wide)
-      hipLaunchKernelGGL((xof_kernel<K1_FUSED, true>), grid, block, 0, s, c, b);
-    else
-      hipLaunchKernelGGL((xof_kernel<K1_FUSED, false>), grid, block, 0, s, c, b);
-  } else if (b.k1_split == 3) {  // lane-split: 32 reports per wave
+  else if (b.k1_split == 3) {  // lane-split: 32 reports per wave
     const dim3 g2((2 * nb + K1_WAVES - 1) / K1_WAVES);
     if (wide)
       hipLaunchKernelGGL((xof_lanes_kernel<true>), g2, block, 0, s, c, b);
     else
       hipLaunchKernelGGL((xof_lanes_kernel<false>), g2, block, 0, s, c, b);
-  } else if (b.k1_split == 4 && !wide)
-    hipLaunchKernelGGL((xof_kernel<K1_SEQ, false>), grid, block, 0, s, c, b);
-  else if (b.k1_split && wide) {
-    hipLaunchKernelGGL((xof_kernel<K1_SQUEEZE, true>), grid, block, 0, s, c, b);
-    hipLaunchKernelGGL((xof_kernel<K1_ABSORB, true>), grid, block, 0, s, c, b);
-  } else if (b.k1_split == 2) {
-    hipLaunchKernelGGL((xof_kernel<K1_SQUEEZE, false>), grid, block, 0, s, c, b);
-    hipLaunchKernelGGL((xof_kernel<K1_ABSORB2, false>), grid, block, 0, s, c, b);
-  } else if (b.k1_split) {
-    hipLaunchKernelGGL((xof_kernel<K1_SQUEEZE, false>), grid, block, 0, s, c, b);
-    hipLaunchKernelGGL((xof_kernel<K1_ABSORB, false>), grid, block, 0, s, c, b);
   } else if (wide)
-    hipLaunchKernelGGL((xof_kernel<K1_FUSED, true>), grid, block, 0, s, c, b);
+    hipLaunchKernelGGL((xof_kernel<true>), grid, block, 0, s, c, b);
   else
-    hipLaunchKernelGGL((xof_kernel<K1_FUSED, false>), grid, block, 0, s, c, b);
+    hipLaunchKernelGGL((xof_kernel<false>), grid, block, 0, s, c, b);
   return hipGetLastError();
 }
 // Reports that occupy every K1 wave slot of the device exactly once: CUs x resident
@@ -2588,10 +2450,8 @@ uint64_t k1_round_reports(const Cfg& c, int device, uint32_t k1_split) {
   } else if (k1_split == 3) {
     st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_lanes_kernel<false>, threads, 0);
     per_wg = threads / 2;
-  } else if (k1_split == 4) {
-    st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_kernel<K1_SEQ>, threads, 0);
   } else {
-    st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_kernel<K1_FUSED>, threads, 0);
+    st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_kernel<false>, threads, 0);
   }
   if (st != hipSuccess || wgs <= 0) return 0;
   return (uint64_t)cus * (uint64_t)wgs * per_wg;
@@ -2629,42 +2489,17 @@ int psum_ppw(uint32_t chunk) {
   return best;
 }
 
-// k3_pf: calls of loads in flight, + 10 for the 3-waves/SIMD (168-VGPR) build; 20 / 21: the LDS-DMA ring
+// K3 phase 1: the depth-4 LDS-DMA ring (K3W slot groups per workgroup) for PPW = 2; the per-wave
+// register-prefetch kernel for PPW = 1 (chunk_length 1). Measured and removed:
+// 2 / 3 calls of register prefetch, 3-waves/SIMD builds, a depth-3 ring, 8 groups per workgroup.
 template <int PPW, bool HIST, bool LEADER>
 static void launch_psum_part(const Cfg& c, const Bufs& b, hipStream_t s, uint32_t grid) {
   if constexpr (PPW == 2) {
-    if (b.k3_pf == 20 || b.k3_pf == 21) {  // LDS-DMA ring, K3W groups per workgroup
-      const uint32_t g2 = grid / c.ngroups * ((c.ngroups + K3W - 1) / K3W);
-      if (b.k3_pf == 20)
-        hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 3>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
-      else
-        hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
-      return;
-    }
-    if (b.k3_pf == 26) {  // depth-4 ring, 8 slot groups per workgroup
-      const uint32_t g2 = grid / c.ngroups * ((c.ngroups + 7) / 8);
-      hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4, 0, 8>), dim3(g2), dim3(64 * 8), 0, s, c, b);
-      return;
-    }
-    if (b.k3_pf == 22 || b.k3_pf == 23 || b.k3_pf == 25) {  // timing probes (wrong results)
-      const uint32_t g2 = grid / c.ngroups * ((c.ngroups + K3W - 1) / K3W);
-      if (b.k3_pf == 25)
-        hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4, 3>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
-      else if (b.k3_pf == 22)
-        hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4, 1>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
-      else
-        hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4, 2>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
-      return;
-    }
-  }
-  if (b.k3_pf == 2)
-    hipLaunchKernelGGL((flp_psum_part_kernel<PPW, HIST, LEADER, 2>), dim3(grid), dim3(64), 0, s, c, b);
-  else if (b.k3_pf == 12)
-    hipLaunchKernelGGL((flp_psum_part_kernel<PPW, HIST, LEADER, 2, 3>), dim3(grid), dim3(64), 0, s, c, b);
-  else if (b.k3_pf == 13)
-    hipLaunchKernelGGL((flp_psum_part_kernel<PPW, HIST, LEADER, 3, 3>), dim3(grid), dim3(64), 0, s, c, b);
-  else
+    const uint32_t g2 = grid / c.ngroups * ((c.ngroups + K3W - 1) / K3W);
+    hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
+  } else {
     hipLaunchKernelGGL((flp_psum_part_kernel<PPW, HIST, LEADER>), dim3(grid), dim3(64), 0, s, c, b);
+  }
 }
 template <int PPW, bool HIST, bool LEADER>
 static void launch_psum_r(const Cfg& c, const Bufs& b, hipStream_t s) {
@@ -2764,8 +2599,8 @@ hipError_t launch_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, u
   return hipGetLastError();
 }
 hipError_t launch_record_export(const Cfg& c, const uint4* agg, const unsigned long long* count,
-                                const uint32_t* checksum, uint8_t* dst, hipStream_t s) {
-  hipLaunchKernelGGL(record_export_kernel, dim3((c.out_len + 1 + 255) / 256), dim3(256), 0, s, c, agg, count,
+                                const uint32_t* checksum, uint8_t* dst, hipStream_t s, uint32_t ns) {
+  hipLaunchKernelGGL(record_export_kernel, dim3((c.out_len + 1 + 255) / 256, ns), dim3(256), 0, s, c, agg, count,
                      checksum, dst);
   return hipGetLastError();
 }

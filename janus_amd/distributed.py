@@ -106,32 +106,45 @@ class ShardCombiner:
 
     export -> RCCL all-gather (one collective of world x record_bytes) -> device merge.
     Every rank ends up with the merged record (all-gather, not gather: any rank can serve
-    the aggregate share)."""
+    the aggregate share). The engine runs on its own HIP stream; the three steps are ordered
+    with stream waits (engine stream -> torch's current stream, on which the collective's
+    result is ready -> engine stream), so a combine never blocks the host. The record, gather
+    and merge buffers are allocated once and live as long as the combiner, so no buffer the
+    engine stream may still read is ever handed back to torch's allocator mid-flight."""
 
     def __init__(self, engine, group=None):
         import torch
+        import torch.distributed as dist
 
         self.engine = engine
         self.group = group
         self.nbytes = record_bytes(engine.output_len, engine.field_bytes)
-        dev = torch.device("cuda", engine.device)
-        self.record = torch.zeros(self.nbytes, dtype=torch.uint8, device=dev)
-        self.merged = torch.zeros(self.nbytes, dtype=torch.uint8, device=dev)
+        self.dev = torch.device("cuda", engine.device)
+        self.world = dist.get_world_size(group)
+        self.record = torch.zeros(self.nbytes, dtype=torch.uint8, device=self.dev)
+        self.gathered = torch.zeros((self.world, self.nbytes), dtype=torch.uint8, device=self.dev)
+        self.merged = torch.zeros(self.nbytes, dtype=torch.uint8, device=self.dev)
+        self.stream = torch.cuda.ExternalStream(engine.stream(), device=self.dev)
 
     def combine(self, segment: int = 0):
+        """Queue export -> all-gather -> merge; the merged record is ready on the engine stream
+        (engine.sync() or any later engine call orders after it)."""
         import torch
         import torch.distributed as dist
 
+        cur = torch.cuda.current_stream(self.dev)
         self.engine.export_record_device(segment, self.record.data_ptr())
-        self.engine.sync()  # the engine stream is not torch's stream
+        # the all-gather reads the exported record and overwrites `gathered`, which the previous merge
+        # (queued before the export on the engine stream) has read
+        cur.wait_stream(self.stream)
         if dist.get_backend(self.group) == "gloo":  # gloo gathers host tensors (CPU tests, 1-GPU boxes)
-            gathered = all_gather_records(self.record.cpu(), self.group).to(self.record.device)
-        else:  # RCCL over xGMI
-            gathered = all_gather_records(self.record, self.group)
-        torch.cuda.current_stream().synchronize()
-        self.engine.combine_records_device(gathered.data_ptr(), gathered.shape[0], self.merged.data_ptr())
-        self.engine.sync()
+            self.gathered.copy_(all_gather_records(self.record.cpu(), self.group))
+        else:  # RCCL over xGMI into the persistent buffer; ready on the current stream when the call returns
+            dist.all_gather(list(self.gathered.unbind(0)), self.record, group=self.group)
+        self.stream.wait_stream(cur)  # the merge reads the gathered records
+        self.engine.combine_records_device(self.gathered.data_ptr(), self.world, self.merged.data_ptr())
         return self.merged
 
     def result(self) -> tuple[bytes, int, bytes]:
+        self.engine.sync()
         return unpack_record(self.merged.cpu().numpy(), self.engine.field_bytes)

@@ -8,10 +8,13 @@ Janus calls per report at /root/reference/aggregator/src/aggregator.rs:1945-1967
 
 `HelperEngine.helper_initialized_batch` does that for a whole batch and returns, per
 report, either the outbound `PingPongMessage::Finish{prep_msg}` or a verdict naming the
-`PingPongError` variant (labels of aggregator/src/aggregator/error.rs:379-424).
-`accumulate` is `BatchAggregation::merged_with` (aggregator_core/src/datastore/models.rs:
-1275-1330) for the finished reports, with an accept mask and per-report batch segment so
-the host can drop replayed / collected reports first (aggregation_job_writer.rs:557-704).
+`PingPongError` variant (labels of aggregator/src/aggregator/error.rs:379-424), plus the
+handle of the new resident batch (one per aggregation job in flight; any number can be
+resident). `aggregate_records` turns a batch into per-batch-identifier deltas
+(BatchAggregation rows to merge with `merged_with`, aggregator_core/src/datastore/
+models.rs:1275-1330) without changing the engine, so a retried datastore transaction can
+recompute them; `accumulate` merges a batch into the engine's running aggregations (the
+engine as one shard) and releases it.
 
 All compute runs in the HIP kernels of libjanus_prio3.so; nothing here falls back to the CPU.
 """
@@ -72,7 +75,7 @@ def _seg_table(segment_ids):
 class LeaderInit:
     verdicts: np.ndarray       # uint8[n]: 0 initialized, 1 prepare_init_failure
     prep_shares: np.ndarray    # uint8[n, LPS]: payloads of PingPongMessage::Initialize
-    batch_id: int = 0          # names the engine's resident leader batch (finish / accumulate)
+    batch_id: int = 0          # the resident leader batch (finish / records / accumulate / release)
 
 
 @dataclass
@@ -80,7 +83,7 @@ class BatchResult:
     verdicts: np.ndarray       # uint8[n]
     prep_msgs: np.ndarray      # uint8[n, PM]
     out_shares: np.ndarray | None  # uint8[n, OUT*FB]
-    batch_id: int = 0          # the resident batch these results belong to (for accumulate)
+    batch_id: int = 0          # the resident batch these results belong to (records / accumulate / release)
 
     def finished(self) -> np.ndarray:
         return self.verdicts == FINISHED
@@ -154,18 +157,51 @@ class HelperEngine:
         verdicts = np.zeros(max(n, 1), np.uint8)
         msgs = np.zeros((max(n, 1), max(self.prep_msg_len, 1)), np.uint8)
         outs = np.zeros((max(n, 1), self.output_len * self.field_bytes), np.uint8) if want_out_shares else None
+        bid = ctypes.c_uint64()
         st = self._L.jx_helper_prep_batch(self._h, n, _ptr(nn), _ptr(ps) if self.public_share_len else None,
                                           _ptr(his), _ptr(lps), _ptr(msgs) if self.prep_msg_len else None,
-                                          _ptr(verdicts), _ptr(outs))
+                                          _ptr(verdicts), _ptr(outs), ctypes.byref(bid))
         check(st, self._h, "jx_helper_prep_batch")
         return BatchResult(verdicts[:n], msgs[:n, : self.prep_msg_len], outs[:n] if outs is not None else None,
-                           self.batch_id())
+                           bid.value)
 
     def batch_id(self) -> int:
-        """Id of the resident prepared batch (0: none / already accumulated)."""
+        """Handle of the most recently prepared batch if still resident (0 otherwise)."""
         b = ctypes.c_uint64()
         check(self._L.jx_engine_batch_id(self._h, ctypes.byref(b)), self._h, "jx_engine_batch_id")
         return b.value
+
+    def resident_batches(self) -> tuple[int, int]:
+        """(resident batches, device bytes they hold)."""
+        n, b = ctypes.c_uint64(), ctypes.c_uint64()
+        check(self._L.jx_engine_batches(self._h, ctypes.byref(n), ctypes.byref(b)), self._h, "jx_engine_batches")
+        return n.value, b.value
+
+    def release(self, batch_id: int):
+        """Drop a resident batch (an aggregation job that is done or abandoned)."""
+        check(self._L.jx_batch_release(self._h, batch_id), self._h, "jx_batch_release")
+
+    def aggregate_records(self, batch_id: int, n: int, accept_mask: np.ndarray | None = None,
+                          segment_index: np.ndarray | None = None, nsegments: int = 1) -> list[tuple[bytes, int, bytes]]:
+        """Per-batch-identifier deltas of a resident batch: for each of nsegments aggregations, the
+        (encoded aggregate share, report count, checksum) of the finished reports i with
+        accept_mask[i] and segment_index[i] == that index. Changes nothing on the engine: repeatable
+        (a retried transaction recomputes the same rows), the batch stays resident."""
+        m = None if accept_mask is None else np.ascontiguousarray(accept_mask, dtype=np.uint8)
+        s = None if segment_index is None else np.ascontiguousarray(segment_index, dtype=np.uint32)
+        rb = self.record_bytes()
+        out = np.zeros(nsegments * rb, np.uint8)
+        check(self._L.jx_batch_aggregate_records(self._h, batch_id, n, _ptr(m), _ptr(s), nsegments, _ptr(out)),
+              self._h, "jx_batch_aggregate_records")
+        from .distributed import unpack_record
+        return [unpack_record(out[k * rb:(k + 1) * rb], self.field_bytes) for k in range(nsegments)]
+
+    def aggregate_records_device(self, batch_id: int, n: int, d_accept_mask: int | None, d_segment_index: int | None,
+                                 nsegments: int, d_out_records: int):
+        """aggregate_records with device arrays; asynchronous on the engine stream."""
+        check(self._L.jx_batch_aggregate_records_device(self._h, batch_id, n, d_accept_mask, d_segment_index,
+                                                        nsegments, d_out_records),
+              self._h, "jx_batch_aggregate_records_device")
 
     # ------------------------------------------------------------------ leader role
     def leader_initialized_batch(self, nonces, public_shares, leader_input_shares) -> "LeaderInit":
@@ -191,7 +227,7 @@ class HelperEngine:
                                init: "LeaderInit | None" = None) -> BatchResult:
         """prio ping-pong leader_continued on the helper's Finish{prep_msg} (aggregation_job_driver.rs:
         588-602): prepare_next for the batch of `init` (default: the last leader_initialized_batch).
-        Raises EngineError (JX_E_STATE) if another prepare call has replaced that batch."""
+        Raises EngineError (JX_E_STATE) if that batch was released or already finished."""
         n = self._leader_n if init is None else len(init.verdicts)
         bid = self._leader_id if init is None else init.batch_id
         msgs = None
@@ -206,9 +242,9 @@ class HelperEngine:
 
     def accumulate(self, n: int, accept_mask: np.ndarray | None = None, segments: np.ndarray | None = None,
                    batch_id: int | None = None):
-        """Merge the finished output shares of a prepared batch into batch aggregations (at most once
-        per batch). segments[i]: the batch-aggregation id (any u32) of report i. batch_id defaults to
-        the resident batch."""
+        """Merge the finished output shares of a prepared batch into the engine's running batch
+        aggregations and release the batch (at most once per batch). segments[i]: the
+        batch-aggregation id (any u32) of report i. batch_id defaults to the last prepared batch."""
         m = None if accept_mask is None else np.ascontiguousarray(accept_mask, dtype=np.uint8)
         s = None if segments is None else np.ascontiguousarray(segments, dtype=np.uint32)
         bid = self.batch_id() if batch_id is None else batch_id

@@ -2,9 +2,10 @@
 
 Each rank prepares its contiguous shard of a golden batch on the real engine (cuda:0 on a 1-GPU
 box: both ranks share the card), then exports its shard record, all-gathers the records over
-torch.distributed (gloo: host-staged) and merges them on the device (ShardCombiner), the
-compute_aggregate_share step (aggregator/src/aggregator/aggregate_share.rs:55-96). Prints one
-JSON line with the merged record.
+torch.distributed (argv[2]: "gloo", host-staged, or "nccl" = RCCL on device tensors -- world size 1
+on a 1-GPU box, RCCL refuses two ranks on one device) and merges them on the device
+(ShardCombiner), the compute_aggregate_share step (aggregator/src/aggregator/aggregate_share.rs:
+55-96). Prints one JSON line with the merged record.
 """
 from __future__ import annotations
 
@@ -18,6 +19,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     import numpy as np
+    import torch
     import torch.distributed as dist
 
     from janus_amd import distributed as D
@@ -25,8 +27,13 @@ def main():
     from janus_amd.vdaf import Prio3
 
     name = sys.argv[1]
+    backend = sys.argv[2] if len(sys.argv) > 2 else "gloo"
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     doc = json.load(open(os.path.join(ROOT, "tests", "golden", name)))
     reps = doc["reports"]
     n = len(reps)
@@ -43,10 +50,13 @@ def main():
                                cat("leader_prep_share")[a:b], segment=0)
         comb = D.ShardCombiner(eng)
         comb.combine(0)
+        # a second round on the same buffers, queued without a host sync in between: the
+        # stream ordering alone must keep export -> gather -> merge in order
+        comb.combine(0)
         agg, count, checksum = comb.result()
         own = eng.aggregate_share(0)
-    print(json.dumps({"rank": rank, "agg_sha": __import__("hashlib").sha256(agg).hexdigest(), "count": count,
-                      "checksum": checksum.hex(), "own_count": own[1], "shard": [a, b]}), flush=True)
+    print(json.dumps({"rank": rank, "backend": dist.get_backend(), "agg_sha": __import__("hashlib").sha256(agg).hexdigest(),
+                      "count": count, "checksum": checksum.hex(), "own_count": own[1], "shard": [a, b]}), flush=True)
     dist.destroy_process_group()
 
 

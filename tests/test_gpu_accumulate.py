@@ -143,12 +143,9 @@ def test_fused_device_segments_match_oracle():
 
 @pytest.mark.parametrize("name,vdaf", [("sumvec", Prio3.sum_vec(2, 50, 9)), ("histogram", Prio3.histogram(40, 5)),
                                        ("sum", Prio3.sum(7))])
-@pytest.mark.parametrize("overlap", [1, 0], ids=["two_streams", "serial"])
-def test_fused_device_multi_launch_overlap(name, vdaf, overlap):
-    """A fused device call over several launches into one aggregation: the two-stream pipeline (K1 of
-    launch i+1 beside K3 + K4 of launch i, two staging sets, jx_engine_debug option 5) and the serial
-    path give the oracle's verdicts, prep messages and aggregate (five launches: both staging sets are
-    reused)."""
+def test_fused_device_multi_launch(name, vdaf):
+    """A fused device call over five launches into one aggregation gives the oracle's verdicts, prep
+    messages and aggregate (the staging is reused launch after launch)."""
     import os
 
     import torch
@@ -165,7 +162,6 @@ def test_fused_device_multi_launch_overlap(name, vdaf, overlap):
     finally:
         del os.environ["JX_CHUNK_REPORTS"]
     with eng:
-        eng.debug(5, overlap)
         d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
         d_m = torch.zeros((n, 16), dtype=torch.uint8, device=dev)
         keep = [T(nonces), T(ps) if ps is not None else None, T(his), T(lps)]
@@ -180,9 +176,134 @@ def test_fused_device_multi_launch_overlap(name, vdaf, overlap):
         assert eng.aggregate_share(0) == (want["agg"], want["count"], want["checksum"])
 
 
-def test_batch_ids_refuse_interleaved_and_double_accumulate():
-    """two interleaved leader jobs of the same size (init A, init B, finish A) must not
-    finish A against B's device state; a batch accumulates at most once."""
+def _leader_job(orc, vdaf, n, seed):
+    rng = np.random.default_rng(seed)
+    meas = rng.integers(0, 1 << vdaf.bits, size=(n, vdaf.length), dtype=np.uint64)
+    nonces = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+    rands = rng.integers(0, 256, size=(n, orc.sizes.client_rand), dtype=np.uint8)
+    sh = [orc.shard(meas[i], nonces[i].tobytes(), rands[i].tobytes()) for i in range(n)]
+    ps, lis, his = (np.frombuffer(b"".join(s[k] for s in sh), np.uint8).reshape(n, -1) for k in range(3))
+    return nonces, ps, lis, his
+
+
+def test_interleaved_jobs_on_one_engine():
+    """three aggregation jobs in flight on ONE engine -- two leader jobs (init A, init B,
+    helper job C prepared in between, finish B, finish A) and one helper job -- each keeps its own
+    resident batch; every job's deltas equal the oracle's and are repeatable; a batch finishes and
+    accumulates at most once and a released batch is refused."""
+    vdaf = Prio3.sum_vec(4, 30, 7)
+    vk = bytes(range(5, 21))
+    orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
+    sizes = {"A": 70, "B": 50, "C": 90}
+    jobs = {k: _leader_job(orc, vdaf, sizes[k], seed) for k, seed in (("A", 1), ("B", 2), ("C", 3))}
+    with HelperEngine(vdaf, vk) as eng, HelperEngine(vdaf, vk) as peer:
+        nA, psA, lisA, hisA = jobs["A"]
+        nB, psB, lisB, hisB = jobs["B"]
+        nC, psC, lisC, hisC = jobs["C"]
+        a = eng.leader_initialized_batch(nA, psA, lisA)
+        b = eng.leader_initialized_batch(nB, psB, lisB)
+        # job C: this engine is the helper; its leader runs on the peer engine
+        c_lead = peer.leader_initialized_batch(nC, psC, lisC)
+        c = eng.helper_initialized_batch(nC, psC, hisC, c_lead.prep_shares)
+        assert len({a.batch_id, b.batch_id, c.batch_id}) == 3
+        assert eng.resident_batches()[0] == 3
+        # the helper answers A and B (on the peer engine); B finishes before A
+        hb = peer.helper_initialized_batch(nB, psB, hisB, b.prep_shares)
+        ha = peer.helper_initialized_batch(nA, psA, hisA, a.prep_shares)
+        fb = eng.leader_continued_batch(hb.prep_msgs, init=b)
+        fa = eng.leader_continued_batch(ha.prep_msgs, init=a)
+        assert not fa.verdicts.any() and not fb.verdicts.any() and not c.verdicts.any()
+        with pytest.raises(EngineError, match="call out of order"):
+            eng.leader_continued_batch(ha.prep_msgs, init=a)  # finished once
+        for name, res in (("A", a), ("B", b)):
+            nonces, ps, lis, _ = jobs[name]
+            n = sizes[name]
+            outs = [orc.prep_init(vk, 0, nonces[i].tobytes(), ps[i].tobytes(), lis[i].tobytes())[2] for i in range(n)]
+            seg = (np.arange(n) % 3).astype(np.uint32)
+            mask = (np.arange(n) % 5 != 0).astype(np.uint8)
+            recs = eng.aggregate_records(res.batch_id, n, mask, seg, 3)
+            assert recs == eng.aggregate_records(res.batch_id, n, mask, seg, 3)  # repeatable: a retried transaction
+            for k in range(3):
+                sel = [i for i in range(n) if seg[i] == k and mask[i]]
+                cs = bytes(32)
+                for i in sel:
+                    cs = bytes(x ^ y for x, y in zip(cs, O.sha256(nonces[i].tobytes())))
+                assert recs[k] == (orc.aggregate([outs[i] for i in sel]), len(sel), cs), (name, k)
+        # the helper job's records match the oracle's helper prep
+        want = orc.helper_prep_batch(vk, nC, psC, hisC, c_lead.prep_shares, nthreads=16, want_out_shares=True)
+        assert eng.aggregate_records(c.batch_id, sizes["C"]) == [(want["agg"], want["count"], want["checksum"])]
+        assert eng.aggregate_share(0)[1] == 0  # records never touch the running aggregations
+        eng.accumulate(sizes["A"], batch_id=a.batch_id)
+        with pytest.raises(EngineError, match="call out of order"):
+            eng.accumulate(sizes["A"], batch_id=a.batch_id)  # released by the accumulate: no double count
+        eng.release(b.batch_id)
+        with pytest.raises(EngineError, match="call out of order"):
+            eng.aggregate_records(b.batch_id, sizes["B"])
+        with pytest.raises(EngineError, match="invalid argument"):
+            eng.aggregate_records(c.batch_id, sizes["C"] + 1)
+        eng.release(c.batch_id)
+        assert eng.resident_batches()[0] == 0
+        assert eng.aggregate_share(0)[1] == sizes["A"]
+
+
+def test_records_device_match_host_and_skip_out_of_range():
+    import torch
+
+    from janus_amd import distributed as D
+
+    vdaf = Prio3.histogram(40, 5)
+    vk = bytes(range(16))
+    n = 1000
+    orc, nonces, ps, his, lps = _batch(vdaf, vk, n, seed=21)
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
+    rng = np.random.default_rng(4)
+    idx = rng.integers(0, 9, size=n).astype(np.uint32)  # 8 = out of range: skipped
+    mask = (rng.random(n) < 0.8).astype(np.uint8)
+    with HelperEngine(vdaf, vk) as eng:
+        res = eng.helper_initialized_batch(nonces, ps, his, lps)
+        host = eng.aggregate_records(res.batch_id, n, mask, idx, 8)
+        dev = torch.device("cuda", 0)
+        rb = eng.record_bytes()
+        d_out = torch.zeros(8 * rb, dtype=torch.uint8, device=dev)
+        d_m, d_i = torch.from_numpy(mask.copy()).to(dev), torch.from_numpy(idx.astype(np.int32)).to(dev)
+        torch.cuda.synchronize()
+        eng.aggregate_records_device(res.batch_id, n, d_m.data_ptr(), d_i.data_ptr(), 8, d_out.data_ptr())
+        eng.sync()
+        out = d_out.cpu().numpy()
+        assert [D.unpack_record(out[k * rb:(k + 1) * rb], 16) for k in range(8)] == host
+        for k in range(8):
+            sel = (want["verdicts"] == 0) & (mask == 1) & (idx == k)
+            assert host[k] == _expected(orc, want, nonces, sel), k
+
+
+def test_repeated_segment_ids_refused():
+    """a segment-id table repeating an id would race two reduce rows on one
+    aggregation; the device entry points refuse it."""
+    import torch
+
+    vdaf = Prio3.sum_vec(2, 50, 9)
+    vk = bytes(range(16))
+    n = 200
+    orc, nonces, ps, his, lps = _batch(vdaf, vk, n, seed=5)
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.array(a, copy=True)).to(dev)  # noqa: E731
+    keep = [T(nonces), T(ps), T(his), T(lps)]
+    d_seg = T((np.arange(n) % 2).astype(np.int32))
+    with HelperEngine(vdaf, vk) as eng:
+        with pytest.raises(EngineError, match="repeated"):
+            eng.prep_and_aggregate_device(*[t.data_ptr() for t in keep], n, d_segments=d_seg.data_ptr(),
+                                          segment_ids=[7, 7])
+        res = eng.helper_initialized_batch(nonces, ps, his, lps)
+        with pytest.raises(EngineError, match="repeated"):
+            eng.accumulate_device(res.batch_id, n, None, d_seg.data_ptr(), (3, 3))
+        eng.accumulate_device(res.batch_id, n, None, d_seg.data_ptr(), (3, 4))
+        eng.sync()
+        assert eng.aggregate_share(3)[1] + eng.aggregate_share(4)[1] == int((res.verdicts == 0).sum())
+
+
+def test_interleaved_count_jobs_and_double_accumulate():
+    """Two interleaved leader jobs of the same size (init A, init B, finish A) on one engine: A finishes
+    against its own device state, not B's; a batch accumulates at most once."""
     vdaf = Prio3.count()
     vk = bytes(range(16))
     orc = O.Prio3Oracle(vdaf.algo_id)
@@ -200,9 +321,10 @@ def test_batch_ids_refuse_interleaved_and_double_accumulate():
         b = leader.leader_initialized_batch(nonces[n:], empty, lis[n:])
         assert a.batch_id != b.batch_id
         with pytest.raises(EngineError, match="call out of order"):
-            leader.leader_continued_batch(None, init=a)
-        with pytest.raises(EngineError, match="call out of order"):
-            leader.accumulate(n, batch_id=a.batch_id)
+            leader.accumulate(n, batch_id=a.batch_id)  # a leader batch accumulates after its finish
+        fa = leader.leader_continued_batch(None, init=a)
+        assert not fa.verdicts.any()
+        leader.release(a.batch_id)
         hres = helper.helper_initialized_batch(nonces[n:], empty, his[n:], b.prep_shares)
         fin = leader.leader_continued_batch(None, init=b)
         assert not fin.verdicts.any() and not hres.verdicts.any()
@@ -214,6 +336,7 @@ def test_batch_ids_refuse_interleaved_and_double_accumulate():
     assert c_l == c_h == n
     p = 2**64 - 2**32 + 1
     assert (int.from_bytes(agg_l, "little") + int.from_bytes(agg_h, "little")) % p == int(meas[n:].sum())
+
 
 
 def test_device_leader_ping_pong_with_peer_verdicts():
@@ -291,8 +414,9 @@ def test_device_combine_rejects_non_canonical(name):
 
 
 def test_handler_batch_aggregations_with_writer():
-    """handle_aggregate_init over several batch identifiers with a BatchAggregationWriter: the device
-    half (share, count, checksum) and the host half (client timestamp interval over every report
+    """handle_aggregate_init over several batch identifiers with a BatchAggregationWriter: per-job deltas
+    from the resident batch merged in a transaction that is rolled back twice and retried (the rows
+    equal one clean attempt's), plus the host half (client timestamp interval over every report
     aggregation, failed ones included; None share for a batch without finished reports)."""
     from janus_amd.aggregator import handle_aggregate_init
     from janus_amd.batch_aggregation import BatchAggregationWriter, Interval
@@ -309,11 +433,14 @@ def test_handler_batch_aggregations_with_writer():
     inits = [PrepareInit(ReportShare(ReportMetadata(nonces[i].tobytes(), times[i]), ps[i].tobytes(),
                                      HpkeCiphertext(1, b"e", b"c")), PingPongMessage.initialize(lps[i].tobytes()))
              for i in range(n)]
-    w = BatchAggregationWriter(field_bytes=16)
+    w = BatchAggregationWriter(field_bytes=16, shard_count=2)
     with HelperEngine(vdaf, vk) as eng:
-        out = handle_aggregate_init(eng, inits, [his[i].tobytes() for i in range(n)], segs, writer=w)
+        out = handle_aggregate_init(eng, inits, [his[i].tobytes() for i in range(n)], segs, writer=w,
+                                    inject_tx_failures=2)
         assert want["verdicts"][0] != 0 and not out.finished[0]
-        rows = {s: w.batch_aggregation(eng, s) for s in w.segments()}
+        assert w.datastore.attempts == 3 and eng.resident_batches()[0] == 0  # the job's batch is released
+        assert eng.aggregate_share(100)[1] == 0  # deltas only: the running aggregations are untouched
+        rows = {s: w.batch_aggregation(s) for s in w.segments()}
     assert rows[999].aggregate_share is None and rows[999].report_count == 0
     assert rows[999].client_timestamp_interval == Interval.from_time(times[0])
     for s in (100, 101, 102):

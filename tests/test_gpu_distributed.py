@@ -46,6 +46,25 @@ def test_two_ranks_engine_shards_and_device_merge(name):
     assert outs[0]["shard"][1] == outs[1]["shard"][0]  # contiguous shards
 
 
+@pytest.mark.parametrize("name", ["sumvec_8x1000_88.json", "fixedpoint16_37.json", "count.json"])
+def test_rccl_world1_shard_combine(name):
+    """the RCCL branch of ShardCombiner executed -- an nccl (RCCL) process group of world
+    size 1 on the box's GPU, device-tensor all-gather ordered against the engine's own stream by stream
+    waits (no host sync between export, gather and merge; two combines queued back to back), merged
+    record == the golden fixture."""
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(HERE, "dist_worker.py"), name, "nccl"], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    o = json.loads(p.stdout.strip().splitlines()[-1])
+    doc = json.load(open(os.path.join(HERE, "golden", name)))
+    want_sha = hashlib.sha256(bytes.fromhex(doc["aggregate_share"])).hexdigest() if "aggregate_share" in doc \
+        else doc["aggregate_share_sha256"]
+    assert o["backend"] == "nccl"
+    assert o["agg_sha"] == want_sha and o["count"] == doc["report_count"] and o["checksum"] == doc["checksum"]
+
+
 def test_bench_refuses_more_gpus_than_visible():
     """bench.py --gpus N never silently measures fewer GPUs (here: N beyond the visible ones)."""
     import torch

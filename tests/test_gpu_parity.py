@@ -262,15 +262,14 @@ def test_shard_records_device_merge(name):
         e.close()
 
 
-@pytest.mark.parametrize("split", [1, 2, 3, 4, 5], ids=["absorb_occ3", "absorb_occ2", "lanes", "seq_occ3", "fused"])
+@pytest.mark.parametrize("split", [3, 5], ids=["lanes", "fused"])
 @pytest.mark.parametrize("name", ["sumvec_8x1000_88", "histogram_256_16", "sum64", "sumvec_small", "sumvec_64x20_9",
                                   "sum5", "sum32"])
 def test_k1_split_variants(name, split):
-    """The helper K1 variants == the oracle, fast and slow path: the split launches (squeeze-only, then
-    absorb-only), the lane-split kernel (S and J sponges in the two halves of a wave; the engine's choice
-    for launches under one fused wave per SIMD, i.e. every small test batch), the fused kernel with
-    sequential permutations, and the fused two-sponge kernel itself (the engine's choice for large
-    launches, forced here). sum5 has its whole joint_rand_part message in one block."""
+    """The two helper K1 kernels == the oracle, fast and slow path: the lane-split kernel (S and J sponges
+    in the two halves of a wave; the engine's choice for launches under one fused wave per SIMD, i.e.
+    every small test batch) and the fused two-sponge kernel (the engine's choice for large launches,
+    forced here). sum5 has its whole joint_rand_part message in one block."""
     vdaf = CASES[name]
     vk = bytes(range(60, 76))
     orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
@@ -286,18 +285,17 @@ def test_k1_split_variants(name, split):
         np.testing.assert_array_equal(res.out_shares[fin], want["out_shares"][fin])
         eng.accumulate(n)
         assert eng.aggregate_share(0) == (want["agg"], want["count"], want["checksum"])
-        eng.debug(1, 1)  # slow path behind the split launches
+        eng.debug(1, 1)  # slow path behind either K1 kernel
         res = eng.helper_initialized_batch(nonces, ps, his, lps)
         np.testing.assert_array_equal(res.verdicts, want["verdicts"])
 
 
-@pytest.mark.parametrize("pf", [1, 2, 12, 13, 20, 21, 26],
-                         ids=["pf1_occ4", "pf2_occ4", "pf2_occ3", "pf3_occ3", "glds3", "glds4", "glds4_w8"])
 @pytest.mark.parametrize("name", ["sumvec_8x1000_88", "histogram_256_16", "sumvec_64x20_9", "sumvec_small"])
-def test_k3_pipeline_variants(name, pf):
-    """The deeper-pipelined ParallelSum FLP part kernels (register rings; the LDS-DMA ring of depth 3 / 4
-    with 4 slot groups per workgroup) == the oracle, helper (verdicts, messages, output shares,
-    aggregate) and leader (prep shares). sumvec_64x20_9 and sumvec_small have a padded last group."""
+def test_k3_ring_padded_groups(name):
+    """The ParallelSum FLP part kernel (the depth-4 LDS-DMA ring, 4 slot groups per workgroup) == the
+    oracle, helper (verdicts, messages, output shares, aggregate) and leader (prep shares).
+    sumvec_64x20_9 and sumvec_small have a padded last group and workgroup."""
+    pf = 21
     vdaf = CASES[name]
     vk = bytes(range(90, 106))
     orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
@@ -305,7 +303,6 @@ def test_k3_pipeline_variants(name, pf):
     nonces, ps, his, lps = _random_batch(orc, vk, n, seed=pf * 11 + sum(map(ord, name)))
     want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
     with HelperEngine(vdaf, vk) as eng:
-        eng.debug(4, pf)
         res = eng.helper_initialized_batch(nonces, ps, his, lps, want_out_shares=True)
         np.testing.assert_array_equal(res.verdicts, want["verdicts"])
         fin = want["verdicts"] == 0
@@ -321,7 +318,6 @@ def test_k3_pipeline_variants(name, pf):
     shards = [orc.shard(meas[i], ln[i].tobytes(), rands[i].tobytes()) for i in range(24)]
     lps_, lis_ = (np.stack([np.frombuffer(s[k], np.uint8) for s in shards]) for k in (0, 1))
     with HelperEngine(vdaf, vk) as eng:
-        eng.debug(4, pf)
         init = eng.leader_initialized_batch(ln, lps_, lis_)
     for i in range(24):
         rc, share, _, _ = orc.prep_init(vk, 0, ln[i].tobytes(), lps_[i].tobytes(), lis_[i].tobytes())

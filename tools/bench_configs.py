@@ -8,8 +8,9 @@ here; Sum32 / Histogram: 1M reports). Per config: a pool of K distinct client re
 client + leader prep_init, 1 % tampered) tiled on the device, inputs resident in HBM; `steps`
 fused jx_helper_prep_aggregate_device calls are timed between torch.cuda.synchronize(); the
 aggregate share and count are verified against multiplicity x the oracle's output shares, and
-every verdict against the oracle. The C oracle on the host's cores is timed beside it on a
-bounded sample (kind "port"). One JSON line per config.
+every verdict against the oracle. The C++ CPU engine (cpu_baseline/jc_cpu_engine.cpp) is timed
+beside it on the host's cores at 1 thread and at the affinity/cgroup thread budget (kind "port"),
+with the literal C oracle port as a secondary figure. One JSON line per config.
 
     python tools/bench_configs.py [--only count,sum32,hist] [--cpu-seconds 3]
 """
@@ -30,7 +31,7 @@ P64 = 2**64 - 2**32 + 1
 P128 = 2**128 - 28 * 2**64 + 1
 
 
-def run(name, vdaf, meas_fn, R, K, steps, warmup, cpu_seconds, threads):
+def run(name, vdaf, meas_fn, R, K, steps, warmup, cpu_seconds, threads, cpu):
     import torch
 
     from janus_amd.engine import HelperEngine
@@ -91,15 +92,32 @@ def run(name, vdaf, meas_fn, R, K, steps, warmup, cpu_seconds, threads):
     verified = agg == exp and count == total * int(mult[fin].sum()) and \
         bool(np.array_equal(d_v.cpu().numpy(), np.tile(want["verdicts"], reps)[:R]))
 
-    # CPU baseline: the C oracle on this host's cores, ~cpu_seconds of work
+    # CPU baseline: the C++ CPU engine (cpu_baseline/jc_cpu_engine.cpp, byte-checked against the fixtures)
+    # at 1 thread and at the host's thread budget on ~cpu_seconds of work each; the literal C oracle
+    # port beside it as a secondary figure
+    from cpu_baseline import cpu_engine as CE
+
+    def engine_rate(nth, budget):
+        m = min(K, max(64, 32 * nth))
+        t = time.perf_counter()
+        CE.helper_prep_aggregate(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length, vk, nonces[:m], ps[:m],
+                                 his[:m], lps[:m], nthreads=nth)
+        r0 = m / (time.perf_counter() - t)
+        nn = max(m, int(budget * r0))
+        idx = np.arange(nn) % K
+        t = time.perf_counter()
+        got = CE.helper_prep_aggregate(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length, vk, nonces[idx],
+                                       ps[idx], his[idx], lps[idx], nthreads=nth)
+        dt_ = time.perf_counter() - t
+        assert np.array_equal(got["verdicts"], want["verdicts"][idx])
+        return nn / dt_, nn, dt_
+
+    r1, n1, d1 = engine_rate(1, cpu_seconds * 0.4)
+    rN, nN, dN = engine_rate(cpu["threads"], cpu_seconds * 0.6)
+    m = min(K, 512)
     t = time.perf_counter()
-    orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=threads)
-    rate0 = K / (time.perf_counter() - t)
-    creps = max(1, int(cpu_seconds * rate0 / K))
-    ct = lambda a: np.ascontiguousarray(np.tile(a, (creps, 1)))  # noqa: E731
-    t = time.perf_counter()
-    orc.helper_prep_batch(vk, ct(nonces), ct(ps), ct(his), ct(lps), nthreads=threads)
-    cdt = time.perf_counter() - t
+    orc.helper_prep_batch(vk, nonces[:m], ps[:m], his[:m], lps[:m], nthreads=cpu["threads"])
+    r_oracle = m / (time.perf_counter() - t)
 
     def per_launch(stage):
         return round(kt[stage]["ms"] / max(1, kt[stage]["launches"]), 3)
@@ -112,9 +130,11 @@ def run(name, vdaf, meas_fn, R, K, steps, warmup, cpu_seconds, threads):
         "kernels": {"k1_ms_per_launch": per_launch("xof"), "k3_ms_per_launch": per_launch("flp"),
                     "k4_ms_per_launch": per_launch("accumulate"), "launches_per_step": kt["xof"]["launches"] // steps},
         "verified": verified,
-        "cpu_baseline": {"value": round(creps * K / cdt, 1), "unit": "reports/s", "cores": threads, "kind": "port",
-                         "sample": f"{creps * K} reports ({K} distinct x {creps}), C oracle, {threads} threads, "
-                                   f"{cdt:.1f} s"},
+        "cpu_baseline": {"value": round(rN, 1), "unit": "reports/s", "cores": cpu["threads"], "kind": "port",
+                         "engine": "cpu_baseline/jc_cpu_engine.cpp", "value_1_thread": round(r1, 1),
+                         "oracle_port_reports_per_s": round(r_oracle, 1), **cpu,
+                         "sample": f"{nN} reports at {cpu['threads']} threads ({dN:.1f} s) and {n1} at 1 thread "
+                                   f"({d1:.1f} s), pool of {K} tiled, verdicts checked; C oracle on {m} reports"},
     }
 
 
@@ -128,7 +148,10 @@ def main():
     a = ap.parse_args()
     from janus_amd.vdaf import Prio3
 
-    threads = min(16, os.cpu_count() or 1)
+    from bench import cpu_threads
+
+    cpu = cpu_threads()
+    threads = min(16, cpu["threads"])  # pool generation
     cfgs = {
         "count100k": ("Prio3Count (configs[0]: 100k reports)", Prio3.count(),
                       lambda rng, K: rng.integers(0, 2, size=(K, 1), dtype=np.uint64), 100_000),
@@ -141,7 +164,7 @@ def main():
     }
     for key in a.only.split(","):
         name, vdaf, fn, R = cfgs[key]
-        print(json.dumps(run(name, vdaf, fn, R, a.pool, a.steps, a.warmup, a.cpu_seconds, threads)), flush=True)
+        print(json.dumps(run(name, vdaf, fn, R, a.pool, a.steps, a.warmup, a.cpu_seconds, threads, cpu)), flush=True)
 
 
 if __name__ == "__main__":

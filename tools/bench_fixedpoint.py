@@ -13,7 +13,8 @@ helper-only rate (the north-star unit) and per-role kernel times are reported to
 of K distinct client reports (C-oracle shard; 1 in 6 claims a false norm and must be rejected)
 tiled on the device. Verified: both aggregates add up to multiplicity x the sum of the accepted
 entries' encodings, and every verdict matches the oracle. The C oracle (leader prep_init + helper
-prep per report) is timed on the host beside it (kind "port").
+prep per report) and the C++ CPU engine's two roles (the baseline proper) are timed on the host
+beside it (kind "port").
 
     python tools/bench_fixedpoint.py [--bits 16 --length 10000 --reports 8192 --pool 48]
 """
@@ -40,6 +41,7 @@ def main():
     ap.add_argument("--pool", type=int, default=48)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     a = ap.parse_args()
 
     import torch
@@ -127,15 +129,37 @@ def main():
         np.array_equal(d_hv.cpu().numpy(), np.tile(want["verdicts"], reps)[:R]) and \
         np.array_equal(d_lv.cpu().numpy() == 0, np.tile(fin, reps)[:R])
 
-    # CPU baseline: the C oracle's leader prep_init + helper prep of the same reports
-    m = min(K, 6)
+    # CPU baseline: the C++ CPU engine's leader prep_init -> helper prep + aggregate -> leader finish +
+    # aggregate (cpu_baseline/jc_cpu_engine.cpp, byte-checked against the oracle) at 1 thread and at the
+    # host's thread budget; the literal C oracle (leader prep_init + helper prep) per core beside it
+    from bench import cpu_threads
+    from cpu_baseline import cpu_engine as CE
+
+    cpu = cpu_threads()
+
+    def cpu_ping_pong(nth, m):
+        idx = np.arange(m) % K
+        t = time.perf_counter()
+        ld = CE.leader_prep_init(5, a.bits, a.length, 0, vk, nonces[idx], ps[idx], lis[idx], vdaf.prep_share_len,
+                                 nthreads=nth)
+        hp = CE.helper_prep_aggregate(5, a.bits, a.length, 0, vk, nonces[idx], ps[idx], his[idx], ld["prep_shares"],
+                                      nthreads=nth)
+        fn = CE.leader_finish_aggregate(5, a.bits, a.length, 0, nonces[idx], lis[idx], ld["seeds"], ld["verdicts"],
+                                        hp["prep_msgs"], hp["verdicts"], nthreads=nth)
+        dt_ = time.perf_counter() - t
+        assert np.array_equal(hp["verdicts"], want["verdicts"][idx]) and np.array_equal(fn["verdicts"] == 0, fin[idx])
+        return m / dt_, dt_
+
+    r1, d1 = cpu_ping_pong(1, min(K, 8))
+    mN = max(cpu["threads"], int(a.cpu_seconds * r1 * cpu["threads"] * 0.8))
+    rN, dN = cpu_ping_pong(cpu["threads"], mN)
+    m = min(K, 2)
     t = time.perf_counter()
     for i in range(m):
         orc.prep_init(vk, 0, nonces[i].tobytes(), ps[i].tobytes(), lis[i].tobytes())
     th = time.perf_counter()
     orc.helper_prep_batch(vk, nonces[:m], ps[:m], his[:m], lps[:m], nthreads=1)
     per_l, per_h = (th - t) / m, (time.perf_counter() - th) / m
-    cpu_rate_1t = 1.0 / (per_l + per_h)
 
     def per_launch(kt, stage):
         return round(kt[stage]["ms"] / max(1, kt[stage]["launches"]), 3)
@@ -152,9 +176,13 @@ def main():
         "kernels": {"helper": {s: per_launch(kh, s) for s in ("xof", "flp", "accumulate", "slow")},
                     "leader": {s: per_launch(kl, s) for s in ("xof", "flp", "accumulate")}},
         "verified": bool(verified),
-        "cpu_baseline": {"value": round(cpu_rate_1t, 2), "unit": "reports/s", "cores": 1, "kind": "port",
-                         "sample": f"{m} reports: C oracle leader prep_init + helper prep, per core "
-                                   f"({per_l * 1e3:.0f} + {per_h * 1e3:.0f} ms per report)"},
+        "cpu_baseline": {"value": round(rN, 2), "unit": "reports/s", "cores": cpu["threads"], "kind": "port",
+                         "engine": "cpu_baseline/jc_cpu_engine.cpp (leader init + helper prep/aggregate + leader "
+                                   "finish/aggregate, both roles)", "value_1_thread": round(r1, 2), **cpu,
+                         "oracle_port_reports_per_s_1_core": round(1.0 / (per_l + per_h), 3),
+                         "sample": f"{mN} reports at {cpu['threads']} threads ({dN:.1f} s), {min(K, 8)} at 1 thread "
+                                   f"({d1:.1f} s); C oracle {m} reports ({per_l * 1e3:.0f} + {per_h * 1e3:.0f} ms "
+                                   "per report)"},
         "data": f"synthetic: {K} distinct C-oracle client reports (1 in 6 with a false norm claim) tiled to {R}",
     }), flush=True)
 
