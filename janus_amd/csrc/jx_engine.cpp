@@ -73,6 +73,7 @@ struct jx_engine {
   hipStream_t stream = nullptr;
   std::mutex mu;  // held by every entry point for the duration of the call
   uint64_t cap = 0;  // reports (multiple of 64)
+  uint64_t meas_cap = 0;  // reports of measurement-share staging (allocated only when needed, see leader_inplace)
   uint64_t default_chunk = 0;
   uint64_t round_reports = 0;  // reports that fill every K1 wave slot once (0: unknown)
   // inputs (engine-owned copies for host entry points)
@@ -125,6 +126,7 @@ struct jx_engine {
   uint64_t launches[NST] = {0, 0, 0, 0};
   uint32_t force_slow = 0;
   uint32_t k1_split = 0;  // helper K1: 0 automatic, 3 lane-split, 5 fused (JX_K1_SPLIT, debug option 3)
+  uint32_t leader_staged = 0;  // debug option 6: the leader stages its measurement share (no in-place reads)
   std::string err;
 };
 
@@ -442,6 +444,7 @@ static void free_staging(jx_engine* e) {
   e->d_mask = nullptr;
   e->d_seg = nullptr;
   e->cap = 0;
+  e->meas_cap = 0;
   for (uint8_t** p : {&e->d_lis, &e->d_lps_out, &e->d_in_msgs}) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
@@ -457,9 +460,14 @@ static uint64_t part_bytes(const Cfg& c) {
 }
 // the output shares alias the measurement-share staging (Histogram: output = measurement share)
 static bool outs_alias_meas(const Cfg& c) { return c.out_is_meas && c.algo != ALGO_COUNT; }
+// The leader's FLP kernels read its explicit measurement share in place (Bufs::meas_rs) instead of a
+// staged copy: every TurboSHAKE instance whose output is not the measurement share itself.
+static bool leader_inplace(const Cfg& c) {
+  return c.algo == ALGO_SUM || c.algo == ALGO_SUMVEC || c.algo == ALGO_FIXEDPOINT_L2;
+}
 
-static uint64_t per_report_bytes(const Cfg& c) {
-  uint64_t b = (uint64_t)stage_eb(c) * (c.meas_len + (uint64_t)c.np * c.proof_len + coef_elems(c));
+static uint64_t per_report_bytes(const Cfg& c, bool with_meas = true) {
+  uint64_t b = (uint64_t)stage_eb(c) * ((with_meas ? c.meas_len : 0) + (uint64_t)c.np * c.proof_len + coef_elems(c));
   b += 16ull * (c.out_is_meas ? 0 : c.out_len);
   b += 16 + c.ps_bytes + c.his_bytes + c.lps_bytes + 4 + 1 + c.seed + 1 + 4 + 1;
   b += part_bytes(c);  // FLP partial sums
@@ -474,8 +482,16 @@ static uint32_t acc_nchunks(const jx_engine* e) {
   return want < 16u ? 16u : (want > 4096u ? 4096u : want);
 }
 
-static int32_t ensure_capacity(jx_engine* e, uint64_t n) {
-  if (n <= e->cap) return JX_OK;
+static int32_t ensure_capacity(jx_engine* e, uint64_t n, bool need_meas = true) {
+  if (n <= e->cap) {
+    if (!need_meas || e->meas_cap >= e->cap) return JX_OK;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->d_meas) (void)hipFree(e->d_meas);
+    e->d_meas = nullptr;
+    HIPCHK(e, hipMalloc((void**)&e->d_meas, e->cap * e->cfg.meas_len * stage_eb(e->cfg)));
+    e->meas_cap = e->cap;
+    return JX_OK;
+  }
   HIPCHK(e, hipStreamSynchronize(e->stream));  // queued work may still read the old staging
   free_staging(e);
   const Cfg& c = e->cfg;
@@ -486,7 +502,10 @@ static int32_t ensure_capacity(jx_engine* e, uint64_t n) {
   HIPCHK(e, A((void**)&e->d_his, cap * c.his_bytes));
   HIPCHK(e, A((void**)&e->d_lps, cap * c.lps_bytes));
   const uint64_t eb = stage_eb(c);
-  HIPCHK(e, A((void**)&e->d_meas, cap * c.meas_len * eb));
+  if (need_meas) {
+    HIPCHK(e, A((void**)&e->d_meas, cap * c.meas_len * eb));
+    e->meas_cap = cap;
+  }
   HIPCHK(e, A((void**)&e->d_proof, cap * c.np * c.proof_len * eb));
   if (!outs_alias_meas(c)) HIPCHK(e, A((void**)&e->d_outs, cap * c.out_len * 16));
   HIPCHK(e, A((void**)&e->d_coef, cap * coef_elems(c) * eb));
@@ -630,6 +649,8 @@ static int32_t drain_timing(jx_engine* e) {
   return JX_OK;
 }
 
+static bool use_inplace(const jx_engine* e) { return leader_inplace(e->cfg) && !e->leader_staged; }
+
 // ---------------------------------------------------------------------------- core sequencing
 
 // Prepare n <= cap reports whose inputs are at the given device pointers; the output shares go to
@@ -650,6 +671,10 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
   b.lps_out = lps_out;
   b.leader = leader ? 1u : 0u;
   b.meas = outs_alias_meas(c) ? outs : e->d_meas;
+  if (leader && use_inplace(e)) {
+    b.meas_src = lis;
+    b.meas_rs = c.lis_bytes;
+  }
   b.proof = e->d_proof;
   b.outs = outs;
   b.coef = e->d_coef;
@@ -664,7 +689,7 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
   // the per-report sponge latency, not by issue: the lane-split kernel runs it in twice the waves
   // (FixedPointBoundedL2VecSum 16 x 10000, 24,576 reports: 153 -> 92 ms on MI355X).
   const bool wide = c.bits > 32 && (c.algo == ALGO_SUM || c.algo == ALGO_SUMVEC);
-  if (e->k1_split == 0 && !leader && !wide && e->round_reports && 2 * n < e->round_reports) b.k1_split = 3;
+  if (e->k1_split == 0 && !leader && !wide && e->round_reports && 2 * n <= e->round_reports) b.k1_split = 3;
   hipEvent_t ev = nullptr;
   if (c.algo == ALGO_COUNT) {
     HIPCHK(e, stage_begin(e, &ev));
@@ -699,7 +724,7 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
 }
 
 static int32_t ensure_leader_capacity(jx_engine* e, uint64_t n) {
-  int32_t rc = ensure_capacity(e, n);
+  int32_t rc = ensure_capacity(e, n, !use_inplace(e));
   if (rc) return rc;
   if (n <= e->leader_cap && e->d_lis) return JX_OK;
   HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -1208,7 +1233,7 @@ int32_t jx_leader_prep_init_device(jx_engine* e, uint64_t n, const void* d_nonce
   if (rc) return rc;
   if (n) {
     auto run = [&]() -> int32_t {
-      int32_t r = ensure_capacity(e, n);
+      int32_t r = ensure_capacity(e, n, !use_inplace(e));
       if (r) return r;
       HIPCHK(e, hipMemcpyAsync(B->nonces, d_nonces, n * 16, hipMemcpyDeviceToDevice, e->stream));
       r = prep_core(e, n, B->nonces, (const uint8_t*)d_public_shares, nullptr, nullptr, B->verdicts, B->msgs, B->outs,
@@ -1303,7 +1328,7 @@ int32_t jx_accumulate(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t
   HIPCHK(e, hipSetDevice(e->device));
   auto run = [&]() -> int32_t {
     if (n == 0) return JX_OK;
-    int32_t r = ensure_capacity(e, n);  // mask / index scratch and the accumulate partials
+    int32_t r = ensure_capacity(e, n, false);  // mask / index scratch and the accumulate partials
     if (r) return r;
     const uint8_t* dm = nullptr;
     if (accept_mask) {
@@ -1342,7 +1367,7 @@ int32_t jx_accumulate_device(jx_engine* e, uint64_t batch_id, uint64_t n, const 
   if (rc) return rc;
   HIPCHK(e, hipSetDevice(e->device));
   if (n) {
-    rc = ensure_capacity(e, n);
+    rc = ensure_capacity(e, n, false);  // mask / index scratch and the accumulate partials
     if (rc) return rc;
     std::vector<Segment> targets;
     rc = segment_targets(e, segment_ids, nsegments, targets);
@@ -1377,7 +1402,7 @@ int32_t jx_batch_aggregate_records(jx_engine* e, uint64_t batch_id, uint64_t n, 
   HIPCHK(e, hipSetDevice(e->device));
   const uint64_t rb = record_bytes(e->cfg);
   if (n) {
-    rc = ensure_capacity(e, n);
+    rc = ensure_capacity(e, n, false);  // mask / index scratch and the accumulate partials
     if (rc) return rc;
   }
   const uint8_t* dm = nullptr;
@@ -1408,7 +1433,7 @@ int32_t jx_batch_aggregate_records_device(jx_engine* e, uint64_t batch_id, uint6
   if (rc) return rc;
   HIPCHK(e, hipSetDevice(e->device));
   if (n) {
-    rc = ensure_capacity(e, n);
+    rc = ensure_capacity(e, n, false);  // mask / index scratch and the accumulate partials
     if (rc) return rc;
   }
   return batch_records(e, B, (const uint8_t*)d_accept_mask, (const uint32_t*)d_segment_index, nsegments,
@@ -1650,6 +1675,11 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
     if (value != 0 && value != 3 && value != 5) return JX_E_INVALID;
     // 0: automatic (fused; lane-split below one fused wave per SIMD), 3: lane-split, 5: fused
     e->k1_split = (uint32_t)value;
+    return JX_OK;
+  }
+  if (option == 6) {  // leader measurement share: 0 read in place (default), 1 staged by K1
+    if (value != 0 && value != 1) return JX_E_INVALID;
+    e->leader_staged = (uint32_t)value;
     return JX_OK;
   }
   if (option == 2) {  // accumulate chunking (tests)

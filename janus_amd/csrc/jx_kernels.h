@@ -95,6 +95,11 @@ struct Bufs {
   uint8_t* lps_out;     // leader role: outbound prep shares (n x lps_bytes)
   uint32_t leader;      // 1: run prepare_init for agg_id 0 (leader_initialized)
   uint4* meas;
+  // leader, read in place: the FLP kernels read measurement element e of report r at
+  // meas_src + r * meas_rs + 16 e (the explicit leader input share) instead of the interleaved
+  // staging, which K1 then does not write (meas_rs == 0: the staging)
+  const uint8_t* meas_src;
+  uint64_t meas_rs;
   uint4* proof;
   uint4* outs;
   uint4* coef;

@@ -46,6 +46,20 @@ __device__ __forceinline__ f128 ld_il(const uint4* base, uint64_t blk, uint32_t 
 __device__ __forceinline__ void st_il(uint4* base, uint64_t blk, uint32_t len, uint32_t e, uint32_t lane, f128 v) {
   base[il_idx(blk, len, e, lane)] = f_to_u4(v);
 }
+// The measurement share as the FLP kernels read it: the interleaved staging (element e of the lane's
+// report at p[e * IL]) or, for the leader, its explicit input share in place (p[e], report-major).
+struct MeasView {
+  const uint4* p;
+  uint32_t es;  // element stride in uint4
+  __device__ __forceinline__ const uint4& operator[](uint64_t e) const { return p[e * es]; }
+};
+__device__ __forceinline__ MeasView meas_view(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t lane) {
+  if (b.meas_rs) {
+    const uint64_t r0 = blk * 64 + lane, r = r0 < b.n ? r0 : b.n - 1;
+    return MeasView{reinterpret_cast<const uint4*>(b.meas_src + r * b.meas_rs), 1u};
+  }
+  return MeasView{b.meas + il_idx(blk, c.meas_len, 0, lane), (uint32_t)IL};
+}
 __device__ __forceinline__ void load16(const uint8_t* p, uint32_t w[4]) {
   uint4 v = *reinterpret_cast<const uint4*>(p);
   w[0] = v.x;
@@ -290,14 +304,14 @@ __device__ __forceinline__ f128 shl32_mod(f128 h) {
 // one measurement element at static stream position e (fast path: no rejections)
 // WIDE (bits in (32, 64], Sum / SumVec): the word columns of bits 0..31 are folded into `lo` at
 // bit 32 and restart for the bits 32.. (weights 2^(j-32) < 2^32); out = lo + 2^32 * high.
-template <bool WIDE>
+template <bool WIDE, bool STORE = true>
 __device__ __forceinline__ void emit_meas(const Cfg& c, uint4* mp, uint4* op, uint32_t e, uint4 v, uint32_t& gmax,
                                           TruncW& tr, f128& lo) {
   // e is uniform. Straight-line except for the store guard and the once-per-output-element finish:
   // elements past the share (last block) or not truncated (Histogram; FixedPoint's trailing norm
   // bits) add with weight 0 instead of branching around the column sums.
   const bool in = e < c.meas_len;
-  if (in) mp[(uint64_t)e * IL] = v;
+  if (STORE && in) mp[(uint64_t)e * IL] = v;
   gmax = max(gmax, in ? ge_screen(v) : 0u);
   const bool tin = !c.out_is_meas && e < c.trunc_len;
   const uint32_t sh = opaque_u32(tin ? 1u << (WIDE ? (tr.j & 31u) : tr.j) : 0u);
@@ -992,7 +1006,10 @@ __global__ __launch_bounds__(64 * K1_WAVES, WIDE ? 2 : 4) void xof_lanes_kernel(
 // while J permutes block m, so the loads land under the permutation. Elements >= p fail the report
 // (decode). One buffer, one sponge: no spills even when a launch holds a third of a wave per SIMD
 // (FixedPointBoundedL2VecSum at length 10000), where every scratch access would be exposed.
-template <bool WIDE>
+// INPLACE: the FLP kernels read the explicit share where it lies (Bufs::meas_rs), so K1 stages nothing
+// of it (2.56 MB per FixedPoint 16 x 10000 report: no store traffic, no waits on the stores, and the
+// staging memory goes to more reports per launch).
+template <bool WIDE, bool INPLACE>
 __global__ __launch_bounds__(64 * K1_WAVES) void xof_leader_kernel(Cfg c, Bufs b) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t blk = (uint64_t)blockIdx.x * K1_WAVES + (threadIdx.x >> 6);
@@ -1041,7 +1058,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_leader_kernel(Cfg c, Bufs b
   uint4* const op = b.outs + il_idx(blk, c.out_len, 0, lane);
   auto emit = [&](uint32_t e, uint4 v) __attribute__((always_inline)) {
     if (e < c.meas_len) bad |= ge_exact(v);
-    emit_meas<WIDE>(c, mp, op, e, v, unused_screen, tr, trunc_lo);
+    emit_meas<WIDE, !INPLACE>(c, mp, op, e, v, unused_screen, tr, trunc_lo);
   };
   auto emit_block = [&](uint32_t m) __attribute__((always_inline)) {
     const uint32_t e0 = 21 * (m >> 1);
@@ -1343,8 +1360,9 @@ __global__ __launch_bounds__(256) void flp_sum_kernel(Cfg c, Bufs b) {
   f128 tR = ld_il(b.coef, blk, NC, COEF_T, lane), rR = ld_il(b.coef, blk, NC, COEF_R, lane);
   acc192 ao;
   acc_zero(ao);
+  const MeasView mv = meas_view(c, b, blk, lane);
   for (uint32_t k = 1; k <= C; k++) {
-    f128 x = ld_il(b.meas, blk, c.meas_len, k - 1, lane);
+    f128 x = u4_to_f(mv[k - 1]);
     uint64_t lo, hi;
     uint32_t top;
     mont128_lazy(x, ld_il(b.coef, blk, NC, COEF_K + k - 1, lane), lo, hi, top);
@@ -1436,7 +1454,7 @@ __device__ __forceinline__ void psum_part_finish(const Cfg& c, const Bufs& b, ui
   const uint32_t NC = c.ncoef, C = c.calls, chunk = c.chunk, M = c.meas_len, A = 2 * chunk;
   const uint32_t j0 = g * PPW;
   const uint4* coefb = b.coef + il_idx(blk, NC, 0, lane);
-  const uint4* measb = b.meas + il_idx(blk, M, 0, lane);
+  const MeasView measb = meas_view(c, b, blk, lane);
 #pragma unroll 1
   for (uint32_t k = kf + 1; k <= C; k++) {  // the ragged last call(s), or every call of a padded group
     const limbs26 ck = to_limbs26(u4_to_f(coefb[(COEF_K + 2 * (k - 1)) * IL]));
@@ -1445,7 +1463,7 @@ __device__ __forceinline__ void psum_part_finish(const Cfg& c, const Bufs& b, ui
 #pragma unroll
     for (int i = 0; i < PPW; i++) {
       if (j0 + i < chunk && nb + i < M) {
-        const f128 x = u4_to_f(measb[(uint64_t)(nb + i) * IL]);
+        const f128 x = u4_to_f(measb[nb + i]);
         const limbs26 xl = to_limbs26(x);
         wacc_mac(ae[i], xl, dk);
         wacc_mac(ao[i], xl, ck);
@@ -1552,7 +1570,7 @@ __global__ __launch_bounds__(64, 4) void flp_psum_part_kernel(Cfg c, Bufs b) {
   }
   acc_zero(sx);
   const uint4* coefb = b.coef + il_idx(blk, NC, 0, lane);
-  const uint4* measb = b.meas + il_idx(blk, M, 0, lane);
+  const MeasView measb = meas_view(c, b, blk, lane);
   // calls whose PPW slots of this group are all real measurement elements run branch-free;
   // the rest (the ragged last chunk, slots beyond chunk) take the guarded tail loop
   uint32_t kf = 0;
@@ -1568,7 +1586,7 @@ __global__ __launch_bounds__(64, 4) void flp_psum_part_kernel(Cfg c, Bufs b) {
         cr[u] = coefb[(COEF_K + 2 * (k - 1)) * IL];
         dr[u] = coefb[(COEF_K + 2 * (k - 1) + 1) * IL];
 #pragma unroll
-        for (int i = 0; i < PPW; i++) xr[u][i] = measb[(uint64_t)((k - 1) * chunk + j0 + i) * IL];
+        for (int i = 0; i < PPW; i++) xr[u][i] = measb[(uint64_t)((k - 1) * chunk + j0 + i)];
       }
     }
 #pragma unroll 1
@@ -1587,7 +1605,7 @@ __global__ __launch_bounds__(64, 4) void flp_psum_part_kernel(Cfg c, Bufs b) {
             cr[u] = coefb[(COEF_K + 2 * (kn - 1)) * IL];
             dr[u] = coefb[(COEF_K + 2 * (kn - 1) + 1) * IL];
 #pragma unroll
-            for (int i = 0; i < PPW; i++) xr[u][i] = measb[(uint64_t)((kn - 1) * chunk + j0 + i) * IL];
+            for (int i = 0; i < PPW; i++) xr[u][i] = measb[(uint64_t)((kn - 1) * chunk + j0 + i)];
           }
 #pragma unroll
           for (int i = 0; i < PPW; i++) {
@@ -1664,7 +1682,7 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
   const uint32_t j0 = g * PPW;
   const bool full = g < NG && j0 + PPW <= chunk;  // this wave's PPW slots are all real
   const uint4* coefb = b.coef + il_idx(blk, c.ncoef, 0, lane);
-  const uint4* measb = b.meas + il_idx(blk, M, 0, lane);
+  const MeasView measb = meas_view(c, b, blk, lane);
   // calls whose every slot is a measurement element; a wave whose group is padded or absent runs the
   // loop for the barriers (and, waves 0/1, the coefficient loads) but computes in the tail only
   const uint32_t kfw = C < M / chunk ? C : M / chunk;
@@ -1686,7 +1704,7 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
 #pragma unroll
       for (int i = 0; i < PPW; i++) {
         const uint64_t e = (uint64_t)((k - 1) * chunk + j0 + i);
-        glds16(measb + e * IL, &ring[sl][2 + wave * PPW + i][0]);
+        glds16(&measb[e], &ring[sl][2 + wave * PPW + i][0]);
       }
     }
   };
@@ -1896,7 +1914,8 @@ __global__ __launch_bounds__(256) void flp_fp_final_kernel(Cfg c, Bufs b) {
   acc192 cn;
   acc_zero(cn);
   const uint32_t nb0 = c.trunc_len;
-  for (uint32_t i = 0; i < c.norm_bits; i++) trunc_add(cn, ld_il(b.meas, blk, c.meas_len, nb0 + i, lane), i);
+  const MeasView mv = meas_view(c, b, blk, lane);
+  for (uint32_t i = 0; i < c.norm_bits; i++) trunc_add(cn, u4_to_f(mv[nb0 + i]), i);
   const f128 claimed = acc_reduce(cn);
   const f128 r2R = ld_il(b.coef, blk, c.ncoef, COEF_R2, lane);
   const f128 vh = add128(mont128(V0, r2R), mont128(sub128(V1, claimed), mont128(r2R, r2R)));
@@ -2418,10 +2437,14 @@ hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
   uint32_t nb = nblk_of(b.n);
   const dim3 grid((nb + K1_WAVES - 1) / K1_WAVES), block(64 * K1_WAVES);
   const bool wide = c.bits > 32 && (c.algo == ALGO_SUM || c.algo == ALGO_SUMVEC);
-  if (b.leader && wide)
-    hipLaunchKernelGGL((xof_leader_kernel<true>), grid, block, 0, s, c, b);
+  if (b.leader && wide && b.meas_rs)
+    hipLaunchKernelGGL((xof_leader_kernel<true, true>), grid, block, 0, s, c, b);
+  else if (b.leader && wide)
+    hipLaunchKernelGGL((xof_leader_kernel<true, false>), grid, block, 0, s, c, b);
+  else if (b.leader && b.meas_rs)
+    hipLaunchKernelGGL((xof_leader_kernel<false, true>), grid, block, 0, s, c, b);
   else if (b.leader)
-    hipLaunchKernelGGL((xof_leader_kernel<false>), grid, block, 0, s, c, b);
+    hipLaunchKernelGGL((xof_leader_kernel<false, false>), grid, block, 0, s, c, b);
   else if (b.k1_split == 3) {  // lane-split: 32 reports per wave
     const dim3 g2((2 * nb + K1_WAVES - 1) / K1_WAVES);
     if (wide)

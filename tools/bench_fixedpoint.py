@@ -2,21 +2,25 @@
 """BASELINE configs[4]: Prio3FixedPointBoundedL2VecSum 16-bit length=10000, leader+helper ping-pong
 prep with joint randomness, on one MI355X.
 
-One step = one aggregation job of R reports taken through both roles with every input resident in
-HBM (aggregation_job_driver.rs:259-436 + aggregator.rs:1712-2161, minus HTTP and the datastore):
+One ping-pong step = one aggregation job of R reports taken through both roles with every input
+resident in HBM (aggregation_job_driver.rs:259-436 + aggregator.rs:1712-2161, minus HTTP and the
+datastore):
   leader  jx_leader_prep_init_device   (leader_initialized: prepare_init agg_id 0, explicit shares)
   helper  jx_helper_prep_aggregate_device (helper_initialized + evaluate + accumulate)
   leader  jx_leader_prep_finish_device (leader_continued on the helper's Finish; helper rejects fail)
   leader  jx_accumulate_device
-The two engines (one per role) share the GPU here; in a deployment they are two aggregators. The
-helper-only rate (the north-star unit) and per-role kernel times are reported too. Inputs: a pool
-of K distinct client reports (C-oracle shard; 1 in 6 claims a false norm and must be rejected)
-tiled on the device. Verified: both aggregates add up to multiplicity x the sum of the accepted
-entries' encodings, and every verdict matches the oracle. The C oracle (leader prep_init + helper
-prep per report) and the C++ CPU engine's two roles (the baseline proper) are timed on the host
-beside it (kind "port").
+The two engines (one per role) share the GPU here; in a deployment they are two aggregators on two
+GPUs. So the tool also measures each role ALONE at its own full-device launch size (--role-reports):
+  helper  prep + aggregate of R_h reports, one engine owning the GPU (its staging, 2.8 MB/report,
+          sized to the launch instead of the shared 1/3-of-HBM budget);
+  leader  prep_init + finish + aggregate of R_l reports (the leader reads its explicit 2.6 MB input
+          share in place: HBM holds R_l input shares and ~0.2 MB/report of staging).
+Inputs: a pool of K distinct client reports (C-oracle shard; 1 in 6 claims a false norm and must be
+rejected) tiled on the device. Verified: aggregates add up to multiplicity x the sum of the accepted
+entries' encodings, every verdict matches the oracle. The C++ CPU engine's two roles (the baseline
+proper, kind "port") and the literal C oracle are timed on the host beside it.
 
-    python tools/bench_fixedpoint.py [--bits 16 --length 10000 --reports 8192 --pool 48]
+    python tools/bench_fixedpoint.py [--bits 16 --length 10000 --reports 32768 --role-reports 65536]
 """
 from __future__ import annotations
 
@@ -33,16 +37,25 @@ sys.path.insert(0, ROOT)
 P128 = 2**128 - 28 * 2**64 + 1
 
 
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bits", type=int, default=16)
     ap.add_argument("--length", type=int, default=10000)
-    ap.add_argument("--reports", type=int, default=8192)
+    ap.add_argument("--reports", type=int, default=32768, help="reports per ping-pong step (both roles on the GPU)")
+    ap.add_argument("--role-reports", type=int, default=65536, help="reports per single-role step")
     ap.add_argument("--pool", type=int, default=48)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--skip", default="", help="comma list of legs to skip: pingpong,pipelined,helper,leader,cpu")
+    ap.add_argument("--leader-staged", action="store_true",
+                    help="the leader stages its measurement share (debug option 6) instead of reading it in place")
     a = ap.parse_args()
+    skip = set(filter(None, a.skip.split(",")))
 
     import torch
 
@@ -55,7 +68,7 @@ def main():
     vdaf = Prio3.fixedpoint_boundedl2_vec_sum(a.bits, a.length)
     orc = O.Prio3Oracle(O.FIXEDPOINT_L2, a.bits, a.length, 0)
     vk = bytes(range(16))
-    K, R = a.pool, a.reports
+    K = a.pool
     rng = np.random.default_rng(0x5EED)
     meas = fixedpoint_measurements(a.bits, a.length, rng, K)
     nonces = rng.integers(0, 256, size=(K, 16), dtype=np.uint8)
@@ -66,125 +79,285 @@ def main():
     lps = np.stack([np.frombuffer(orc.prep_init(vk, 0, nonces[i].tobytes(), ps[i].tobytes(), lis[i].tobytes())[1],
                                   np.uint8) for i in range(K)])
     want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=threads)
-    print(f"pool of {K} generated in {time.perf_counter() - t0:.1f}s; oracle verdicts {want['verdicts'].tolist()}",
-          file=sys.stderr)
-
-    reps = -(-R // K)
-    dev = torch.device("cuda", 0)
-
-    def tile(x):
-        return torch.from_numpy(np.ascontiguousarray(x)).to(dev).repeat(reps, 1)[:R].contiguous()
-
-    d_n, d_ps, d_lis, d_his = tile(nonces), tile(ps), tile(lis), tile(his)
-    d_lps = torch.empty((R, vdaf.prep_share_len), dtype=torch.uint8, device=dev)
-    d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
-    d_hv = torch.empty(R, dtype=torch.uint8, device=dev)
-    d_lv = torch.empty(R, dtype=torch.uint8, device=dev)
-    leader, helper = HelperEngine(vdaf, vk), HelperEngine(vdaf, vk)
-    role_s = {"leader_init": 0.0, "helper": 0.0, "leader_finish_acc": 0.0}
-
-    def step(timed):
-        t = time.perf_counter()
-        bid = leader.leader_init_device(R, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(), d_lps.data_ptr())
-        leader.sync()
-        t1 = time.perf_counter()
-        helper.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(), d_lps.data_ptr(), R, 0,
-                                         d_msgs.data_ptr(), d_hv.data_ptr())
-        helper.sync()
-        t2 = time.perf_counter()
-        leader.leader_finish_device(bid, R, d_msgs.data_ptr(), d_hv.data_ptr(), d_lv.data_ptr())
-        leader.accumulate_device(bid, R)
-        leader.sync()
-        t3 = time.perf_counter()
-        if timed:
-            role_s["leader_init"] += t1 - t
-            role_s["helper"] += t2 - t1
-            role_s["leader_finish_acc"] += t3 - t2
-
-    for _ in range(a.warmup):
-        step(False)
-    leader.timing(True)
-    helper.timing(True)
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(a.steps):
-        step(True)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t
-    kl, kh = leader.timing_read(), helper.timing_read()
-    agg_l, cnt_l, cs_l = leader.aggregate_share(0)
-    agg_h, cnt_h, cs_h = helper.aggregate_share(0)
-    leader.close()
-    helper.close()
-
-    total = a.steps + a.warmup
-    mult = np.bincount(np.arange(R) % K, minlength=K)
     fin = want["verdicts"] == 0
     enc = meas.astype(object) ^ (1 << (a.bits - 1))
-    exp = [int((enc[fin, j] * mult[fin]).sum()) * total % P128 for j in range(a.length)]
-    got = [(int.from_bytes(agg_l[16 * j:16 * j + 16], "little") + int.from_bytes(agg_h[16 * j:16 * j + 16], "little"))
-           % P128 for j in range(a.length)]
-    exp_count = total * int(mult[fin].sum())
-    verified = got == exp and cnt_l == cnt_h == exp_count and cs_l == cs_h and \
-        np.array_equal(d_hv.cpu().numpy(), np.tile(want["verdicts"], reps)[:R]) and \
-        np.array_equal(d_lv.cpu().numpy() == 0, np.tile(fin, reps)[:R])
+    log(f"pool of {K} generated in {time.perf_counter() - t0:.1f}s; oracle verdicts {want['verdicts'].tolist()}")
+    dev = torch.device("cuda", 0)
+    total = a.steps + a.warmup
 
-    # CPU baseline: the C++ CPU engine's leader prep_init -> helper prep + aggregate -> leader finish +
-    # aggregate (cpu_baseline/jc_cpu_engine.cpp, byte-checked against the oracle) at 1 thread and at the
-    # host's thread budget; the literal C oracle (leader prep_init + helper prep) per core beside it
-    from bench import cpu_threads
-    from cpu_baseline import cpu_engine as CE
+    def tile(x, R):
+        x = np.ascontiguousarray(x)
+        x2 = x.reshape(K, -1)
+        reps = -(-R // K)
+        return torch.from_numpy(x2).to(dev).repeat(reps, 1)[:R].contiguous()
 
-    cpu = cpu_threads()
+    def tiled(x, R):
+        return np.tile(x, -(-R // K))[:R]
 
-    def cpu_ping_pong(nth, m):
-        idx = np.arange(m) % K
-        t = time.perf_counter()
-        ld = CE.leader_prep_init(5, a.bits, a.length, 0, vk, nonces[idx], ps[idx], lis[idx], vdaf.prep_share_len,
-                                 nthreads=nth)
-        hp = CE.helper_prep_aggregate(5, a.bits, a.length, 0, vk, nonces[idx], ps[idx], his[idx], ld["prep_shares"],
-                                      nthreads=nth)
-        fn = CE.leader_finish_aggregate(5, a.bits, a.length, 0, nonces[idx], lis[idx], ld["seeds"], ld["verdicts"],
-                                        hp["prep_msgs"], hp["verdicts"], nthreads=nth)
-        dt_ = time.perf_counter() - t
-        assert np.array_equal(hp["verdicts"], want["verdicts"][idx]) and np.array_equal(fn["verdicts"] == 0, fin[idx])
-        return m / dt_, dt_
+    def expected(R):
+        mult = np.bincount(np.arange(R) % K, minlength=K)
+        return ([int((enc[fin, j] * mult[fin]).sum()) * total % P128 for j in range(a.length)],
+                total * int(mult[fin].sum()))
 
-    r1, d1 = cpu_ping_pong(1, min(K, 8))
-    mN = max(cpu["threads"], int(a.cpu_seconds * r1 * cpu["threads"] * 0.8))
-    rN, dN = cpu_ping_pong(cpu["threads"], mN)
-    m = min(K, 2)
-    t = time.perf_counter()
-    for i in range(m):
-        orc.prep_init(vk, 0, nonces[i].tobytes(), ps[i].tobytes(), lis[i].tobytes())
-    th = time.perf_counter()
-    orc.helper_prep_batch(vk, nonces[:m], ps[:m], his[:m], lps[:m], nthreads=1)
-    per_l, per_h = (th - t) / m, (time.perf_counter() - th) / m
+    def add_shares(*aggs):
+        return [sum(int.from_bytes(g[16 * j:16 * j + 16], "little") for g in aggs) % P128 for j in range(a.length)]
 
     def per_launch(kt, stage):
         return round(kt[stage]["ms"] / max(1, kt[stage]["launches"]), 3)
 
-    print(json.dumps({
+    def timed_steps(step, engines):
+        for _ in range(a.warmup):
+            step(False)
+        for e in engines:
+            e.timing(True)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(a.steps):
+            step(True)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t
+
+    out = {
+        "leader_measurement": "staged by K1" if a.leader_staged else "read in place by the FLP kernels",
         "metric": "leader+helper ping-pong reports/sec (prep_init+prep_next+aggregate, both roles), "
                   f"Prio3FixedPointBoundedL2VecSum {a.bits}-bit length={a.length} (configs[4])",
-        "value": round(R * a.steps / dt, 1), "unit": "reports/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
-        "helper_reports_per_s": round(R * a.steps / role_s["helper"], 1),
-        "role_ms_per_step": {k: round(v / a.steps * 1e3, 3) for k, v in role_s.items()},
-        "config": {"workload": f"FixedPointBoundedL2VecSum bitsize={a.bits} length={a.length}", "reports": R,
-                   "pool": K, "launches_per_step_helper": kh["xof"]["launches"] // a.steps},
-        "kernels": {"helper": {s: per_launch(kh, s) for s in ("xof", "flp", "accumulate", "slow")},
-                    "leader": {s: per_launch(kl, s) for s in ("xof", "flp", "accumulate")}},
-        "verified": bool(verified),
-        "cpu_baseline": {"value": round(rN, 2), "unit": "reports/s", "cores": cpu["threads"], "kind": "port",
-                         "engine": "cpu_baseline/jc_cpu_engine.cpp (leader init + helper prep/aggregate + leader "
-                                   "finish/aggregate, both roles)", "value_1_thread": round(r1, 2), **cpu,
-                         "oracle_port_reports_per_s_1_core": round(1.0 / (per_l + per_h), 3),
-                         "sample": f"{mN} reports at {cpu['threads']} threads ({dN:.1f} s), {min(K, 8)} at 1 thread "
-                                   f"({d1:.1f} s); C oracle {m} reports ({per_l * 1e3:.0f} + {per_h * 1e3:.0f} ms "
-                                   "per report)"},
-        "data": f"synthetic: {K} distinct C-oracle client reports (1 in 6 with a false norm claim) tiled to {R}",
-    }), flush=True)
+        "unit": "reports/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "higher_is_better": True,
+        "data": f"synthetic: {K} distinct C-oracle client reports (1 in 6 with a false norm claim) tiled on device",
+    }
+    verified = True
+
+    # ---------------------------------------------------------------- ping-pong, both roles on one GPU
+    if "pingpong" not in skip:
+        R = a.reports
+        d_n, d_ps, d_lis, d_his = tile(nonces, R), tile(ps, R), tile(lis, R), tile(his, R)
+        d_lps = torch.empty((R, vdaf.prep_share_len), dtype=torch.uint8, device=dev)
+        d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
+        d_hv = torch.empty(R, dtype=torch.uint8, device=dev)
+        d_lv = torch.empty(R, dtype=torch.uint8, device=dev)
+        leader, helper = HelperEngine(vdaf, vk), HelperEngine(vdaf, vk)
+        if a.leader_staged:
+            leader.debug(6, 1)
+        role_s = {"leader_init": 0.0, "helper": 0.0, "leader_finish_acc": 0.0}
+
+        def step(timed):
+            t = time.perf_counter()
+            bid = leader.leader_init_device(R, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(), d_lps.data_ptr())
+            leader.sync()
+            t1 = time.perf_counter()
+            helper.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(), d_lps.data_ptr(), R,
+                                             0, d_msgs.data_ptr(), d_hv.data_ptr())
+            helper.sync()
+            t2 = time.perf_counter()
+            leader.leader_finish_device(bid, R, d_msgs.data_ptr(), d_hv.data_ptr(), d_lv.data_ptr())
+            leader.accumulate_device(bid, R)
+            leader.sync()
+            t3 = time.perf_counter()
+            if timed:
+                role_s["leader_init"] += t1 - t
+                role_s["helper"] += t2 - t1
+                role_s["leader_finish_acc"] += t3 - t2
+
+        dt = timed_steps(step, (leader, helper))
+        kl, kh = leader.timing_read(), helper.timing_read()
+        agg_l, cnt_l, cs_l = leader.aggregate_share(0)
+        agg_h, cnt_h, cs_h = helper.aggregate_share(0)
+        exp, exp_count = expected(R)
+        ok = add_shares(agg_l, agg_h) == exp and cnt_l == cnt_h == exp_count and cs_l == cs_h and \
+            np.array_equal(d_hv.cpu().numpy(), tiled(want["verdicts"], R)) and \
+            np.array_equal(d_lv.cpu().numpy() == 0, tiled(fin, R))
+        verified &= bool(ok)
+        leader.close()
+        helper.close()
+        del d_n, d_ps, d_lis, d_his, d_lps, d_msgs, d_hv, d_lv
+        torch.cuda.empty_cache()
+        out.update({
+            "value": round(R * a.steps / dt, 1), "ms_per_step": round(dt / a.steps * 1e3, 3),
+            "helper_reports_per_s_in_pingpong": round(R * a.steps / role_s["helper"], 1),
+            "role_ms_per_step": {k: round(v / a.steps * 1e3, 3) for k, v in role_s.items()},
+            "config": {"workload": f"FixedPointBoundedL2VecSum bitsize={a.bits} length={a.length}", "reports": R,
+                       "pool": K, "launches_per_step_helper": kh["xof"]["launches"] // a.steps},
+            "kernels": {"helper": {s: per_launch(kh, s) for s in ("xof", "flp", "accumulate", "slow")},
+                        "leader": {s: per_launch(kl, s) for s in ("xof", "flp", "accumulate")}},
+            "pingpong_verified": bool(ok),
+        })
+        log(f"ping-pong: {out['value']} reports/s, verified {ok}")
+
+    # ---------------------------------------------------------------- ping-pong, two jobs in flight
+    # Janus steps several aggregation jobs at once (max_concurrent_job_workers, job_driver.rs:116-138), and
+    # the two aggregators are independent processes: while the helper prepares job i-1 (helper engine,
+    # its own stream), the leader initializes job i (leader engine, its own stream); then the leader
+    # finishes job i-1. Each role alone leaves most SIMDs idle at these launch sizes (one report's sponge
+    # chain is serial), so the two roles' kernels run side by side.
+    if "pipelined" not in skip:
+        R = a.reports
+        d_n, d_ps, d_lis, d_his = tile(nonces, R), tile(ps, R), tile(lis, R), tile(his, R)
+        d_lps = [torch.empty((R, vdaf.prep_share_len), dtype=torch.uint8, device=dev) for _ in range(2)]
+        d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
+        d_hv = torch.empty(R, dtype=torch.uint8, device=dev)
+        d_lv = torch.empty(R, dtype=torch.uint8, device=dev)
+        leader, helper = HelperEngine(vdaf, vk), HelperEngine(vdaf, vk)
+        if a.leader_staged:
+            leader.debug(6, 1)
+        state = {"i": 0, "prev": None, "done": 0}
+
+        def pstep(timed):
+            i = state["i"]
+            bid = leader.leader_init_device(R, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(), d_lps[i % 2].data_ptr())
+            if state["prev"] is not None:
+                helper.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(),
+                                                 d_lps[(i - 1) % 2].data_ptr(), R, 0, d_msgs.data_ptr(), d_hv.data_ptr())
+            helper.sync()
+            if state["prev"] is not None:
+                leader.leader_finish_device(state["prev"], R, d_msgs.data_ptr(), d_hv.data_ptr(), d_lv.data_ptr())
+                leader.accumulate_device(state["prev"], R)
+                state["done"] += 1
+            leader.sync()
+            state["prev"] = bid
+            state["i"] = i + 1
+
+        pstep(False)  # fill the pipeline: job 0's leader init
+        dt = timed_steps(pstep, (leader, helper))
+        # drain: the last job's helper step and leader finish (untimed)
+        helper.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(),
+                                         d_lps[(state["i"] - 1) % 2].data_ptr(), R, 0, d_msgs.data_ptr(), d_hv.data_ptr())
+        helper.sync()
+        leader.leader_finish_device(state["prev"], R, d_msgs.data_ptr(), d_hv.data_ptr(), d_lv.data_ptr())
+        leader.accumulate_device(state["prev"], R)
+        leader.sync()
+        jobs = state["done"] + 1
+        kl, kh = leader.timing_read(), helper.timing_read()
+        agg_l, cnt_l, cs_l = leader.aggregate_share(0)
+        agg_h, cnt_h, cs_h = helper.aggregate_share(0)
+        mult = np.bincount(np.arange(R) % K, minlength=K)
+        exp = [int((enc[fin, j] * mult[fin]).sum()) * jobs % P128 for j in range(a.length)]
+        ok = add_shares(agg_l, agg_h) == exp and cnt_l == cnt_h == jobs * int(mult[fin].sum()) and cs_l == cs_h and \
+            np.array_equal(d_hv.cpu().numpy(), tiled(want["verdicts"], R)) and \
+            np.array_equal(d_lv.cpu().numpy() == 0, tiled(fin, R))
+        verified &= bool(ok)
+        leader.close()
+        helper.close()
+        del d_n, d_ps, d_lis, d_his, d_lps, d_msgs, d_hv, d_lv
+        torch.cuda.empty_cache()
+        out["pipelined"] = {"reports_per_s": round(R * a.steps / dt, 1), "ms_per_step": round(dt / a.steps * 1e3, 3),
+                            "reports_per_job": R, "jobs_in_flight": 2, "verified": bool(ok),
+                            "kernels": {"helper": {s: per_launch(kh, s) for s in ("xof", "flp", "accumulate")},
+                                        "leader": {s: per_launch(kl, s) for s in ("xof", "flp", "accumulate")}}}
+        log(f"pipelined ping-pong: {out['pipelined']}")
+
+    # ---------------------------------------------------------------- each role alone, full-device launch
+    roles = {}
+    R = a.role_reports
+    if "helper" not in skip:
+        d_n, d_ps, d_his, d_lps = tile(nonces, R), tile(ps, R), tile(his, R), tile(lps, R)
+        d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
+        d_hv = torch.empty(R, dtype=torch.uint8, device=dev)
+        free, _ = torch.cuda.mem_get_info()
+        os.environ["JX_STAGING_GB"] = str(max(1, int(free * 0.85) >> 30))  # this engine owns the GPU
+        try:
+            helper = HelperEngine(vdaf, vk)
+        finally:
+            del os.environ["JX_STAGING_GB"]
+
+        def hstep(timed):
+            helper.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(), d_lps.data_ptr(), R,
+                                             0, d_msgs.data_ptr(), d_hv.data_ptr())
+            helper.sync()
+
+        dt = timed_steps(hstep, (helper,))
+        kh = helper.timing_read()
+        _, cnt_h, _ = helper.aggregate_share(0)
+        _, exp_count = expected(R)
+        ok = cnt_h == exp_count and np.array_equal(d_hv.cpu().numpy(), tiled(want["verdicts"], R))
+        verified &= bool(ok)
+        roles["helper"] = {"reports_per_s": round(R * a.steps / dt, 1), "reports": R,
+                           "ms_per_step": round(dt / a.steps * 1e3, 3),
+                           "launches_per_step": kh["xof"]["launches"] // a.steps,
+                           "kernels_ms_per_launch": {s: per_launch(kh, s) for s in ("xof", "flp", "accumulate", "slow")},
+                           "verified": bool(ok)}
+        helper.close()
+        del d_n, d_ps, d_his, d_lps, d_msgs, d_hv
+        torch.cuda.empty_cache()
+        log(f"helper alone: {roles['helper']}")
+    if "leader" not in skip:
+        d_n, d_ps, d_lis = tile(nonces, R), tile(ps, R), tile(lis, R)
+        d_lps = torch.empty((R, vdaf.prep_share_len), dtype=torch.uint8, device=dev)
+        d_msgs = tile(want["prep_msgs"], R)  # the helper's Finish messages (rejected reports: peer verdicts)
+        d_hv = tile(want["verdicts"], R).reshape(R).contiguous()
+        d_lv = torch.empty(R, dtype=torch.uint8, device=dev)
+        leader = HelperEngine(vdaf, vk)
+        if a.leader_staged:
+            leader.debug(6, 1)
+
+        def lstep(timed):
+            bid = leader.leader_init_device(R, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(), d_lps.data_ptr())
+            leader.leader_finish_device(bid, R, d_msgs.data_ptr(), d_hv.data_ptr(), d_lv.data_ptr())
+            leader.accumulate_device(bid, R)
+            leader.sync()
+
+        dt = timed_steps(lstep, (leader,))
+        kl = leader.timing_read()
+        _, cnt_l, _ = leader.aggregate_share(0)
+        _, exp_count = expected(R)
+        ok = cnt_l == exp_count and np.array_equal(d_lv.cpu().numpy() == 0, tiled(fin, R)) and \
+            np.array_equal(d_lps[:K].cpu().numpy(), lps)  # prep shares == the oracle's prepare_init
+        verified &= bool(ok)
+        roles["leader"] = {"reports_per_s": round(R * a.steps / dt, 1), "reports": R,
+                           "ms_per_step": round(dt / a.steps * 1e3, 3),
+                           "kernels_ms_per_launch": {s: per_launch(kl, s) for s in ("xof", "flp", "accumulate")},
+                           "verified": bool(ok)}
+        leader.close()
+        del d_n, d_ps, d_lis, d_lps, d_msgs, d_hv, d_lv
+        torch.cuda.empty_cache()
+        log(f"leader alone: {roles['leader']}")
+    if roles:
+        out["roles_alone"] = roles
+        if len(roles) == 2:
+            h, l_ = roles["helper"]["reports_per_s"], roles["leader"]["reports_per_s"]
+            out["pingpong_from_roles_one_gpu"] = round(1.0 / (1.0 / h + 1.0 / l_), 1)
+            out["pingpong_two_gpus"] = round(min(h, l_), 1)
+    out["verified"] = bool(verified)
+
+    # ---------------------------------------------------------------- CPU baseline
+    if "cpu" not in skip:
+        # the C++ CPU engine's leader prep_init -> helper prep + aggregate -> leader finish + aggregate
+        # (cpu_baseline/jc_cpu_engine.cpp, byte-checked against the oracle) at 1 thread and at the host's
+        # thread budget; the literal C oracle (leader prep_init + helper prep) per core beside it
+        from bench import cpu_threads
+        from cpu_baseline import cpu_engine as CE
+
+        cpu = cpu_threads()
+
+        def cpu_ping_pong(nth, m):
+            idx = np.arange(m) % K
+            t = time.perf_counter()
+            ld = CE.leader_prep_init(5, a.bits, a.length, 0, vk, nonces[idx], ps[idx], lis[idx], vdaf.prep_share_len,
+                                     nthreads=nth)
+            hp = CE.helper_prep_aggregate(5, a.bits, a.length, 0, vk, nonces[idx], ps[idx], his[idx],
+                                          ld["prep_shares"], nthreads=nth)
+            fn = CE.leader_finish_aggregate(5, a.bits, a.length, 0, nonces[idx], lis[idx], ld["seeds"], ld["verdicts"],
+                                            hp["prep_msgs"], hp["verdicts"], nthreads=nth)
+            dt_ = time.perf_counter() - t
+            assert np.array_equal(hp["verdicts"], want["verdicts"][idx]) and np.array_equal(fn["verdicts"] == 0, fin[idx])
+            return m / dt_, dt_
+
+        r1, d1 = cpu_ping_pong(1, min(K, 8))
+        mN = max(cpu["threads"], int(a.cpu_seconds * r1 * cpu["threads"] * 0.8))
+        rN, dN = cpu_ping_pong(cpu["threads"], mN)
+        m = min(K, 2)
+        t = time.perf_counter()
+        for i in range(m):
+            orc.prep_init(vk, 0, nonces[i].tobytes(), ps[i].tobytes(), lis[i].tobytes())
+        th = time.perf_counter()
+        orc.helper_prep_batch(vk, nonces[:m], ps[:m], his[:m], lps[:m], nthreads=1)
+        per_l, per_h = (th - t) / m, (time.perf_counter() - th) / m
+        out["cpu_baseline"] = {
+            "value": round(rN, 2), "unit": "reports/s", "cores": cpu["threads"], "kind": "port",
+            "engine": "cpu_baseline/jc_cpu_engine.cpp (leader init + helper prep/aggregate + leader finish/aggregate, "
+                      "both roles)", "value_1_thread": round(r1, 2), **cpu,
+            "oracle_port_reports_per_s_1_core": round(1.0 / (per_l + per_h), 3),
+            "sample": f"{mN} reports at {cpu['threads']} threads ({dN:.1f} s), {min(K, 8)} at 1 thread ({d1:.1f} s); "
+                      f"C oracle {m} reports ({per_l * 1e3:.0f} + {per_h * 1e3:.0f} ms per report)"}
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
