@@ -410,10 +410,10 @@ def main():
     k1_dom = kt["xof"]["ms"] >= kt["flp"]["ms"]
     dominant = "K1 xof_kernel" if k1_dom else "K3 flp_psum_part_kernel"
     ach, alg = (k1_tops, k1_alg) if k1_dom else (k3_tops, k3_alg)
-    traffic, traffic_src, traffic_note = pmc_traffic("jx::xof_kernel<0, false>" if k1_dom else
-                                                     "jx::flp_psum_part_kernel<2, false, false>", chunk_reports)
+    traffic, traffic_src, traffic_note = pmc_traffic("jx::xof_kernel<false>" if k1_dom else
+                                                     "jx::flp_psum_part_glds_kernel<2, false, false, 4, 4>", chunk_reports)
     alg_bytes = (work["hbm_k1"] if k1_dom else work["hbm_k3"]) * chunk_reports
-    k1_clock = pmc_clock("jx::xof_kernel<0, false>")
+    k1_clock = pmc_clock("jx::xof_kernel<false>")
     k1_clock = round(k1_clock, 3) if k1_clock else None
     dom_ms = k1_ms if k1_dom else k3_ms
     out = {

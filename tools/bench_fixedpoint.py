@@ -52,6 +52,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--skip", default="", help="comma list of legs to skip: pingpong,pipelined,helper,leader,cpu")
+    ap.add_argument("--helper-staging-gb", type=int, default=0,
+                    help="staging budget of the helper engine in the two-role legs (default: the engine's own, 1/3 "
+                         "of HBM); raise it so one launch holds --reports")
     ap.add_argument("--leader-staged", action="store_true",
                     help="the leader stages its measurement share (debug option 6) instead of reading it in place")
     a = ap.parse_args()
@@ -105,6 +108,15 @@ def main():
     def per_launch(kt, stage):
         return round(kt[stage]["ms"] / max(1, kt[stage]["launches"]), 3)
 
+    def helper_engine():
+        if not a.helper_staging_gb:
+            return HelperEngine(vdaf, vk)
+        os.environ["JX_STAGING_GB"] = str(a.helper_staging_gb)
+        try:
+            return HelperEngine(vdaf, vk)
+        finally:
+            del os.environ["JX_STAGING_GB"]
+
     def timed_steps(step, engines):
         for _ in range(a.warmup):
             step(False)
@@ -134,7 +146,7 @@ def main():
         d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
         d_hv = torch.empty(R, dtype=torch.uint8, device=dev)
         d_lv = torch.empty(R, dtype=torch.uint8, device=dev)
-        leader, helper = HelperEngine(vdaf, vk), HelperEngine(vdaf, vk)
+        leader, helper = HelperEngine(vdaf, vk), helper_engine()
         if a.leader_staged:
             leader.debug(6, 1)
         role_s = {"leader_init": 0.0, "helper": 0.0, "leader_finish_acc": 0.0}
@@ -195,7 +207,7 @@ def main():
         d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
         d_hv = torch.empty(R, dtype=torch.uint8, device=dev)
         d_lv = torch.empty(R, dtype=torch.uint8, device=dev)
-        leader, helper = HelperEngine(vdaf, vk), HelperEngine(vdaf, vk)
+        leader, helper = HelperEngine(vdaf, vk), helper_engine()
         if a.leader_staged:
             leader.debug(6, 1)
         state = {"i": 0, "prev": None, "done": 0}
