@@ -252,7 +252,9 @@ int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]);
 
 /* Debug knobs (tests and measurements): option 1 = route every report through the slow XOF kernel;
  * 2 = accumulate chunking; 3 = helper K1 kernel (0 automatic: the fused two-sponge kernel, the
- * lane-split kernel for launches under one fused wave per SIMD; 3 lane-split; 5 fused, forced);
+ * lane-split kernel for launches under one fused wave per SIMD, the lane-pair kernel under one lane-split
+ * wave per SIMD; 3 lane-split; 5 fused, forced; 6 lane pairs); 6 = leader measurement share staged by K1
+ * (1) instead of read in place by the FLP kernels (0, default);
  * 5 = overlapped two-stream fused path. JX_K1_SPLIT sets option 3 at create. */
 int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value);
 

@@ -125,7 +125,7 @@ struct jx_engine {
   double ms[NST] = {0, 0, 0, 0};
   uint64_t launches[NST] = {0, 0, 0, 0};
   uint32_t force_slow = 0;
-  uint32_t k1_split = 0;  // helper K1: 0 automatic, 3 lane-split, 5 fused (JX_K1_SPLIT, debug option 3)
+  uint32_t k1_split = 0;  // helper K1: 0 automatic, 3 lane-split, 5 fused, 6 lane pairs (JX_K1_SPLIT, debug option 3)
   uint32_t leader_staged = 0;  // debug option 6: the leader stages its measurement share (no in-place reads)
   std::string err;
 };
@@ -687,9 +687,16 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
   b.k1_split = e->k1_split;
   // A helper launch that would give the fused two-sponge K1 less than one wave per SIMD is bound by
   // the per-report sponge latency, not by issue: the lane-split kernel runs it in twice the waves
-  // (FixedPointBoundedL2VecSum 16 x 10000, 24,576 reports: 153 -> 92 ms on MI355X).
+  // (FixedPointBoundedL2VecSum 16 x 10000, 24,576 reports: 153 -> 92 ms on MI355X), and below one
+  // lane-split wave per SIMD the lane-pair kernel splits every sponge over two lanes (round_reports:
+  // the fused kernel's two waves per SIMD, 4 x that many lane-split or 8 x lane-pair lanes).
   const bool wide = c.bits > 32 && (c.algo == ALGO_SUM || c.algo == ALGO_SUMVEC);
-  if (e->k1_split == 0 && !leader && !wide && e->round_reports && 2 * n <= e->round_reports) b.k1_split = 3;
+  if (e->k1_split == 0 && !leader && !wide && e->round_reports) {
+    if (4 * n <= e->round_reports)
+      b.k1_split = 6;
+    else if (2 * n <= e->round_reports)
+      b.k1_split = 3;
+  }
   hipEvent_t ev = nullptr;
   if (c.algo == ALGO_COUNT) {
     HIPCHK(e, stage_begin(e, &ev));
@@ -1004,7 +1011,7 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
   const uint64_t per = per_report_bytes(e->cfg);
   if (const char* env = getenv("JX_K1_SPLIT")) {
     const int v = atoi(env);
-    if (v == 0 || v == 3 || v == 5) e->k1_split = (uint32_t)v;
+    if (v == 0 || v == 3 || v == 5 || v == 6) e->k1_split = (uint32_t)v;
   }
   e->round_reports = k1_round_reports(e->cfg, device, e->k1_split);
   uint64_t budget = 48ull << 30;
@@ -1672,8 +1679,9 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
     return JX_OK;
   }
   if (option == 3) {  // helper K1 kernel
-    if (value != 0 && value != 3 && value != 5) return JX_E_INVALID;
-    // 0: automatic (fused; lane-split below one fused wave per SIMD), 3: lane-split, 5: fused
+    if (value != 0 && value != 3 && value != 5 && value != 6) return JX_E_INVALID;
+    // 0: automatic (fused; lane-split below one fused wave per SIMD, lane pairs below one lane-split
+    // wave per SIMD), 3: lane-split, 5: fused, 6: lane pairs (bits <= 32)
     e->k1_split = (uint32_t)value;
     return JX_OK;
   }

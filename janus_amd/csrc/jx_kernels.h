@@ -109,7 +109,8 @@ struct Bufs {
   uint8_t* msgs;
   const uint4* consts;
   uint32_t force_slow;  // debug: route every report through the slow XOF kernel
-  uint32_t k1_split;    // helper K1 kernel: 3 = lane-split (xof_lanes_kernel), otherwise the fused kernel
+  uint32_t k1_split;    // helper K1 kernel: 3 = lane-split (xof_lanes_kernel), 6 = lane pairs (xof_pairs_kernel,
+                        // bits <= 32), otherwise the fused kernel
 };
 
 struct AccArgs {

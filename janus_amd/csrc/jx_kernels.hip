@@ -999,6 +999,340 @@ __global__ __launch_bounds__(64 * K1_WAVES, WIDE ? 2 : 4) void xof_lanes_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------- K1, lane-pair helper
+// Launches that would give the lane-split kernel at most one wave per SIMD are bound by how fast ONE
+// wave issues its own dependent chain (a lone wave64 issues a VALU op every ~4-6.5 cycles, against 2
+// with a partner wave, MI355X_MICROARCH.md 'vector-instruction ISSUE cost'). This kernel halves each
+// sponge's chain instead: a Keccak state is split over a lane PAIR, the even lane holding the low and
+// the odd lane the high 32-bit halves of the 25 64-bit words (25 VGPRs each). A 64-bit rotation is
+// then one v_alignbit_b32 per lane between its own half and its partner's (fetched by a DPP quad_perm
+// [1,0,3,2] move): 124 instructions per round on each lane instead of 190 on one. Four lanes per
+// report: lanes 2k / 2k+1 of the lower half squeeze the measurement share (S, low / high halves),
+// lanes 32+2k / 33+2k absorb the joint_rand_part (J), 16 reports per wave, twice the waves of the
+// lane-split kernel and 1.45x its instructions per report, so it is the choice only below one
+// lane-split wave per SIMD (FixedPointBoundedL2VecSum 16 x 10000 at <= 32,768 reports per launch).
+// The S lanes emit the elements (each lane two of an element's four words), keep the truncation
+// word columns of their two words, and form J's message words from their own and their partner's
+// halves; v_permlane32_swap hands them to the J lanes.
+
+// the partner lane's value (lane ^ 1)
+__device__ __forceinline__ uint32_t pswap(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1, 0, 3, 2]
+}
+__device__ __forceinline__ uint64_t pswap64(uint64_t v) {
+  return (uint64_t)pswap((uint32_t)v) | ((uint64_t)pswap((uint32_t)(v >> 32)) << 32);
+}
+// this lane's half of rotl64(word, N) from its own and its partner's half (the same formula on both)
+template <int N>
+__device__ __forceinline__ uint32_t hrot(uint32_t own, uint32_t par) {
+  if constexpr (N == 0)
+    return own;
+  else if constexpr (N < 32)
+    return alignbit(own, par, 32 - N);
+  else if constexpr (N == 32)
+    return par;
+  else
+    return alignbit(par, own, 64 - N);
+}
+template <int I>
+__device__ __forceinline__ void rho_pi_half_one(const uint32_t* s, uint32_t* B) {
+  constexpr int R = RotOf<I>::value;
+  if constexpr (R == 0)
+    B[PiDst<I>::value] = s[I];
+  else
+    B[PiDst<I>::value] = hrot<R>(s[I], pswap(s[I]));
+}
+template <int... Is>
+__device__ __forceinline__ void rho_pi_half_all(const uint32_t* s, uint32_t* B, IndexSeq<Is...>) {
+  (rho_pi_half_one<Is>(s, B), ...);
+}
+// One Keccak-f[1600] round on this lane's half s[25]; rc = this lane's half of the round constant.
+// theta parity 10 v_bitop3, partner parities 5 DPP moves, D 5 alignbit + 5 xor, D applied 25 xor,
+// rho 24 DPP moves + 24 alignbit, chi 25 v_bitop3, iota 1: 124 VALU.
+__device__ __forceinline__ void keccak_round_half(uint32_t* s, uint32_t rc) {
+  uint32_t C[5], Cp[5], B[25];
+#pragma unroll
+  for (int x = 0; x < 5; x++) C[x] = xor3(xor3(s[x], s[x + 5], s[x + 10]), s[x + 15], s[x + 20]);
+#pragma unroll
+  for (int x = 0; x < 5; x++) Cp[x] = pswap(C[x]);
+#pragma unroll
+  for (int x = 0; x < 5; x++) {
+    const uint32_t D = C[(x + 4) % 5] ^ hrot<1>(C[(x + 1) % 5], Cp[(x + 1) % 5]);
+#pragma unroll
+    for (int y = 0; y < 5; y++) s[x + 5 * y] ^= D;
+  }
+  rho_pi_half_all(s, B, typename MakeSeq<25>::type{});
+#pragma unroll
+  for (int y = 0; y < 5; y++) {
+#pragma unroll
+    for (int x = 0; x < 5; x++) {
+      const int i = x + 5 * y, i1 = (x + 1) % 5 + 5 * y, i2 = (x + 2) % 5 + 5 * y;
+      s[i] = B[i] ^ (~B[i1] & B[i2]);
+    }
+  }
+  s[0] ^= rc;
+}
+__device__ __forceinline__ void keccak_p12_half(uint32_t* s, bool hi) {
+#pragma unroll 1
+  for (int ir = 12; ir < 24; ir++) keccak_round_half(s, hi ? KECCAK_RC_HI[ir] : KECCAK_RC_LO[ir]);
+}
+// a ? x1 : x0 as bit operations on an opaque all-ones / zero mask: a select between two array elements
+// written `a ? v[i + 1] : v[i]` becomes an indexed load v[i + a], which puts the array in scratch
+__device__ __forceinline__ uint32_t msel(uint32_t m, uint32_t x0, uint32_t x1) { return x0 ^ ((x0 ^ x1) & m); }
+// state := 0; absorb one final block (42 words, this lane takes words 2i + hi); permute
+__device__ __forceinline__ void sponge_oneblock_half(uint32_t* s, const Block& m, bool hi) {
+  const uint32_t hm = opaque_u32(hi ? 0xFFFFFFFFu : 0u);
+#pragma unroll
+  for (int i = 0; i < 21; i++) s[i] = msel(hm, m.w[2 * i], m.w[2 * i + 1]);
+#pragma unroll
+  for (int i = 21; i < 25; i++) s[i] = 0;
+  keccak_p12_half(s, hi);
+}
+
+__global__ __launch_bounds__(64 * K1_WAVES, 2) void xof_pairs_kernel(Cfg c, Bufs b) {
+  const uint32_t lane = threadIdx.x & 63;
+  const bool jh = lane >= 32;     // J lanes
+  const bool hi = (lane & 1u) != 0;  // high halves
+  const uint32_t hm = opaque_u32(hi ? 0xFFFFFFFFu : 0u);
+  const uint64_t gw = (uint64_t)blockIdx.x * K1_WAVES + (threadIdx.x >> 6);  // 16 reports per wave
+  const uint64_t blk = gw >> 2;
+  const uint32_t il = ((uint32_t)gw & 3u) * 16u + ((lane & 31u) >> 1);  // this report's slot in its 64-report block
+  const uint64_t nblk = (b.n + 63) / 64;
+  if (blk >= nblk) return;
+  const uint64_t r0 = blk * 64 + il;
+  const uint64_t r = r0 < b.n ? r0 : b.n - 1;
+  const uint8_t* hs = b.his + (uint64_t)c.his_bytes * r;
+  const uint32_t MB = c.meas_len * 16;
+  const uint32_t ML = 42 + MB;
+  const uint32_t NM = (MB + 167) / 168;
+  const uint32_t b_last = ML / 168;
+
+  uint32_t h[25];
+  {  // squeeze block 0 = XOF(k_meas, DST(1), [1]) on every lane pair
+    uint32_t kmeas[4];
+    load16(hs, kmeas);
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.dst_id, 1, kmeas);
+    blk_put_byte(m, pos, 1);
+    blk_pad(m, pos + 1);
+    sponge_oneblock_half(h, m, hi);
+  }
+  uint32_t hdr[11];
+  {
+    uint32_t nonce[4], kblind[4];
+    load16(b.nonces + 16 * r, nonce);
+    load16(hs + 32, kblind);
+    Block hb;
+    blk_zero(hb);
+    int pos = blk_xof_prefix(hb, c.dst_id, 7, kblind);
+    blk_put_byte(hb, pos, 1);  // agg_id
+#pragma unroll
+    for (int i = 0; i < 4; i++) blk_put_word(hb, pos + 1 + 4 * i, nonce[i]);
+#pragma unroll
+    for (int w = 0; w < 11; w++) hdr[w] = hb.w[w];
+  }
+  // S lanes: the truncation word columns of this lane's two words of an element (Ta: word 0 | 1, Tb:
+  // word 2 | 3), the element carry, the >= p screen (meaningful on the high lane: w & (z | 0x1F)) and
+  // the own halves 15..20 of the previous squeezed block (J's message words 0..10 need them)
+  uint64_t Ta = 0, Tb = 0;
+  uint32_t carry = 0, gmax = 0, pv[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) pv[k] = 0;
+  uint32_t* const mp32 = reinterpret_cast<uint32_t*>(b.meas + il_idx(blk, c.meas_len, 0, il)) + (hi ? 1u : 0u);
+  uint4* const op = b.outs + il_idx(blk, c.out_len, 0, il);
+  uint32_t tj = 0, ti = 0;  // uniform truncation position of the next measurement element
+  const uint32_t tlen = c.out_is_meas ? 0u : min(c.trunc_len, c.meas_len);
+  // S lanes: element e's words (a, bw) = (x, z) on the low lane, (y, w) on the high lane
+  auto emit = [&](uint32_t e, uint32_t a, uint32_t bw, uint32_t& tjl, uint32_t& til) {
+    if (e >= c.meas_len) return;
+    const uint32_t pb = pswap(bw);
+    gmax = max(gmax, bw & (pb | 0x1Fu));
+    mp32[(uint64_t)e * IL * 4] = a;
+    mp32[(uint64_t)e * IL * 4 + 2] = bw;
+    if (e < tlen) {
+      const uint32_t sh = opaque_u32(1u << tjl);
+      Ta += (uint64_t)a * sh;
+      Tb += (uint64_t)bw * sh;
+      ++tjl;
+      if (tjl == c.bits) {  // V = T0 + T1 2^32 + T2 2^64 + T3 2^96, finished on the low lane
+        TruncW tr;
+        tr.T[0] = Ta;
+        tr.T[1] = pswap64(Ta);
+        tr.T[2] = Tb;
+        tr.T[3] = pswap64(Tb);
+        const f128 val = truncw_value(tr);
+        if (!hi) op[(uint64_t)til * IL] = f_to_u4(val);
+        Ta = 0;
+        Tb = 0;
+        tjl = 0;
+        til++;
+      }
+    }
+  };
+  auto s_emit_block = [&](uint32_t m) {
+    uint32_t tjl = tj, til = ti;
+    const uint32_t e0 = 21 * (m >> 1);
+    if ((m & 1) == 0) {
+#pragma unroll
+      for (int ci = 0; ci < 10; ci++) emit(e0 + ci, h[2 * ci], h[2 * ci + 1], tjl, til);
+      carry = h[20];
+    } else {
+      emit(e0 + 10, carry, h[0], tjl, til);
+#pragma unroll
+      for (int ci = 0; ci < 10; ci++) emit(e0 + 11 + ci, h[1 + 2 * ci], h[2 + 2 * ci], tjl, til);
+    }
+  };
+  // uniform: advance (ti, tj) past the truncated elements of block m
+  auto advance_trunc = [&](uint32_t m) {
+    const uint32_t e0 = 21 * (m >> 1) + ((m & 1) ? 10u : 0u);
+    const uint32_t e1 = e0 + ((m & 1) ? 11u : 10u);
+    const uint32_t cnt = e1 <= tlen ? e1 - e0 : (e0 < tlen ? tlen - e0 : 0u);
+    tj += cnt;
+    while (tj >= c.bits && cnt) {
+      tj -= c.bits;
+      ti++;
+    }
+  };
+  // last absorbed block: message bytes [0, nb) of the block, then TurboSHAKE padding; jw[i] is this
+  // lane's word 2i + hi
+  auto pad_last_half = [&](uint32_t* jw, uint32_t nb) {
+#pragma unroll
+    for (int i = 0; i < 21; i++) {
+      const uint32_t w = 2 * i + (hi ? 1u : 0u);
+      const uint32_t lo_b = 4 * w;
+      if (lo_b >= nb)
+        jw[i] = 0;
+      else if (lo_b + 4 > nb)
+        jw[i] &= (1u << (8 * (nb - lo_b))) - 1u;
+      if (w == (nb >> 2)) jw[i] ^= 1u << (8 * (nb & 3));
+      if (w == 41) jw[i] ^= 0x80000000u;
+    }
+  };
+  // J's message words of a block from the S stream E (the previous block's halves 15..20, then the
+  // current block's): J word 2i + hi = alignbit(E_own[i - 5], E_par[i - 6 + hi], 16). Past the share
+  // (the block after the last squeezed one, m == b_last == NM) the current halves are a squeezed block
+  // that is not part of the message: every word they reach lies at or past byte nb, which the padding
+  // of that last block clears.
+  auto message = [&](uint32_t* jw) {
+    uint32_t Eo[21], Ep[22];
+#pragma unroll
+    for (int k = 0; k < 5; k++) Eo[k] = pv[k + 1];
+#pragma unroll
+    for (int k = 0; k < 16; k++) Eo[5 + k] = h[k];
+#pragma unroll
+    for (int k = 0; k < 6; k++) Ep[k] = pswap(pv[k]);
+#pragma unroll
+    for (int k = 0; k < 16; k++) Ep[6 + k] = pswap(h[k]);
+#pragma unroll
+    for (int i = 0; i < 21; i++) jw[i] = alignbit(Eo[i], msel(hm, Ep[i], Ep[i + 1]), 16);
+  };
+
+  if (!jh) s_emit_block(0);
+  advance_trunc(0);
+  {
+    // J's message block 0: the 42-byte header || S_0[0, 126) (the J lanes hold S_0 too)
+    uint32_t Hp[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) Hp[k] = pswap(h[k]);
+    uint32_t jw[21];
+#pragma unroll
+    for (int i = 0; i < 5; i++) jw[i] = msel(hm, hdr[2 * i], hdr[2 * i + 1]);
+    jw[5] = msel(hm, (hdr[10] & 0xffffu) | (h[0] << 16), alignbit(h[0], Hp[0], 16));
+#pragma unroll
+    for (int i = 6; i < 21; i++) jw[i] = alignbit(h[i - 5], msel(hm, Hp[i - 6], Hp[i - 5]), 16);
+    if (b_last == 0) pad_last_half(jw, ML);
+#pragma unroll
+    for (int k = 0; k < 6; k++) pv[k] = h[15 + k];
+    if (jh) {
+#pragma unroll
+      for (int i = 0; i < 21; i++) h[i] = jw[i];
+#pragma unroll
+      for (int i = 21; i < 25; i++) h[i] = 0;
+    }
+  }
+#pragma unroll 1
+  for (uint32_t m = 1; m <= b_last; m++) {
+    keccak_p12_half(h, hi);  // S: squeeze block m; J: absorb block m - 1
+    const bool have = m < NM;
+    if (have) {
+      if (!jh) s_emit_block(m);
+      advance_trunc(m);
+    }
+    uint32_t msg[21], jw[21];
+    message(msg);
+#pragma unroll
+    for (int k = 0; k < 6; k++) pv[k] = h[15 + k];
+    uint32_t dead = h[0];
+#pragma unroll
+    for (int i = 0; i < 21; i++) {  // S lanes -> J lanes (lane l -> l + 32, the same half)
+      const auto r2 = __builtin_amdgcn_permlane32_swap(dead, msg[i], false, false);
+      jw[i] = r2[0];
+      dead = r2[1];
+    }
+    if (jh) {
+      if (m == b_last) pad_last_half(jw, ML - 168 * m);
+#pragma unroll
+      for (int i = 0; i < 21; i++) h[i] ^= jw[i];
+    }
+  }
+  keccak_p12_half(h, hi);  // J: absorb block b_last
+  // J state words 0..3: the low J lane holds words 0, 2 and gets 1, 3 from its partner
+  const uint32_t p0 = pswap(h[0]), p1 = pswap(h[1]);
+  uint32_t own_part[4] = {h[0], p0, h[1], p1};
+
+  // proof share: XOF(k_proofs, DST(2), [PROOFS=1, agg_id=1]) on every lane pair, emitted by the S lanes
+  uint32_t* const pp32 = reinterpret_cast<uint32_t*>(b.proof + il_idx(blk, c.proof_len, 0, il)) + (hi ? 1u : 0u);
+  {
+    uint32_t kproof[4];
+    load16(hs + 16, kproof);
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.dst_id, 2, kproof);
+    blk_put_byte(m, pos, 1);
+    blk_put_byte(m, pos + 1, 1);
+    blk_pad(m, pos + 2);
+    sponge_oneblock_half(h, m, hi);
+  }
+  auto emit_p = [&](uint32_t e, uint32_t a, uint32_t bw) {
+    if (e >= c.proof_len) return;
+    const uint32_t pb = pswap(bw);
+    gmax = max(gmax, bw & (pb | 0x1Fu));
+    if (!jh) {
+      pp32[(uint64_t)e * IL * 4] = a;
+      pp32[(uint64_t)e * IL * 4 + 2] = bw;
+    }
+  };
+  carry = 0;
+  const uint32_t NP = (c.proof_len * 16 + 167) / 168;
+#pragma unroll 1
+  for (uint32_t m = 0; m < NP; m++) {
+    if (m > 0) keccak_p12_half(h, hi);
+    const uint32_t e0 = 21 * (m >> 1);
+    if ((m & 1) == 0) {
+#pragma unroll
+      for (int ci = 0; ci < 10; ci++) emit_p(e0 + ci, h[2 * ci], h[2 * ci + 1]);
+      carry = h[20];
+    } else {
+      emit_p(e0 + 10, carry, h[0]);
+#pragma unroll
+      for (int ci = 0; ci < 10; ci++) emit_p(e0 + 11 + ci, h[1 + 2 * ci], h[2 + 2 * ci]);
+    }
+  }
+  // the high S lane's screen -> its low partner -> the low J lane, which finishes the report
+  const uint32_t smax = lower_to_upper(pswap(gmax));
+  if (jh && !hi) {
+    uint32_t flags = smax == 0xFFFFFFFFu ? FLAG_SLOW : 0u;
+    uint32_t nonce[4], part_l[4], lead_part[4];
+    load16(b.nonces + 16 * r, nonce);
+    load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
+    load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
+    flags = xof_tail(c, b, blk, il, r, r0 < b.n, nonce, part_l, lead_part, own_part, flags, false);
+    if (b.force_slow) flags |= FLAG_SLOW;
+    if (r0 < b.n) b.flags[r0] = flags;
+  }
+}
+
 // ---------------------------------------------------------------------------- K1, leader role
 // leader_initialized (aggregation_job_driver.rs:345): prepare_init with agg_id 0 on the explicit leader
 // input share [meas || proofs || k_blind], one report per lane. Only the joint_rand_part absorb runs
@@ -2445,6 +2779,8 @@ hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
     hipLaunchKernelGGL((xof_leader_kernel<false, true>), grid, block, 0, s, c, b);
   else if (b.leader)
     hipLaunchKernelGGL((xof_leader_kernel<false, false>), grid, block, 0, s, c, b);
+  else if (b.k1_split == 6 && !wide)  // lane pairs: 16 reports per wave
+    hipLaunchKernelGGL(xof_pairs_kernel, dim3((4 * nb + K1_WAVES - 1) / K1_WAVES), block, 0, s, c, b);
   else if (b.k1_split == 3) {  // lane-split: 32 reports per wave
     const dim3 g2((2 * nb + K1_WAVES - 1) / K1_WAVES);
     if (wide)
@@ -2473,6 +2809,9 @@ uint64_t k1_round_reports(const Cfg& c, int device, uint32_t k1_split) {
   } else if (k1_split == 3) {
     st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_lanes_kernel<false>, threads, 0);
     per_wg = threads / 2;
+  } else if (k1_split == 6) {
+    st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_pairs_kernel, threads, 0);
+    per_wg = threads / 4;
   } else {
     st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_kernel<false>, threads, 0);
   }
