@@ -23,7 +23,9 @@ def ht():
     hdrs = [os.path.join(HERE, "..", "janus_amd", "csrc", h) for h in ("jx_field.h", "jx_keccak.h", "jx_sha256.h",
                                                                          "jx_hpke.h", "jx_sha_aes.h")]
     if not os.path.exists(so) or any(os.path.getmtime(h) > os.path.getmtime(so) for h in hdrs + [src]):
-        subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", so, src], check=True)
+        tmp = f"{so}.{os.getpid()}.tmp"  # atomic: pytest-xdist workers may build concurrently
+        subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", tmp, src], check=True)
+        os.replace(tmp, so)
     L = ctypes.CDLL(so)
     vp = ctypes.c_void_p
     L.ht_f128.argtypes = [ctypes.c_int, vp, vp, vp]
