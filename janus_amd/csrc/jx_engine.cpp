@@ -342,6 +342,12 @@ static int32_t make_cfg(const jx_prio3_params* p, const uint8_t* vk, uint32_t vk
     c.ncoef = COEF_K + c.calls;
   else
     c.ncoef = COEF_K + 2 * c.calls;
+  if (c.algo == ALGO_SUMVEC || c.algo == ALGO_HISTOGRAM || fp) {  // gadget 0's power tables (jx_kernels.h)
+    c.c_rpow = c.ncoef;
+    c.ncoef += c.chunk;
+    c.c_tpow = c.ncoef;
+    c.ncoef += c.ngroups;
+  }
   if (fp) {
     c.coef1 = c.ncoef;
     c.ncoef += G1_K + c.calls1;

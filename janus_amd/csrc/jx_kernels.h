@@ -62,6 +62,10 @@ struct Cfg {
   uint32_t proof1_off;  // first element of gadget 1's sub-proof [seeds (chunk1) || gadget poly]
   uint32_t coef1;       // first coefficient slot of gadget 1 (G1_* below)
   uint32_t c_omega1, c_S1;  // constant-table offsets of gadget 1's roots and S1_m
+  // ParallelSum(Mul) gadget 0 (SumVec, Histogram, FixedPoint): per-report power tables K1 writes so that
+  // the FLP group finish needs no exponentiation: c_rpow + j = r^(j+1) canonical (j < chunk), c_tpow + g
+  // = t^(g * per) R, per = ceil(gpoly_len / ngroups) (the group's first gadget-polynomial coefficient)
+  uint32_t c_rpow, c_tpow;
 };
 
 // coefficient slots (Montgomery form unless noted) for the ParallelSum / Sum FLP

@@ -490,6 +490,21 @@ __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t
       st_il(coef, blk, NC, sk + 1, lane, mont128(ck, rp));
       rp = mont128(rp, rc);
     }
+    // power tables of the ParallelSum group finish (psum_part_finish): r^(j+1) canonical for the even
+    // wires of slot j (a chain of mont products starting from the canonical r), and t^(g * per) R for
+    // group g's share of G(t)
+    f128 rj = jr[0];
+    for (uint32_t j = 0; j < c.chunk; j++) {
+      st_il(coef, blk, NC, c.c_rpow + j, lane, rj);
+      rj = mont128(rj, rR);
+    }
+    const uint32_t per = (c.gpoly_len + c.ngroups - 1) / c.ngroups;
+    const f128 tstep = mpow(tR, per);
+    f128 tg = R1;
+    for (uint32_t g = 0; g < c.ngroups; g++) {
+      st_il(coef, blk, NC, c.c_tpow + g, lane, tg);
+      tg = mont128(tg, tstep);
+    }
   }
   if (c.algo == ALGO_FIXEDPOINT_L2) {
     // gadget 1 (the norm's ParallelSum(PolyEval)): its own query randomness t1 and P1-th roots
@@ -1814,22 +1829,21 @@ __device__ __forceinline__ void psum_part_finish(const Cfg& c, const Bufs& b, ui
   }
   // ---- wires at t for this group's slots, plus the leader's verifier share
   const f128 LR = u4_to_f(coefb[COEF_L * IL]), c0R = u4_to_f(coefb[COEF_C0 * IL]);
-  const f128 hs = u4_to_f(coefb[COEF_HALFSUM * IL]), tR = u4_to_f(coefb[COEF_T * IL]);
-  const f128 rR = u4_to_f(coefb[COEF_R * IL]);
+  const f128 hs = u4_to_f(coefb[COEF_HALFSUM * IL]);
   bool dfail = false;
   f128 prod = make128(0, 0);
-  f128 rpow = mpow(rR, j0 + 1);
 #pragma unroll
   for (int i = 0; i < PPW; i++) {
     const uint32_t j = j0 + i;
     if (j < chunk) {
       f128 se = ld_il(b.proof, blk, c.proof_len, 2 * j, lane);
       f128 so = ld_il(b.proof, blk, c.proof_len, 2 * j + 1, lane);
-      // from Montgomery form: E = sum_k d_k x_{k,i}, O = sum_k c_k x_{k,i} (canonical)
-      f128 E = mont128(wacc_reduce(ae[i]), make128(1, 0)), O = mont128(wacc_reduce(ao[i]), make128(1, 0));
-      f128 We = mont128(add128(mont128(se, c0R), mont128(E, rpow)), LR);
+      // the sums are R-scaled (c_k, d_k are stored in Montgomery form): mont(sum, r^(j+1)) with the
+      // canonical table power is E r^(j+1), and O = mont(sum, 1) (canonical)
+      const f128 rpow = u4_to_f(coefb[(c.c_rpow + j) * IL]);
+      f128 Er = mont128(wacc_reduce(ae[i]), rpow), O = mont128(wacc_reduce(ao[i]), make128(1, 0));
+      f128 We = mont128(add128(mont128(se, c0R), Er), LR);
       f128 Wo = mont128(sub128(add128(mont128(so, c0R), O), hs), LR);
-      rpow = mont128(rpow, rR);
       if (LEADER) {  // the leader's verifier share: wire values at t
         if (r0 < b.n) {
           uint4* o = reinterpret_cast<uint4*>(b.lps_out + (uint64_t)c.lps_bytes * r);
@@ -1850,12 +1864,13 @@ __device__ __forceinline__ void psum_part_finish(const Cfg& c, const Bufs& b, ui
   const uint4* Sm = b.consts + c.c_S;
   f128 vpart = make128(0, 0), gpart = make128(0, 0);
   if (m0 < m1) {
+    const f128 tR = u4_to_f(coefb[COEF_T * IL]);
     for (uint32_t m = m1; m-- > m0;) {
       f128 gm = ld_il(b.proof, blk, c.proof_len, A + m, lane);
       vpart = add128(vpart, mont128(gm, u4_to_f(Sm[m])));
       gpart = add128(mont128(gpart, tR), gm);
     }
-    gpart = mont128(gpart, mpow(tR, m0));
+    gpart = mont128(gpart, u4_to_f(coefb[(c.c_tpow + g) * IL]));  // t^m0 R (K1's table)
   }
   uint4* pp = b.part + ((blk * c.ngt + g) * 4) * IL + lane;
   pp[0] = f_to_u4(prod);
