@@ -86,8 +86,10 @@ enum : uint32_t {
   G1_K = 3,   // c'_k, k = 1..calls1
 };
 // misc constants (uint4 slots at Cfg::c_misc): 0 (1/P)R, 1 1/2, 2 R, 3 (1/2)R; FixedPoint: 4 2^n,
-// 5 2^(2n-2) R^-1, 6 2^(n-2) (gadget-1 padding, a share of the encoded 0.0), 7 (1/P1)R
-constexpr uint32_t NMISC = 8;
+// 5 2^(2n-2) R^-1, 6 2^(n-2) (gadget-1 padding, a share of the encoded 0.0), 7 (1/P1)R; 8 zero (the
+// source of the FLP ring's loads for measurement elements past the share and for padded slots)
+constexpr uint32_t NMISC = 9;
+constexpr uint32_t MISC_ZERO = 8;
 
 struct Bufs {
   uint64_t n;  // reports in this launch

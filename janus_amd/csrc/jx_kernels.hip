@@ -1987,12 +1987,13 @@ __device__ __forceinline__ void glds16(const uint4* src, uint4* lds_row) {
 
 // K3 with an LDS-DMA ring of depth D (4). A workgroup is K3W waves = K3W consecutive slot
 // groups of one 64-report block. Per call k, wave 0 streams c_k and wave 1 d_k (one
-// global_load_lds_dwordx4 each: 1 KiB, the block's 64 reports) into ring slot (k-1) % D, and every live
+// global_load_lds_dwordx4 each: 1 KiB, the block's 64 reports) into ring slot (k-1) % D, and every
 // wave its own PPW measurement elements; the coefficients are fetched once per K3W groups instead of
 // once per group, and D-1 calls stay in flight without holding VGPRs. One s_barrier per call: after it,
 // every wave's loads of call k have landed (each waited for its own with vmcnt) and every wave has
-// finished reading call k-1's slot, which the next issue overwrites. Calls beyond floor(M / chunk)
-// (the ragged last one) go through psum_part_finish's guarded loads.
+// finished reading call k-1's slot, which the next issue overwrites. Every call runs in the ring: an
+// element past the share (the ragged last call) or of a padded slot is loaded from a zero constant, so
+// it adds nothing, and a padding group's wave only keeps the barriers.
 constexpr uint32_t K3W = 4;
 // LDS address of a __shared__ object
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
@@ -2029,13 +2030,13 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
   const uint32_t g = wg * W + wave;
   const uint32_t C = c.calls, chunk = c.chunk, M = c.meas_len;
   const uint32_t j0 = g * PPW;
-  const bool full = g < NG && j0 + PPW <= chunk;  // this wave's PPW slots are all real
   const uint4* coefb = b.coef + il_idx(blk, c.ncoef, 0, lane);
   const MeasView measb = meas_view(c, b, blk, lane);
-  // calls whose every slot is a measurement element; a wave whose group is padded or absent runs the
-  // loop for the barriers (and, waves 0/1, the coefficient loads) but computes in the tail only
-  const uint32_t kfw = C < M / chunk ? C : M / chunk;
-  const uint32_t kf = full ? kfw : 0;
+  const uint4* zero = b.consts + c.c_misc + MISC_ZERO;
+  const uint32_t kfw = C;  // every call (see above)
+  bool real[PPW];          // slot j0 + i exists (a padding group's wave has none)
+#pragma unroll
+  for (int i = 0; i < PPW; i++) real[i] = g < NG && j0 + i < chunk;
 
   wacc26 ae[PPW], ao[PPW];
   acc192 sx;
@@ -2049,24 +2050,20 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
   auto issue = [&](uint32_t k) {
     const uint32_t sl = (k - 1) % D;
     if (wave < 2) glds16(coefb + (uint64_t)(COEF_K + 2 * (k - 1) + wave) * IL, &ring[sl][wave][0]);
-    if (full) {
 #pragma unroll
-      for (int i = 0; i < PPW; i++) {
-        const uint64_t e = (uint64_t)((k - 1) * chunk + j0 + i);
-        glds16(&measb[e], &ring[sl][2 + wave * PPW + i][0]);
-      }
+    for (int i = 0; i < PPW; i++) {
+      const uint32_t e = (k - 1) * chunk + j0 + i;
+      glds16(real[i] && e < M ? &measb[e] : zero, &ring[sl][2 + wave * PPW + i][0]);
     }
   };
-  // loads a wave issues per call: 1 (coefficient, waves 0/1) + PPW (measurement, full groups)
+  // loads a wave issues per call: 1 (coefficient, waves 0/1) + PPW (measurement)
   auto wait_call = [&](bool tail) {
     if (tail) {
       wait_vmcnt<0>();
-    } else if (wave < 2 && full) {
-      wait_vmcnt<(D - 2) * (PPW + 1)>();
-    } else if (full) {
-      wait_vmcnt<(D - 2) * PPW>();
     } else if (wave < 2) {
-      wait_vmcnt<D - 2>();
+      wait_vmcnt<(D - 2) * (PPW + 1)>();
+    } else {
+      wait_vmcnt<(D - 2) * PPW>();
     }
   };
   for (uint32_t k = 1; k < D && k <= kfw; k++) issue(k);
@@ -2077,7 +2074,7 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
     wait_call(k + D - 2 > kfw);  // near the end fewer calls are in flight: wait for all
     __builtin_amdgcn_s_barrier();
     if (k + D - 1 <= kfw) issue(k + D - 1);
-    if (full) {
+    if (g < NG) {
       const uint32_t a = ring_base + ((k - 1) % D) * SLOT_BYTES;
       uint4 cv, dv, xv[PPW];
       lds_read4(a, a + ROW_BYTES, a + (2 + wave * PPW) * ROW_BYTES, a + (3 + wave * PPW) * ROW_BYTES, cv, dv, xv[0],
@@ -2102,7 +2099,7 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
     }
   }
   if (g >= NG) return;
-  psum_part_finish<PPW, HIST, LEADER>(c, b, blk, g, lane, kf, ae, ao, sx);
+  psum_part_finish<PPW, HIST, LEADER>(c, b, blk, g, lane, C, ae, ao, sx);
 }
 
 template <bool HIST, bool LEADER>
