@@ -2175,7 +2175,7 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
 // an LDS ring by LDS-DMA, one s_barrier per step. The accumulators fold to a 288-bit signed sum per (slot,
 // coefficient): 4-row groups to 64-bit columns, v_permlane32_swap gathers a slot's 8 columns in one lane
 // (c in lanes 0..31, d in 32..63), then a reduction mod p; the sums go to Bufs::xs and the wires kernel.
-constexpr uint32_t MF_WAVES = 8, MF_NG = 3, MF_D = 4;
+constexpr uint32_t MF_WAVES = 8, MF_NG = 3, MF_KC = 4;  // waves (reports), 32-slot groups, calls per K-step
 typedef int mf_v4i __attribute__((ext_vector_type(4)));
 typedef int mf_v16i __attribute__((ext_vector_type(16)));
 
@@ -2195,168 +2195,268 @@ __device__ __forceinline__ uint32_t mf_sel(uint32_t a, uint32_t w) {
 // clamp a coefficient dword index into 0..3 (a clamped dword's bytes are never selected)
 __device__ __forceinline__ uint32_t mf_dw(int i) { return (uint32_t)(i < 0 ? 0 : (i > 3 ? 3 : i)); }
 
-template <int NGR>
-__global__ __launch_bounds__(64 * MF_WAVES, 1) void flp_psum_mfma_kernel(Cfg c, Bufs b) {
+template <int NGR, uint32_t MF_D, int PROBE = 0, uint32_t KC = MF_KC, int WGS = 1>
+__global__ __launch_bounds__(64 * MF_WAVES, 2 * WGS) void flp_psum_mfma_kernel(Cfg c, Bufs b) {
   constexpr uint32_t SLOTS = 32 * NGR;
-  constexpr uint32_t XE = 2 * SLOTS * 8;  // x entries (16 B) per ring slot: [call h][slot][report]
-  constexpr uint32_t RS = XE + 64;        // + coefficient entries [cd][h][report] (32 used)
+  constexpr uint32_t XE = KC * SLOTS * 8;  // x entries (16 B) per ring slot: [call][slot][report]
+  constexpr uint32_t RS = XE + 128;        // + coefficient entries [cd][call][report], then [report][cd] corrections
   constexpr uint32_t NDMA = XE / 64;      // x DMA instructions per K-step
+  constexpr uint32_t NI = (NDMA + MF_WAVES - 1) / MF_WAVES;  // x DMA instructions per wave (at most)
+  static_assert(NDMA % MF_WAVES == 0, "every wave issues NI x instructions");
   __shared__ uint4 ring[MF_D * RS];
-  const uint32_t NSC = (c.chunk + SLOTS - 1) / SLOTS;  // slot chunks
-  const uint32_t bid = blockIdx.x, xcd = bid & 7u, q8 = bid >> 3, u = q8 % (8 * NSC);
-  const uint64_t blk = (uint64_t)(q8 / (8 * NSC)) * 8 + xcd;
-  const uint64_t nblk = (b.n + 63) / 64;
-  if (blk >= nblk) return;  // uniform over the workgroup
-  const uint32_t e8 = u / NSC, s0 = (u % NSC) * SLOTS;  // eighth of the block, first slot
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
   const uint32_t C = c.calls, chunk = c.chunk, M = c.meas_len, NC = c.ncoef;
-  const uint32_t KS = (C + 1) / 2;
+  const uint32_t KS = (C + KC - 1) / KC;
+  const uint32_t NSC = (chunk + SLOTS - 1) / SLOTS;  // slot chunks
+  const uint64_t nblk = (b.n + 63) / 64;
+  // units (64-report block, eighth, slot chunk), numbered so that unit u runs on XCD u % 8 with the other
+  // units of its block: u = (blk / 8) * 64 NSC + (e8 * NSC + sc) * 8 + blk % 8. This persistent workgroup
+  // takes units blockIdx.x, + gridDim.x, ... (gridDim.x is a multiple of 8) and streams their K-steps
+  // back to back through one ring, so a unit's first steps load under the previous unit's last ones.
+  const uint32_t G = gridDim.x;
+  const uint64_t NU = (nblk + 7) / 8 * 8 * 8 * NSC;
+  const uint64_t nj = blockIdx.x < NU ? (NU - blockIdx.x + G - 1) / G : 0;
+  const uint32_t T = (uint32_t)(nj * KS);  // K-steps of this workgroup
   const uint4* zero = b.consts + c.c_misc + MISC_ZERO;
-
-  // K-step ks (calls 2 ks + 1, 2 ks + 2) into ring slot ks % MF_D. x entry p = 64 i + lane of instruction
-  // i: row = p >> 3 = h * SLOTS + slot, report = (p & 7) ^ ((slot >> 1) & 7) (swizzled so that a wave's
-  // ds_read_b128 of 16 slots touches 16 distinct bank quads)
-  auto issue = [&](uint32_t ks) {
-    uint4* rs = ring + (ks % MF_D) * RS;
-    for (uint32_t i = wave; i < NDMA; i += MF_WAVES) {
-      const uint32_t p = 64 * i + lane, row = p >> 3;
-      const uint32_t hh = row / SLOTS, sl = row % SLOTS, r = (p & 7u) ^ ((sl >> 1) & 7u);
-      const uint32_t k = 2 * ks + hh + 1, e = (k - 1) * chunk + s0 + sl;
-      const MeasView mv = meas_view(c, b, blk, 8 * e8 + r);
-      glds16(k <= C && s0 + sl < chunk && e < M ? &mv[e] : zero, rs + 64 * i);
+  struct Unit {
+    uint64_t blk;
+    uint32_t e8, s0;
+    bool live;
+  };
+  auto unit_of = [&](uint64_t j) {
+    const uint64_t u = blockIdx.x + j * G;
+    const uint64_t q = u >> 3, per = 8ull * NSC;
+    Unit un;
+    un.blk = (q / per) * 8 + (u & 7);
+    const uint32_t w = (uint32_t)(q % per);
+    un.e8 = w / NSC;
+    un.s0 = (w % NSC) * SLOTS;
+    un.live = un.blk < nblk;
+    return un;
+  };
+  // this lane's x entries: instruction i writes entry p = 64 (NI wave + i) + lane; row = p >> 3 =
+  // call * SLOTS + slot, report (p & 7) ^ ((slot >> 1) & 7) (swizzled: a wave's ds_read_b128 of 16 slots
+  // touches 16 distinct bank quads)
+  uint32_t x_hh[NI], x_sl[NI], x_r[NI];
+#pragma unroll
+  for (uint32_t i = 0; i < NI; i++) {
+    const uint32_t p = 64 * (NI * wave + i) + lane, row = p >> 3;
+    x_hh[i] = row / SLOTS;
+    x_sl[i] = row % SLOTS;
+    x_r[i] = (p & 7u) ^ ((x_sl[i] >> 1) & 7u);
+  }
+  // the last wave streams the coefficient digits (entry 8 KC cd + 8 call + r, one instruction) and, with a
+  // unit's first step, the 8 reports' two bias corrections (entry 8 KC 2 + 2 r + cd, lanes 0..15 of a second
+  // one): read back from LDS they cost the fold no global load, whose wait would drain the whole ring
+  // (vmcnt counts in order)
+  static_assert(2 * KC * 8 <= 64, "one coefficient DMA instruction per step");
+  const bool coef_lane = wave == MF_WAVES - 1;
+  const uint32_t c_r = lane & 7, c_hh = (lane >> 3) & (KC - 1), c_cd = lane / (8 * KC);  // c_cd > 1: unused lane
+  const uint32_t k_r = lane >> 1, k_cd = lane & 1;
+  // the issue cursor (unit j, step ks) advances one K-step per call; per-unit lane state is set up once
+  const uint4* x_base[NI];
+  uint32_t x_e0[NI];
+  bool x_ok[NI];
+  uint64_t x_es = 0;
+  const uint4* c_base = zero;
+  const uint4* k_src = zero;
+  bool i_live = false;
+  uint64_t ij = 0;
+  uint32_t iks = 0;
+  auto issue_unit = [&]() {
+    const Unit un = unit_of(ij);
+    i_live = un.live;
+#pragma unroll
+    for (uint32_t i = 0; i < NI; i++) {
+      const MeasView mv = meas_view(c, b, un.live ? un.blk : 0, 8 * un.e8 + x_r[i]);
+      x_base[i] = mv.p;
+      x_es = mv.es;
+      const uint32_t sl = un.s0 + x_sl[i];
+      x_ok[i] = un.live && sl < chunk;
+      x_e0[i] = x_hh[i] * chunk + sl;
     }
-    if (wave == MF_WAVES - 1) {  // coefficient digits: entry 16 cd + 8 h + r (lanes 32..63: padding)
-      const uint32_t r = lane & 7, hh = (lane >> 3) & 1, cd = (lane >> 4) & 1;
-      const uint32_t k = 2 * ks + hh + 1;
-      glds16(lane < 32 && k <= C ? b.coef + il_idx(blk, NC, COEF_K + 2 * (k - 1) + cd, 8 * e8 + r) : zero, rs + XE);
+    c_base = b.coef + il_idx(un.live ? un.blk : 0, NC, COEF_K + (c_cd & 1), 8 * un.e8 + c_r);
+    k_src = un.live && lane < 16 ? b.coef + il_idx(un.blk, NC, c.c_corr + k_cd, 8 * un.e8 + k_r) : zero;
+  };
+  auto issue = [&](uint32_t t) {  // step t of this workgroup = the cursor's (ij, iks)
+    if (iks == 0) issue_unit();
+    uint4* rs = ring + (t % MF_D) * RS;
+    const uint32_t de = KC * iks * chunk;
+#pragma unroll
+    for (uint32_t i = 0; i < NI; i++) {
+      const uint32_t e = x_e0[i] + de;  // e < M implies call <= C
+      glds16(x_ok[i] && e < M ? x_base[i] + (uint64_t)e * x_es : zero, rs + 64 * (NI * wave + i));
+    }
+    if (coef_lane) {
+      const uint32_t k = KC * iks + c_hh + 1;
+      glds16(i_live && c_cd < 2 && k <= C ? c_base + (uint64_t)(2 * (k - 1)) * IL : zero, rs + XE);
+      glds16(iks == 0 ? k_src : zero, rs + XE + 64);
+    }
+    if (++iks == KS) {
+      iks = 0;
+      ij++;
     }
   };
-  constexpr uint32_t NI = (NDMA + MF_WAVES - 1) / MF_WAVES;  // x DMA instructions of wave 0 (the most)
-  const uint32_t nmine = (NDMA > wave ? (NDMA - wave + MF_WAVES - 1) / MF_WAVES : 0) + (wave == MF_WAVES - 1);
-  static_assert(NI + 1 < 16, "vmcnt budget");
 
-  // per-lane constants: window selectors (row a = l31) and source dwords, B read offsets
+  // per-lane constants of the coefficient window (row a = l31) and the element reads
   uint32_t sel[4];
 #pragma unroll
   for (int w = 0; w < 4; w++) sel[w] = mf_sel(l31, w);
   const int a4 = (int)(l31 >> 2);
-  mf_v16i acc[NGR][2];
-#pragma unroll
-  for (int g = 0; g < NGR; g++)
-#pragma unroll
-    for (int cd = 0; cd < 2; cd++)
-#pragma unroll
-      for (int i = 0; i < 16; i++) acc[g][cd][i] = 0;
-
-  for (uint32_t ks = 0; ks + 1 < MF_D && ks < KS; ks++) issue(ks);
-  const uint32_t ring_base = lds_addr(ring);
-  // A source dwords (5 consecutive digit dwords a4-4 .. a4, clamped) of coefficient entry (cd, h, wave)
   uint32_t aoff[5];
 #pragma unroll
   for (int i = 0; i < 5; i++) aoff[i] = 4 * mf_dw(a4 - 4 + i);
-  // B: element (h, slot 32 g + l31) of report `wave`
-  uint32_t boff[NGR];
+  uint32_t boff[NGR];  // element (call h of the pair, slot 32 g + l31) of report `wave`
 #pragma unroll
   for (int g = 0; g < NGR; g++) {
     const uint32_t sl = 32 * g + l31;
     boff[g] = 16 * ((h * SLOTS + sl) * 8 + (wave ^ ((sl >> 1) & 7u)));
   }
+  const uint32_t ring_base = lds_addr(ring);
+  const f128 c288 = u4_to_f(b.consts[c.c_misc + MISC_2P288]);
+
+  mf_v16i acc[NGR][2];
+  auto acc_zero = [&]() {
+#pragma unroll
+    for (int g = 0; g < NGR; g++)
+#pragma unroll
+      for (int cd = 0; cd < 2; cd++)
+#pragma unroll
+        for (int i = 0; i < 16; i++) acc[g][cd][i] = 0;
+  };
+  acc_zero();
+  f128 corr = make128(0, 0);
+  for (uint32_t t = 0; t + 1 < MF_D && t < T; t++) issue(t);
+  uint64_t j = 0;
+  uint32_t ks = 0;
 #pragma unroll 1
-  for (uint32_t ks = 0; ks < KS; ks++) {
-    // this wave's loads of step ks have landed once at most the next step's are outstanding
-    if (ks + MF_D - 2 >= KS) {
+  for (uint32_t t = 0; t < T; t++) {
+    // this wave's loads of step t have landed once at most the next MF_D - 2 steps' are outstanding
+    if (t + MF_D - 2 >= T) {
       wait_vmcnt<0>();
-    } else if (nmine == NI + 1) {
-      wait_vmcnt<(MF_D - 2) * (NI + 1)>();
-    } else if (nmine == NI) {
-      wait_vmcnt<(MF_D - 2) * NI>();
+    } else if (coef_lane) {
+      wait_vmcnt<(MF_D - 2) * (NI + 2)>();
     } else {
-      wait_vmcnt<(MF_D - 2) * (NI - 1)>();
+      wait_vmcnt<(MF_D - 2) * NI>();
     }
     __builtin_amdgcn_s_barrier();
-    if (ks + MF_D - 1 < KS) issue(ks + MF_D - 1);
-    const uint32_t sb = ring_base + (ks % MF_D) * RS * 16;
-    const uint32_t ca = sb + XE * 16 + 16 * (8 * h + wave);  // coefficient entry (cd = 0)
-    // every LDS read of the step and its wait in ONE asm statement: the outputs must not be consumed before
-    // the wait (the compiler cannot see the dependence of a separate waitcnt statement), and ordinary LDS
-    // loads would make it drain the outstanding LDS-DMA (vmcnt(0)) first
-    static_assert(NGR == 3, "the asm below reads three slot groups");
-    uint32_t dc[5], dd[5];
-    uint4 xv[NGR];
-    asm volatile(
-        "ds_read_b32 %0, %13\n\tds_read_b32 %1, %14\n\tds_read_b32 %2, %15\n\tds_read_b32 %3, %16\n\t"
-        "ds_read_b32 %4, %17\n\tds_read_b32 %5, %18\n\tds_read_b32 %6, %19\n\tds_read_b32 %7, %20\n\t"
-        "ds_read_b32 %8, %21\n\tds_read_b32 %9, %22\n\t"
-        "ds_read_b128 %10, %23\n\tds_read_b128 %11, %24\n\tds_read_b128 %12, %25\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(dc[0]), "=&v"(dc[1]), "=&v"(dc[2]), "=&v"(dc[3]), "=&v"(dc[4]), "=&v"(dd[0]), "=&v"(dd[1]),
-          "=&v"(dd[2]), "=&v"(dd[3]), "=&v"(dd[4]), "=&v"(xv[0]), "=&v"(xv[1]), "=&v"(xv[2])
-        : "v"(ca + aoff[0]), "v"(ca + aoff[1]), "v"(ca + aoff[2]), "v"(ca + aoff[3]), "v"(ca + aoff[4]),
-          "v"(ca + 256 + aoff[0]), "v"(ca + 256 + aoff[1]), "v"(ca + 256 + aoff[2]), "v"(ca + 256 + aoff[3]),
-          "v"(ca + 256 + aoff[4]), "v"(sb + boff[0]), "v"(sb + boff[1]), "v"(sb + boff[2])
-        : "memory");
-    // windows: dword w = perm(hi = src[4 - w], lo = src[3 - w]) (src[i] = digit dword a4 - 4 + i)
-    mf_v4i Ac, Ad;
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-      Ac[w] = (int)__builtin_amdgcn_perm(dc[4 - w], dc[3 - w], sel[w]);
-      Ad[w] = (int)__builtin_amdgcn_perm(dd[4 - w], dd[3 - w], sel[w]);
+    if (t + MF_D - 1 < T) issue(t + MF_D - 1);
+    const uint32_t sb = ring_base + (t % MF_D) * RS * 16;
+    {  // this lane's correction (cd = h) rides in the unit's first step
+      const uint32_t ka = sb + (XE + 64 + 2 * wave + h) * 16;
+      uint4 kv;
+      asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(kv) : "v"(ka) : "memory");
+      if (ks == 0) corr = u4_to_f(kv);
     }
 #pragma unroll
-    for (int g = 0; g < NGR; g++) {
-      mf_v4i B;
-      B[0] = (int)(xv[g].x ^ 0x80808080u);
-      B[1] = (int)(xv[g].y ^ 0x80808080u);
-      B[2] = (int)(xv[g].z ^ 0x80808080u);
-      B[3] = (int)(xv[g].w ^ 0x80808080u);
-      acc[g][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ac, B, acc[g][0], 0, 0, 0);
-      acc[g][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ad, B, acc[g][1], 0, 0, 0);
-    }
-  }
-
-  // ---- fold: lane (slot l31, half h) holds rows a = (i & 3) + 8 (i >> 2) + 4 h of C[a][slot] in acc[.][i];
-  // G_m = sum_t C[4 m + t] 2^(8 t) (m = 2 (i >> 2) + h) at weight 2^(32 m). v_permlane32_swap(c, d) leaves
-  // every lane the G's of coefficient cd = h for both halves: r[0] = the h = 0 (even m) value, r[1] the odd.
-  const uint32_t cd = h;
-  const uint32_t lane_r = 8 * e8 + wave;
-  const uint64_t r0 = blk * 64 + lane_r;
-  const f128 corr = ld_il(b.coef, blk, NC, c.c_corr + cd, lane_r);
-  const f128 c288 = u4_to_f(b.consts[c.c_misc + MISC_2P288]);
-#pragma unroll
-  for (int g = 0; g < NGR; g++) {
-    int64_t G[8];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      int64_t gc = 0, gd = 0;
-#pragma unroll
-      for (int t = 0; t < 4; t++) {
-        gc += (int64_t)acc[g][0][4 * j + t] * (int64_t)(1u << (8 * t));
-        gd += (int64_t)acc[g][1][4 * j + t] * (int64_t)(1u << (8 * t));
+    for (uint32_t qp = 0; qp < KC / 2; qp++) {  // MFMA K-halves: calls 2 qp + h
+      // every LDS read of the pair and its wait in ONE asm statement: the outputs must not be consumed before
+      // the wait (the compiler cannot see the dependence of a separate waitcnt statement), and ordinary LDS
+      // loads would make it drain the outstanding LDS-DMA (vmcnt(0)) first
+      const uint32_t ca = sb + (XE + 8 * (2 * qp + h) + wave) * 16;  // coefficient entry, cd = 0 (cd = 1: + 8 KC)
+      const uint32_t cb = ca + 8 * KC * 16;
+      const uint32_t xb = sb + 2 * qp * SLOTS * 8 * 16;
+      uint32_t dc[5], dd[5];
+      uint4 xv[NGR];
+      if constexpr (NGR == 3) {
+        asm volatile(
+            "ds_read_b32 %0, %13\n\tds_read_b32 %1, %14\n\tds_read_b32 %2, %15\n\tds_read_b32 %3, %16\n\t"
+            "ds_read_b32 %4, %17\n\tds_read_b32 %5, %18\n\tds_read_b32 %6, %19\n\tds_read_b32 %7, %20\n\t"
+            "ds_read_b32 %8, %21\n\tds_read_b32 %9, %22\n\t"
+            "ds_read_b128 %10, %23\n\tds_read_b128 %11, %24\n\tds_read_b128 %12, %25\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(dc[0]), "=&v"(dc[1]), "=&v"(dc[2]), "=&v"(dc[3]), "=&v"(dc[4]), "=&v"(dd[0]), "=&v"(dd[1]),
+              "=&v"(dd[2]), "=&v"(dd[3]), "=&v"(dd[4]), "=&v"(xv[0]), "=&v"(xv[1]), "=&v"(xv[2])
+            : "v"(ca + aoff[0]), "v"(ca + aoff[1]), "v"(ca + aoff[2]), "v"(ca + aoff[3]), "v"(ca + aoff[4]),
+              "v"(cb + aoff[0]), "v"(cb + aoff[1]), "v"(cb + aoff[2]), "v"(cb + aoff[3]), "v"(cb + aoff[4]),
+              "v"(xb + boff[0]), "v"(xb + boff[1]), "v"(xb + boff[2])
+            : "memory");
+      } else {
+        static_assert(NGR == 2, "two or three slot groups");
+        asm volatile(
+            "ds_read_b32 %0, %12\n\tds_read_b32 %1, %13\n\tds_read_b32 %2, %14\n\tds_read_b32 %3, %15\n\t"
+            "ds_read_b32 %4, %16\n\tds_read_b32 %5, %17\n\tds_read_b32 %6, %18\n\tds_read_b32 %7, %19\n\t"
+            "ds_read_b32 %8, %20\n\tds_read_b32 %9, %21\n\t"
+            "ds_read_b128 %10, %22\n\tds_read_b128 %11, %23\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(dc[0]), "=&v"(dc[1]), "=&v"(dc[2]), "=&v"(dc[3]), "=&v"(dc[4]), "=&v"(dd[0]), "=&v"(dd[1]),
+              "=&v"(dd[2]), "=&v"(dd[3]), "=&v"(dd[4]), "=&v"(xv[0]), "=&v"(xv[1])
+            : "v"(ca + aoff[0]), "v"(ca + aoff[1]), "v"(ca + aoff[2]), "v"(ca + aoff[3]), "v"(ca + aoff[4]),
+              "v"(cb + aoff[0]), "v"(cb + aoff[1]), "v"(cb + aoff[2]), "v"(cb + aoff[3]), "v"(cb + aoff[4]),
+              "v"(xb + boff[0]), "v"(xb + boff[1])
+            : "memory");
       }
-      const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)gc, (uint32_t)gd, false, false);
-      const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)((uint64_t)gc >> 32), (uint32_t)((uint64_t)gd >> 32),
-                                                       false, false);
-      G[2 * j] = (int64_t)(((uint64_t)hi[0] << 32) | lo[0]);
-      G[2 * j + 1] = (int64_t)(((uint64_t)hi[1] << 32) | lo[1]);
-    }
-    // V = sum_m G_m 2^(32 m): 288-bit two's complement, then mod p
-    uint32_t L[9];
-    int64_t carry = 0;
+      // windows: dword w = perm(hi = src[4 - w], lo = src[3 - w]) (src[i] = digit dword a4 - 4 + i)
+      mf_v4i Ac, Ad;
 #pragma unroll
-    for (int m = 0; m < 8; m++) {
-      const int64_t t = G[m] + carry;
-      L[m] = (uint32_t)t;
-      carry = t >> 32;
-    }
-    L[8] = (uint32_t)carry;
-    f128 v = make128(0, 0);
-    v = reduce192(L[8], 0, 0);
+      for (int w = 0; w < 4; w++) {
+        Ac[w] = (int)__builtin_amdgcn_perm(dc[4 - w], dc[3 - w], sel[w]);
+        Ad[w] = (int)__builtin_amdgcn_perm(dd[4 - w], dd[3 - w], sel[w]);
+      }
 #pragma unroll
-    for (int i = 3; i >= 0; i--) v = reduce192((uint64_t)L[2 * i] | ((uint64_t)L[2 * i + 1] << 32), v.lo, v.hi);
-    if (carry < 0) v = sub128(v, c288);  // V = U - 2^288
-    v = add128(v, corr);
-    const uint32_t sl = s0 + 32 * g + l31;
-    if (sl < chunk && r0 < b.n) st_il(b.xs, blk, 2 * chunk, 2 * sl + cd, lane_r, v);
+      for (int g = 0; g < NGR; g++) {
+        mf_v4i B;
+        B[0] = (int)(xv[g].x ^ 0x80808080u);
+        B[1] = (int)(xv[g].y ^ 0x80808080u);
+        B[2] = (int)(xv[g].z ^ 0x80808080u);
+        B[3] = (int)(xv[g].w ^ 0x80808080u);
+        if (PROBE == 1) {  // timing probe: no matrix instructions (wrong sums)
+          acc[g][0][0] += Ac[0] ^ B[0];
+          acc[g][1][0] += Ad[1] ^ B[1];
+        } else {
+          acc[g][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ac, B, acc[g][0], 0, 0, 0);
+          acc[g][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ad, B, acc[g][1], 0, 0, 0);
+        }
+      }
+    }
+    if (++ks < KS) continue;
+    // ---- the unit's last step: fold. Lane (slot l31, half h) holds rows a = (i & 3) + 8 (i >> 2) + 4 h of
+    // C[a][slot] in acc[.][i]; G_m = sum_t C[4 m + t] 2^(8 t) (m = 2 (i >> 2) + h) at weight 2^(32 m).
+    // v_permlane32_swap(c, d) leaves every lane the G's of coefficient cd = h for both halves: r[0] = the
+    // h = 0 (even m) value, r[1] the odd one. Registers only: the ring keeps streaming the next unit.
+    const Unit fu = unit_of(j);
+    ks = 0;
+    j++;
+    if (fu.live) {
+      const uint32_t cd = h, lane_r = 8 * fu.e8 + wave;
+      const uint64_t r0 = fu.blk * 64 + lane_r;
+#pragma unroll
+      for (int g = 0; g < NGR; g++) {
+        int64_t Gm[8];
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+          int64_t gc = 0, gd = 0;
+#pragma unroll
+          for (int tt = 0; tt < 4; tt++) {
+            gc += (int64_t)acc[g][0][4 * jj + tt] * (int64_t)(1u << (8 * tt));
+            gd += (int64_t)acc[g][1][4 * jj + tt] * (int64_t)(1u << (8 * tt));
+          }
+          const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)gc, (uint32_t)gd, false, false);
+          const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)((uint64_t)gc >> 32),
+                                                           (uint32_t)((uint64_t)gd >> 32), false, false);
+          Gm[2 * jj] = (int64_t)(((uint64_t)hi[0] << 32) | lo[0]);
+          Gm[2 * jj + 1] = (int64_t)(((uint64_t)hi[1] << 32) | lo[1]);
+        }
+        // V = sum_m G_m 2^(32 m): 288-bit two's complement, then mod p
+        uint32_t L[9];
+        int64_t carry = 0;
+#pragma unroll
+        for (int m = 0; m < 8; m++) {
+          const int64_t tv = Gm[m] + carry;
+          L[m] = (uint32_t)tv;
+          carry = tv >> 32;
+        }
+        L[8] = (uint32_t)carry;
+        f128 v = reduce192(L[8], 0, 0);
+#pragma unroll
+        for (int i = 3; i >= 0; i--) v = reduce192((uint64_t)L[2 * i] | ((uint64_t)L[2 * i + 1] << 32), v.lo, v.hi);
+        if (carry < 0) v = sub128(v, c288);  // V = U - 2^288
+        v = add128(v, corr);
+        const uint32_t sl = fu.s0 + 32 * g + l31;
+        if (sl < chunk && r0 < b.n) st_il(b.xs, fu.blk, 2 * chunk, 2 * sl + cd, lane_r, v);
+      }
+    }
+    acc_zero();
   }
 }
 
@@ -3157,8 +3257,25 @@ static void launch_psum_part(const Cfg& c, const Bufs& b, hipStream_t s, uint32_
 // gadget 0 on the matrix cores (Cfg::mfma): the wire sums, then the per-group finish (no HIST)
 template <int PPW, bool LEADER>
 static void launch_psum_mfma(const Cfg& c, const Bufs& b, hipStream_t s, uint32_t grid) {
-  const uint32_t nb = nblk_of(b.n), nsc = (c.chunk + 32 * MF_NG - 1) / (32 * MF_NG);
-  hipLaunchKernelGGL(flp_psum_mfma_kernel<MF_NG>, dim3(((nb + 7) / 8) * 8 * 8 * nsc), dim3(64 * MF_WAVES), 0, s, c, b);
+  // persistent: one workgroup per CU (its LDS ring fills most of a CU), a multiple of 8 (XCDs)
+  static const uint32_t cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? (uint32_t)n : 256u;
+  }();
+  static const int probe = getenv("JX_MF_PROBE") ? atoi(getenv("JX_MF_PROBE")) : 0;  // experiment (temporary)
+  const uint32_t ng = probe == 2 ? 2 : MF_NG;
+  const uint32_t nb = nblk_of(b.n), nsc = (c.chunk + 32 * ng - 1) / (32 * ng);
+  const uint64_t units = (uint64_t)((nb + 7) / 8) * 8 * 8 * nsc;
+  const uint32_t wmax = ((cus + 7) / 8 * 8) * (probe == 2 ? 2 : 1);
+  const uint32_t mgrid = (uint32_t)(units < wmax ? units : wmax);
+  if (probe == 2)
+    hipLaunchKernelGGL((flp_psum_mfma_kernel<2, 3, 0, 2, 2>), dim3(mgrid), dim3(64 * MF_WAVES), 0, s, c, b);
+  else if (probe == 1)
+    hipLaunchKernelGGL((flp_psum_mfma_kernel<MF_NG, 3, 1>), dim3(mgrid), dim3(64 * MF_WAVES), 0, s, c, b);
+  else
+    hipLaunchKernelGGL((flp_psum_mfma_kernel<MF_NG, 3>), dim3(mgrid), dim3(64 * MF_WAVES), 0, s, c, b);
   hipLaunchKernelGGL((flp_psum_wires_kernel<PPW, LEADER>), dim3(grid), dim3(64), 0, s, c, b);
 }
 template <int PPW, bool HIST, bool LEADER>

@@ -4,6 +4,7 @@
 //   ring: K3's LDS-DMA ring structure (flp_psum_part_glds_kernel: 4-wave workgroups = 4 slot groups of a
 //         64-report block, 2 elements per wave per call, depth-4 ring, one barrier per call), XOR only;
 //   flat: plain global_load_dwordx4 sweep, 4 loads in flight per lane, grid-stride;
+//   slice_*: the MFMA K3's per-eighth stream (interleaved vs eighth-major staging, ring depth 4 / 6);
 // and prints one JSON line per kernel with the achieved GB/s. Tells whether K3 (8.4 ms per 250k reports)
 // is bound by its stream or by its VALU work.
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/bin/microbench_stream tools/microbench_stream.hip
@@ -77,6 +78,53 @@ __global__ __launch_bounds__(256, 4) void ring(const uint4* meas, const uint4* c
   out[(blk * NG + g) * 64 + lane] = acc;
 }
 
+
+// The MFMA K3's access pattern: a workgroup of 8 waves streams K-steps of 2 calls x 96 slots x 8 reports
+// (an eighth of a 64-report block; 24 KiB) through a depth-D LDS ring, one barrier per step. CONTIG = 0:
+// the interleaved staging (each row piece is the 128 B of 8 reports inside a 1 KiB element row);
+// CONTIG = 1: an eighth-major staging ([block][eighth][element][8 reports]: a step reads 2 x 12 KiB runs).
+template <int CONTIG, int DD>
+__global__ __launch_bounds__(512, 1) void slice(const uint4* meas, uint64_t nblk, uint4* out) {
+  constexpr uint32_t SL = 96, XE = 2 * SL * 8, NI = XE / 64 / 8;
+  __shared__ uint4 rb[DD][XE];
+  const uint32_t bid = blockIdx.x, xcd = bid & 7u, q8 = bid >> 3;
+  const uint64_t blk = (uint64_t)(q8 >> 3) * 8 + xcd;
+  if (blk >= nblk) return;
+  const uint32_t e8 = q8 & 7u, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t KS = (CALLS + 2) / 2;
+  auto src = [&](uint32_t ks, uint32_t i) {
+    const uint32_t p = 64 * (NI * wave + i) + lane, row = p >> 3, hh = row / SL, sl = row % SL;
+    const uint32_t r = (p & 7u) ^ ((sl >> 1) & 7u);
+    uint32_t e = (2 * ks + hh) * CHUNK + sl;
+    if (sl >= CHUNK || e >= M) e = 0;
+    if (CONTIG) return meas + ((blk * 8 + e8) * M + e) * 8 + r;
+    return meas + (blk * M + e) * 64 + 8 * e8 + r;
+  };
+  auto issue = [&](uint32_t ks) {
+    for (uint32_t i = 0; i < NI; i++)
+      __builtin_amdgcn_global_load_lds((const void*)src(ks, i), (void*)&rb[ks % DD][64 * (NI * wave + i)], 16, 0, 0);
+  };
+  for (uint32_t ks = 0; ks + 1 < DD; ks++) issue(ks);
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  const uint32_t base = lds_addr(&rb[0][0]);
+  for (uint32_t ks = 0; ks < KS; ks++) {
+    if (ks + DD - 2 >= KS)
+      wait_vmcnt<0>();
+    else
+      wait_vmcnt<(DD - 2) * NI>();
+    __builtin_amdgcn_s_barrier();
+    if (ks + DD - 1 < KS) issue(ks + DD - 1);
+    const uint32_t a = base + ((ks % DD) * XE + 64 * wave + lane) * 16;
+    uint4 v0;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(v0) : "v"(a) : "memory");
+    acc.x ^= v0.x;
+    acc.y ^= v0.y;
+    acc.z ^= v0.z;
+    acc.w ^= v0.w;
+  }
+  out[(uint64_t)bid * 512 + threadIdx.x] = acc;
+}
+
 __global__ __launch_bounds__(256) void flat(const uint4* p, uint64_t n16, uint4* out) {
   const uint64_t tid = (uint64_t)blockIdx.x * 256 + threadIdx.x, nt = (uint64_t)gridDim.x * 256;
   uint4 acc = make_uint4(0, 0, 0, 0);
@@ -112,14 +160,25 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CHK(hipEventCreate(&e0));
   CHK(hipEventCreate(&e1));
-  for (int kern = 0; kern < 2; kern++) {
+  const uint64_t slice_grid = ((nblk + 7) / 8) * 8 * 8;
+  uint4* out2;
+  CHK(hipMalloc(&out2, slice_grid * 512 * 16));
+  for (int kern = 0; kern < 6; kern++) {
     float best = 1e30f;
     for (int rep = 0; rep < 4; rep++) {
       CHK(hipEventRecord(e0, 0));
       if (kern == 0)
         hipLaunchKernelGGL(ring, dim3(ring_grid), dim3(256), 0, 0, meas, coef, nblk, out);
-      else
+      else if (kern == 1)
         hipLaunchKernelGGL(flat, dim3(flat_grid), dim3(256), 0, 0, meas, n16, out);
+      else if (kern == 2)
+        hipLaunchKernelGGL((slice<0, 4>), dim3(slice_grid), dim3(512), 0, 0, meas, nblk, out2);
+      else if (kern == 3)
+        hipLaunchKernelGGL((slice<1, 4>), dim3(slice_grid), dim3(512), 0, 0, meas, nblk, out2);
+      else if (kern == 4)
+        hipLaunchKernelGGL((slice<0, 6>), dim3(slice_grid), dim3(512), 0, 0, meas, nblk, out2);
+      else
+        hipLaunchKernelGGL((slice<1, 6>), dim3(slice_grid), dim3(512), 0, 0, meas, nblk, out2);
       CHK(hipEventRecord(e1, 0));
       CHK(hipEventSynchronize(e1));
       float ms;
@@ -127,7 +186,9 @@ int main(int argc, char** argv) {
       if (rep > 0 && ms < best) best = ms;
     }
     printf("{\"kernel\": \"%s\", \"reports\": %llu, \"bytes\": %.0f, \"ms\": %.3f, \"GBps\": %.1f}\n",
-           kern == 0 ? "ring" : "flat", (unsigned long long)nrep, bytes, best, bytes / (best * 1e6));
+           kern == 0 ? "ring" : kern == 1 ? "flat" : kern == 2 ? "slice_il_d4" : kern == 3 ? "slice_contig_d4"
+                                  : kern == 4 ? "slice_il_d6" : "slice_contig_d6",
+           (unsigned long long)nrep, bytes, best, bytes / (best * 1e6));
     fflush(stdout);
   }
   return 0;
