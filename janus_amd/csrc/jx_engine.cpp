@@ -82,7 +82,6 @@ struct jx_engine {
   uint4 *d_meas = nullptr, *d_proof = nullptr, *d_outs = nullptr, *d_coef = nullptr, *d_consts = nullptr;
   uint32_t* d_flags = nullptr;
   uint4* d_part = nullptr;
-  uint4* d_xs = nullptr;  // MFMA path: gadget 0's wire sums (Bufs::xs)
   uint8_t *d_verdicts = nullptr, *d_msgs = nullptr;  // the fused paths' per-launch results
   // accumulation scratch: partials + selection bytes
   uint64_t* d_partials = nullptr;
@@ -349,15 +348,6 @@ static int32_t make_cfg(const jx_prio3_params* p, const uint8_t* vk, uint32_t vk
     c.c_tpow = c.ncoef;
     c.ncoef += c.ngroups;
   }
-  // gadget 0's wire sums on the matrix cores (flp_psum_mfma_kernel) for SumVec and FixedPoint. Histogram
-  // (its range check also needs sum x) keeps the VALU ring. int32 MFMA sums stay exact for up to 4096
-  // calls (2048 K-steps of 2 calls). JX_K3_MFMA=0 selects the VALU ring (A/B measurements, parity tests).
-  const char* mf_env = getenv("JX_K3_MFMA");
-  if ((c.algo == ALGO_SUMVEC || fp) && c.calls <= 4096 && !(mf_env && atoi(mf_env) == 0)) {
-    c.mfma = 1;
-    c.c_corr = c.ncoef;
-    c.ncoef += 2;
-  }
   if (fp) {
     c.coef1 = c.ncoef;
     c.ncoef += G1_K + c.calls1;
@@ -431,9 +421,6 @@ static std::vector<uint4> make_consts(const Cfg& c) {
   t[c.c_misc + 1] = h_u4(from_mont128(half_m));     // 1/2 canonical
   t[c.c_misc + 2] = h_u4(make128(R1_128_LO, R1_128_HI));
   t[c.c_misc + 3] = h_u4(half_m);                   // (1/2) R
-  t[c.c_misc + MISC_J128R] = h_u4(to_mont128(make128(0x8080808080808080ull, 0x8080808080808080ull)));  // (128 J) R
-  // 2^288 = 2^256 2^32: mont(2^256 mod p, 2^32 R) (R2_128 = 2^256 mod p)
-  t[c.c_misc + MISC_2P288] = h_u4(mont128(make128(R2_128_LO, R2_128_HI), to_mont128(make128(1ull << 32, 0))));
   if (c.algo == ALGO_FIXEDPOINT_L2) {
     const uint32_t n = c.bits;
     t[c.c_misc + 4] = h_u4(make128(n < 64 ? 1ull << n : 0, n >= 64 ? 1ull << (n - 64) : 0));  // 2^n
@@ -451,14 +438,13 @@ static std::vector<uint4> make_consts(const Cfg& c) {
 static void free_staging(jx_engine* e) {
   void* ptrs[] = {e->d_nonces, e->d_ps,       e->d_his,     e->d_lps,  e->d_meas, e->d_proof, e->d_outs,
                   e->d_coef,   e->d_flags,    e->d_verdicts, e->d_msgs, e->d_partials, e->d_mask, e->d_seg,
-                  e->d_part,   e->d_xs};
+                  e->d_part};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   e->d_nonces = e->d_ps = e->d_his = e->d_lps = nullptr;
   e->d_meas = e->d_proof = e->d_outs = e->d_coef = nullptr;
   e->d_flags = nullptr;
   e->d_part = nullptr;
-  e->d_xs = nullptr;
   e->d_verdicts = e->d_msgs = nullptr;
   e->d_partials = nullptr;
   e->d_mask = nullptr;
@@ -491,7 +477,6 @@ static uint64_t per_report_bytes(const Cfg& c, bool with_meas = true) {
   b += 16ull * (c.out_is_meas ? 0 : c.out_len);
   b += 16 + c.ps_bytes + c.his_bytes + c.lps_bytes + 4 + 1 + c.seed + 1 + 4 + 1;
   b += part_bytes(c);  // FLP partial sums
-  if (c.mfma) b += 32ull * c.chunk;  // MFMA wire sums
   return b;
 }
 
@@ -532,7 +517,6 @@ static int32_t ensure_capacity(jx_engine* e, uint64_t n, bool need_meas = true) 
   HIPCHK(e, A((void**)&e->d_coef, cap * coef_elems(c) * eb));
   HIPCHK(e, A((void**)&e->d_flags, cap * 4));
   HIPCHK(e, A((void**)&e->d_part, cap * part_bytes(c)));
-  if (c.mfma) HIPCHK(e, A((void**)&e->d_xs, cap * 32ull * c.chunk));
   HIPCHK(e, A((void**)&e->d_verdicts, cap));
   HIPCHK(e, A((void**)&e->d_msgs, cap * c.seed));
   HIPCHK(e, A((void**)&e->d_mask, cap));
@@ -702,7 +686,6 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
   b.coef = e->d_coef;
   b.flags = e->d_flags;
   b.part = e->d_part;
-  b.xs = e->d_xs;
   b.verdicts = verdicts;
   b.msgs = msgs;
   b.consts = e->d_consts;

@@ -66,10 +66,6 @@ struct Cfg {
   // the FLP group finish needs no exponentiation: c_rpow + j = r^(j+1) canonical (j < chunk), c_tpow + g
   // = t^(g * per) R, per = ceil(gpoly_len / ngroups) (the group's first gadget-polynomial coefficient)
   uint32_t c_rpow, c_tpow;
-  // gadget 0's wire sums on the matrix cores (flp_psum_mfma_kernel; SumVec, FixedPoint): K1 stores c_k and
-  // d_k as signed base-256 digits (mf_digits) instead of Montgomery values, plus the two correction terms
-  // 128 J sum_k c_k R, 128 J sum_k d_k R at coefficient slots c_corr, c_corr + 1
-  uint32_t mfma, c_corr;
 };
 
 // coefficient slots (Montgomery form unless noted) for the ParallelSum / Sum FLP
@@ -92,9 +88,8 @@ enum : uint32_t {
 // misc constants (uint4 slots at Cfg::c_misc): 0 (1/P)R, 1 1/2, 2 R, 3 (1/2)R; FixedPoint: 4 2^n,
 // 5 2^(2n-2) R^-1, 6 2^(n-2) (gadget-1 padding, a share of the encoded 0.0), 7 (1/P1)R; 8 zero (the
 // source of the FLP ring's loads for measurement elements past the share and for padded slots)
-// 9 (128 J) R (J = 0x0101..01, 16 bytes: the digit bias of the MFMA wire sums), 10 2^288 mod p
-constexpr uint32_t NMISC = 11;
-constexpr uint32_t MISC_ZERO = 8, MISC_J128R = 9, MISC_2P288 = 10;
+constexpr uint32_t NMISC = 9;
+constexpr uint32_t MISC_ZERO = 8;
 
 struct Bufs {
   uint64_t n;  // reports in this launch
@@ -114,7 +109,6 @@ struct Bufs {
   uint4* proof;
   uint4* outs;
   uint4* coef;
-  uint4* xs;  // MFMA path: gadget 0's R-scaled wire sums [blk][2 * slot + (0: c, 1: d)][lane], canonical
   uint32_t* flags;
   uint4* part;  // ParallelSum FLP partial sums [blk][group][4][lane] (multiproof: uint2 [blk][proof][group][3][lane])
   uint8_t* verdicts;

@@ -36,26 +36,6 @@ __device__ __forceinline__ uint4 f_to_u4(f128 a) { return make_uint4(lo32(a.lo),
 __device__ __forceinline__ f128 w4_to_f(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   return make128((uint64_t)a | ((uint64_t)b << 32), (uint64_t)c | ((uint64_t)d << 32));
 }
-// Signed base-256 digits of a field element v < p, the coefficient operand of the MFMA wire sums
-// (flp_psum_mfma_kernel): s = v if v <= 127 J, else v - p (J = 0x0101..01, 16 bytes), so |s| < 2^127 and
-// s == v (mod p); u = s + 128 J lies in [0, 2^128); the int8 digits d_i = byte_i(u) - 128, stored as
-// byte_i(u) XOR 0x80, satisfy sum_i d_i 256^i = s. (Host check: tests/test_mfma_k3_math.py.)
-__device__ __forceinline__ uint4 mf_digits(f128 v) {
-  constexpr uint64_t J127 = 0x7F7F7F7F7F7F7F7Full, J128 = 0x8080808080808080ull;
-  const bool neg = v.hi > J127 || (v.hi == J127 && v.lo > J127);
-  uint64_t lo = v.lo, hi = v.hi;
-  uint32_t c = 0;
-  if (neg) {  // + (2^128 - p) = 27 * 2^64 + (2^64 - 1)
-    lo = addc64(lo, ~0ull, c);
-    hi = hi + 27u + c;
-    c = 0;
-  }
-  lo = addc64(lo, J128, c);
-  hi = hi + J128 + c;
-  lo ^= J128;
-  hi ^= J128;
-  return make_uint4(lo32(lo), hi32(lo), lo32(hi), hi32(hi));
-}
 // interleaved staging address
 __device__ __forceinline__ uint64_t il_idx(uint64_t blk, uint32_t len, uint32_t e, uint32_t lane) {
   return (blk * len + e) * IL + lane;
@@ -504,25 +484,11 @@ __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t
     // d_k = c_k * r^{(k-1)*chunk}
     f128 rc = mpow(rR, c.chunk);
     f128 rp = R1;
-    f128 sc = make128(0, 0), sd = make128(0, 0);
     for (uint32_t k = 1; k <= C; k++) {
       const uint32_t sk = COEF_K + 2 * (k - 1);
       f128 ck = ld_il(coef, blk, NC, sk, lane);
-      const f128 dk = mont128(ck, rp);
-      if (c.mfma) {  // the matrix-core wire sums read signed digits (and the digit-bias corrections)
-        st_il(coef, blk, NC, sk, lane, u4_to_f(mf_digits(ck)));
-        st_il(coef, blk, NC, sk + 1, lane, u4_to_f(mf_digits(dk)));
-        sc = add128(sc, ck);
-        sd = add128(sd, dk);
-      } else {
-        st_il(coef, blk, NC, sk + 1, lane, dk);
-      }
+      st_il(coef, blk, NC, sk + 1, lane, mont128(ck, rp));
       rp = mont128(rp, rc);
-    }
-    if (c.mfma) {  // 128 J sum_k c_k R and 128 J sum_k d_k R (plain products: mont(x, (128 J) R))
-      const f128 j128R = u4_to_f(b.consts[c.c_misc + MISC_J128R]);
-      st_il(coef, blk, NC, c.c_corr, lane, mont128(sc, j128R));
-      st_il(coef, blk, NC, c.c_corr + 1, lane, mont128(sd, j128R));
     }
     // power tables of the ParallelSum group finish (psum_part_finish): r^(j+1) canonical for the even
     // wires of slot j (a chain of mont products starting from the canonical r), and t^(g * per) R for
@@ -1825,12 +1791,16 @@ __global__ __launch_bounds__(256) void flp_sum_kernel(Cfg c, Bufs b) {
   if (r0 < b.n) b.verdicts[r0] = (uint8_t)verdict;
 }
 
-// The register-prefetch part kernel's calls kf+1..C (the ragged last call, or every call of a padded
-// group) with guarded direct loads.
-template <int PPW, bool HIST>
-__device__ __forceinline__ void psum_tail_calls(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t g, uint32_t lane,
-                                                uint32_t kf, wacc26* ae, wacc26* ao, acc192& sx) {
-  const uint32_t NC = c.ncoef, C = c.calls, chunk = c.chunk, M = c.meas_len;
+// The part kernels' common end: the calls kf+1..C (the ragged last call, or every call of a padded
+// group) with guarded direct loads, then the wires at t, the leader's verifier share and the gadget
+// polynomial's share of v and G(t) for group g of block blk.
+template <int PPW, bool HIST, bool LEADER>
+__device__ __forceinline__ void psum_part_finish(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t g, uint32_t lane,
+                                                 uint32_t kf, wacc26* ae, wacc26* ao, acc192& sx) {
+  const uint32_t NG = c.ngroups;
+  const uint64_t r0 = blk * 64 + lane;
+  const uint64_t r = r0 < b.n ? r0 : b.n - 1;
+  const uint32_t NC = c.ncoef, C = c.calls, chunk = c.chunk, M = c.meas_len, A = 2 * chunk;
   const uint32_t j0 = g * PPW;
   const uint4* coefb = b.coef + il_idx(blk, NC, 0, lane);
   const MeasView measb = meas_view(c, b, blk, lane);
@@ -1857,20 +1827,6 @@ __device__ __forceinline__ void psum_tail_calls(const Cfg& c, const Bufs& b, uin
       }
     }
   }
-}
-
-// The part kernels' common end for group g of block blk: the wires at t of the group's slots from the
-// R-scaled wire sums xe[i] = sum_k d_k R x_{k,i}, xo[i] = sum_k c_k R x_{k,i} (mod p, canonical), the
-// leader's verifier share, and the gadget polynomial's share of v and G(t). sxr: (Histogram) sum of x.
-template <int PPW, bool HIST, bool LEADER>
-__device__ __forceinline__ void psum_part_finish(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t g, uint32_t lane,
-                                                 const f128* xe, const f128* xo, f128 sxr) {
-  const uint32_t NG = c.ngroups;
-  const uint64_t r0 = blk * 64 + lane;
-  const uint64_t r = r0 < b.n ? r0 : b.n - 1;
-  const uint32_t NC = c.ncoef, chunk = c.chunk, A = 2 * chunk;
-  const uint32_t j0 = g * PPW;
-  const uint4* coefb = b.coef + il_idx(blk, NC, 0, lane);
   // ---- wires at t for this group's slots, plus the leader's verifier share
   const f128 LR = u4_to_f(coefb[COEF_L * IL]), c0R = u4_to_f(coefb[COEF_C0 * IL]);
   const f128 hs = u4_to_f(coefb[COEF_HALFSUM * IL]);
@@ -1885,7 +1841,7 @@ __device__ __forceinline__ void psum_part_finish(const Cfg& c, const Bufs& b, ui
       // the sums are R-scaled (c_k, d_k are stored in Montgomery form): mont(sum, r^(j+1)) with the
       // canonical table power is E r^(j+1), and O = mont(sum, 1) (canonical)
       const f128 rpow = u4_to_f(coefb[(c.c_rpow + j) * IL]);
-      f128 Er = mont128(xe[i], rpow), O = mont128(xo[i], make128(1, 0));
+      f128 Er = mont128(wacc_reduce(ae[i]), rpow), O = mont128(wacc_reduce(ao[i]), make128(1, 0));
       f128 We = mont128(add128(mont128(se, c0R), Er), LR);
       f128 Wo = mont128(sub128(add128(mont128(so, c0R), O), hs), LR);
       if (LEADER) {  // the leader's verifier share: wire values at t
@@ -1920,7 +1876,7 @@ __device__ __forceinline__ void psum_part_finish(const Cfg& c, const Bufs& b, ui
   pp[0] = f_to_u4(prod);
   pp[IL] = f_to_u4(vpart);
   pp[2 * IL] = f_to_u4(gpart);
-  if (HIST) pp[3 * IL] = f_to_u4(sxr);
+  if (HIST) pp[3 * IL] = f_to_u4(acc_reduce(sx));
   if (dfail && r0 < b.n) atomicOr(&b.flags[r0], FLAG_DFAIL);
 }
 
@@ -2016,14 +1972,7 @@ __global__ __launch_bounds__(64, 4) void flp_psum_part_kernel(Cfg c, Bufs b) {
       wacc_normalize(ao[i]);
     }
   }
-  psum_tail_calls<PPW, HIST>(c, b, blk, g, lane, kf, ae, ao, sx);
-  f128 xe[PPW], xo[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; i++) {
-    xe[i] = wacc_reduce(ae[i]);
-    xo[i] = wacc_reduce(ao[i]);
-  }
-  psum_part_finish<PPW, HIST, LEADER>(c, b, blk, g, lane, xe, xo, HIST ? acc_reduce(sx) : make128(0, 0));
+  psum_part_finish<PPW, HIST, LEADER>(c, b, blk, g, lane, kf, ae, ao, sx);
 }
 
 // s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt left unconstrained)
@@ -2150,335 +2099,7 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
     }
   }
   if (g >= NG) return;
-  f128 xe[PPW], xo[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; i++) {
-    xe[i] = wacc_reduce(ae[i]);
-    xo[i] = wacc_reduce(ao[i]);
-  }
-  psum_part_finish<PPW, HIST, LEADER>(c, b, blk, g, lane, xe, xo, HIST ? acc_reduce(sx) : make128(0, 0));
-}
-
-// ---------------------------------------------------------------------------- K3 on the matrix cores
-// Gadget 0's wire sums  xo_s = sum_k c_k R x_{k,s},  xe_s = sum_k d_k R x_{k,s}  (SumVec, FixedPoint) as one
-// int8 GEMM per report and 32-slot group on v_mfma_i32_32x32x32_i8:
-//  * B (K x N): column s = slot, K index 16 h + j = byte j of the element x_{call h, s} (two calls per
-//    instruction), XOR 0x80 -- the int8 digits of x - 128 J (J = 0x0101..01). A lane's operand is one
-//    staged element, read from LDS as is;
-//  * A (M x K): A[a][16 h + j] = d_{a-j}(v_h) for the digits d_i of the coefficient v_h = c or d of call h
-//    (mf_digits: sum_i d_i 256^i == v (mod p)), zero outside 0..15 -- a Toeplitz window of the digits,
-//    4 v_perm_b32 with per-lane selectors;
-//  * C[a][s] = sum over calls and j of d_{a-j} x_j: the byte-position-a part of sum_k s_k (x_{k,s} - 128 J),
-//    so x_s = sum_a C[a][s] 256^a + 128 J sum_k v_k (mod p), the correction K1 stores.
-// A workgroup = 8 waves = 8 reports (one eighth of a 64-report block) x one chunk of MF_NG x 32 slots, each
-// wave one report; per K-step (2 calls) the staged elements of the 8 reports stream into
-// an LDS ring by LDS-DMA, one s_barrier per step. The accumulators fold to a 288-bit signed sum per (slot,
-// coefficient): 4-row groups to 64-bit columns, v_permlane32_swap gathers a slot's 8 columns in one lane
-// (c in lanes 0..31, d in 32..63), then a reduction mod p; the sums go to Bufs::xs and the wires kernel.
-constexpr uint32_t MF_WAVES = 8, MF_NG = 3, MF_KC = 4;  // waves (reports), 32-slot groups, calls per K-step
-typedef int mf_v4i __attribute__((ext_vector_type(4)));
-typedef int mf_v16i __attribute__((ext_vector_type(16)));
-
-// lane-fixed byte selectors of the coefficient window: row a, output dword w holds digits a-4w-t (t = 0..3)
-// from the two source dwords lo = floor(a/4) - w - 1 (bytes 0..3) and hi = lo + 1 (bytes 4..7)
-__device__ __forceinline__ uint32_t mf_sel(uint32_t a, uint32_t w) {
-  uint32_t sel = 0;
-  const int base = 4 * ((int)(a >> 2) - (int)w - 1);
-#pragma unroll
-  for (int t = 0; t < 4; t++) {
-    const int pos = (int)a - 4 * (int)w - t;
-    const uint32_t bsel = (pos >= 0 && pos <= 15) ? (uint32_t)(pos - base) : 0x0cu;
-    sel |= bsel << (8 * t);
-  }
-  return sel;
-}
-// clamp a coefficient dword index into 0..3 (a clamped dword's bytes are never selected)
-__device__ __forceinline__ uint32_t mf_dw(int i) { return (uint32_t)(i < 0 ? 0 : (i > 3 ? 3 : i)); }
-
-template <int NGR, uint32_t MF_D, int PROBE = 0, uint32_t KC = MF_KC, int WGS = 1>
-__global__ __launch_bounds__(64 * MF_WAVES, 2 * WGS) void flp_psum_mfma_kernel(Cfg c, Bufs b) {
-  constexpr uint32_t SLOTS = 32 * NGR;
-  constexpr uint32_t XE = KC * SLOTS * 8;  // x entries (16 B) per ring slot: [call][slot][report]
-  constexpr uint32_t RS = XE + 128;        // + coefficient entries [cd][call][report], then [report][cd] corrections
-  constexpr uint32_t NDMA = XE / 64;      // x DMA instructions per K-step
-  constexpr uint32_t NI = (NDMA + MF_WAVES - 1) / MF_WAVES;  // x DMA instructions per wave (at most)
-  static_assert(NDMA % MF_WAVES == 0, "every wave issues NI x instructions");
-  __shared__ uint4 ring[MF_D * RS];
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
-  const uint32_t C = c.calls, chunk = c.chunk, M = c.meas_len, NC = c.ncoef;
-  const uint32_t KS = (C + KC - 1) / KC;
-  const uint32_t NSC = (chunk + SLOTS - 1) / SLOTS;  // slot chunks
-  const uint64_t nblk = (b.n + 63) / 64;
-  // units (64-report block, eighth, slot chunk), numbered so that unit u runs on XCD u % 8 with the other
-  // units of its block: u = (blk / 8) * 64 NSC + (e8 * NSC + sc) * 8 + blk % 8. This persistent workgroup
-  // takes units blockIdx.x, + gridDim.x, ... (gridDim.x is a multiple of 8) and streams their K-steps
-  // back to back through one ring, so a unit's first steps load under the previous unit's last ones.
-  const uint32_t G = gridDim.x;
-  const uint64_t NU = (nblk + 7) / 8 * 8 * 8 * NSC;
-  const uint64_t nj = blockIdx.x < NU ? (NU - blockIdx.x + G - 1) / G : 0;
-  const uint32_t T = (uint32_t)(nj * KS);  // K-steps of this workgroup
-  const uint4* zero = b.consts + c.c_misc + MISC_ZERO;
-  struct Unit {
-    uint64_t blk;
-    uint32_t e8, s0;
-    bool live;
-  };
-  auto unit_of = [&](uint64_t j) {
-    const uint64_t u = blockIdx.x + j * G;
-    const uint64_t q = u >> 3, per = 8ull * NSC;
-    Unit un;
-    un.blk = (q / per) * 8 + (u & 7);
-    const uint32_t w = (uint32_t)(q % per);
-    un.e8 = w / NSC;
-    un.s0 = (w % NSC) * SLOTS;
-    un.live = un.blk < nblk;
-    return un;
-  };
-  // this lane's x entries: instruction i writes entry p = 64 (NI wave + i) + lane; row = p >> 3 =
-  // call * SLOTS + slot, report (p & 7) ^ ((slot >> 1) & 7) (swizzled: a wave's ds_read_b128 of 16 slots
-  // touches 16 distinct bank quads)
-  uint32_t x_hh[NI], x_sl[NI], x_r[NI];
-#pragma unroll
-  for (uint32_t i = 0; i < NI; i++) {
-    const uint32_t p = 64 * (NI * wave + i) + lane, row = p >> 3;
-    x_hh[i] = row / SLOTS;
-    x_sl[i] = row % SLOTS;
-    x_r[i] = (p & 7u) ^ ((x_sl[i] >> 1) & 7u);
-  }
-  // the last wave streams the coefficient digits (entry 8 KC cd + 8 call + r, one instruction) and, with a
-  // unit's first step, the 8 reports' two bias corrections (entry 8 KC 2 + 2 r + cd, lanes 0..15 of a second
-  // one): read back from LDS they cost the fold no global load, whose wait would drain the whole ring
-  // (vmcnt counts in order)
-  static_assert(2 * KC * 8 <= 64, "one coefficient DMA instruction per step");
-  const bool coef_lane = wave == MF_WAVES - 1;
-  const uint32_t c_r = lane & 7, c_hh = (lane >> 3) & (KC - 1), c_cd = lane / (8 * KC);  // c_cd > 1: unused lane
-  const uint32_t k_r = lane >> 1, k_cd = lane & 1;
-  // the issue cursor (unit j, step ks) advances one K-step per call; per-unit lane state is set up once
-  const uint4* x_base[NI];
-  uint32_t x_e0[NI];
-  bool x_ok[NI];
-  uint64_t x_es = 0;
-  const uint4* c_base = zero;
-  const uint4* k_src = zero;
-  bool i_live = false;
-  uint64_t ij = 0;
-  uint32_t iks = 0;
-  auto issue_unit = [&]() {
-    const Unit un = unit_of(ij);
-    i_live = un.live;
-#pragma unroll
-    for (uint32_t i = 0; i < NI; i++) {
-      const MeasView mv = meas_view(c, b, un.live ? un.blk : 0, 8 * un.e8 + x_r[i]);
-      x_base[i] = mv.p;
-      x_es = mv.es;
-      const uint32_t sl = un.s0 + x_sl[i];
-      x_ok[i] = un.live && sl < chunk;
-      x_e0[i] = x_hh[i] * chunk + sl;
-    }
-    c_base = b.coef + il_idx(un.live ? un.blk : 0, NC, COEF_K + (c_cd & 1), 8 * un.e8 + c_r);
-    k_src = un.live && lane < 16 ? b.coef + il_idx(un.blk, NC, c.c_corr + k_cd, 8 * un.e8 + k_r) : zero;
-  };
-  auto issue = [&](uint32_t t) {  // step t of this workgroup = the cursor's (ij, iks)
-    if (iks == 0) issue_unit();
-    uint4* rs = ring + (t % MF_D) * RS;
-    const uint32_t de = KC * iks * chunk;
-#pragma unroll
-    for (uint32_t i = 0; i < NI; i++) {
-      const uint32_t e = x_e0[i] + de;  // e < M implies call <= C
-      glds16(x_ok[i] && e < M ? x_base[i] + (uint64_t)e * x_es : zero, rs + 64 * (NI * wave + i));
-    }
-    if (coef_lane) {
-      const uint32_t k = KC * iks + c_hh + 1;
-      glds16(i_live && c_cd < 2 && k <= C ? c_base + (uint64_t)(2 * (k - 1)) * IL : zero, rs + XE);
-      glds16(iks == 0 ? k_src : zero, rs + XE + 64);
-    }
-    if (++iks == KS) {
-      iks = 0;
-      ij++;
-    }
-  };
-
-  // per-lane constants of the coefficient window (row a = l31) and the element reads
-  uint32_t sel[4];
-#pragma unroll
-  for (int w = 0; w < 4; w++) sel[w] = mf_sel(l31, w);
-  const int a4 = (int)(l31 >> 2);
-  uint32_t aoff[5];
-#pragma unroll
-  for (int i = 0; i < 5; i++) aoff[i] = 4 * mf_dw(a4 - 4 + i);
-  uint32_t boff[NGR];  // element (call h of the pair, slot 32 g + l31) of report `wave`
-#pragma unroll
-  for (int g = 0; g < NGR; g++) {
-    const uint32_t sl = 32 * g + l31;
-    boff[g] = 16 * ((h * SLOTS + sl) * 8 + (wave ^ ((sl >> 1) & 7u)));
-  }
-  const uint32_t ring_base = lds_addr(ring);
-  const f128 c288 = u4_to_f(b.consts[c.c_misc + MISC_2P288]);
-
-  mf_v16i acc[NGR][2];
-  auto acc_zero = [&]() {
-#pragma unroll
-    for (int g = 0; g < NGR; g++)
-#pragma unroll
-      for (int cd = 0; cd < 2; cd++)
-#pragma unroll
-        for (int i = 0; i < 16; i++) acc[g][cd][i] = 0;
-  };
-  acc_zero();
-  f128 corr = make128(0, 0);
-  for (uint32_t t = 0; t + 1 < MF_D && t < T; t++) issue(t);
-  uint64_t j = 0;
-  uint32_t ks = 0;
-#pragma unroll 1
-  for (uint32_t t = 0; t < T; t++) {
-    // this wave's loads of step t have landed once at most the next MF_D - 2 steps' are outstanding
-    if (t + MF_D - 2 >= T) {
-      wait_vmcnt<0>();
-    } else if (coef_lane) {
-      wait_vmcnt<(MF_D - 2) * (NI + 2)>();
-    } else {
-      wait_vmcnt<(MF_D - 2) * NI>();
-    }
-    __builtin_amdgcn_s_barrier();
-    if (t + MF_D - 1 < T) issue(t + MF_D - 1);
-    const uint32_t sb = ring_base + (t % MF_D) * RS * 16;
-    {  // this lane's correction (cd = h) rides in the unit's first step
-      const uint32_t ka = sb + (XE + 64 + 2 * wave + h) * 16;
-      uint4 kv;
-      asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(kv) : "v"(ka) : "memory");
-      if (ks == 0) corr = u4_to_f(kv);
-    }
-#pragma unroll
-    for (uint32_t qp = 0; qp < KC / 2; qp++) {  // MFMA K-halves: calls 2 qp + h
-      // every LDS read of the pair and its wait in ONE asm statement: the outputs must not be consumed before
-      // the wait (the compiler cannot see the dependence of a separate waitcnt statement), and ordinary LDS
-      // loads would make it drain the outstanding LDS-DMA (vmcnt(0)) first
-      const uint32_t ca = sb + (XE + 8 * (2 * qp + h) + wave) * 16;  // coefficient entry, cd = 0 (cd = 1: + 8 KC)
-      const uint32_t cb = ca + 8 * KC * 16;
-      const uint32_t xb = sb + 2 * qp * SLOTS * 8 * 16;
-      uint32_t dc[5], dd[5];
-      uint4 xv[NGR];
-      if constexpr (NGR == 3) {
-        asm volatile(
-            "ds_read_b32 %0, %13\n\tds_read_b32 %1, %14\n\tds_read_b32 %2, %15\n\tds_read_b32 %3, %16\n\t"
-            "ds_read_b32 %4, %17\n\tds_read_b32 %5, %18\n\tds_read_b32 %6, %19\n\tds_read_b32 %7, %20\n\t"
-            "ds_read_b32 %8, %21\n\tds_read_b32 %9, %22\n\t"
-            "ds_read_b128 %10, %23\n\tds_read_b128 %11, %24\n\tds_read_b128 %12, %25\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(dc[0]), "=&v"(dc[1]), "=&v"(dc[2]), "=&v"(dc[3]), "=&v"(dc[4]), "=&v"(dd[0]), "=&v"(dd[1]),
-              "=&v"(dd[2]), "=&v"(dd[3]), "=&v"(dd[4]), "=&v"(xv[0]), "=&v"(xv[1]), "=&v"(xv[2])
-            : "v"(ca + aoff[0]), "v"(ca + aoff[1]), "v"(ca + aoff[2]), "v"(ca + aoff[3]), "v"(ca + aoff[4]),
-              "v"(cb + aoff[0]), "v"(cb + aoff[1]), "v"(cb + aoff[2]), "v"(cb + aoff[3]), "v"(cb + aoff[4]),
-              "v"(xb + boff[0]), "v"(xb + boff[1]), "v"(xb + boff[2])
-            : "memory");
-      } else {
-        static_assert(NGR == 2, "two or three slot groups");
-        asm volatile(
-            "ds_read_b32 %0, %12\n\tds_read_b32 %1, %13\n\tds_read_b32 %2, %14\n\tds_read_b32 %3, %15\n\t"
-            "ds_read_b32 %4, %16\n\tds_read_b32 %5, %17\n\tds_read_b32 %6, %18\n\tds_read_b32 %7, %19\n\t"
-            "ds_read_b32 %8, %20\n\tds_read_b32 %9, %21\n\t"
-            "ds_read_b128 %10, %22\n\tds_read_b128 %11, %23\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(dc[0]), "=&v"(dc[1]), "=&v"(dc[2]), "=&v"(dc[3]), "=&v"(dc[4]), "=&v"(dd[0]), "=&v"(dd[1]),
-              "=&v"(dd[2]), "=&v"(dd[3]), "=&v"(dd[4]), "=&v"(xv[0]), "=&v"(xv[1])
-            : "v"(ca + aoff[0]), "v"(ca + aoff[1]), "v"(ca + aoff[2]), "v"(ca + aoff[3]), "v"(ca + aoff[4]),
-              "v"(cb + aoff[0]), "v"(cb + aoff[1]), "v"(cb + aoff[2]), "v"(cb + aoff[3]), "v"(cb + aoff[4]),
-              "v"(xb + boff[0]), "v"(xb + boff[1])
-            : "memory");
-      }
-      // windows: dword w = perm(hi = src[4 - w], lo = src[3 - w]) (src[i] = digit dword a4 - 4 + i)
-      mf_v4i Ac, Ad;
-#pragma unroll
-      for (int w = 0; w < 4; w++) {
-        Ac[w] = (int)__builtin_amdgcn_perm(dc[4 - w], dc[3 - w], sel[w]);
-        Ad[w] = (int)__builtin_amdgcn_perm(dd[4 - w], dd[3 - w], sel[w]);
-      }
-#pragma unroll
-      for (int g = 0; g < NGR; g++) {
-        mf_v4i B;
-        B[0] = (int)(xv[g].x ^ 0x80808080u);
-        B[1] = (int)(xv[g].y ^ 0x80808080u);
-        B[2] = (int)(xv[g].z ^ 0x80808080u);
-        B[3] = (int)(xv[g].w ^ 0x80808080u);
-        if (PROBE == 1) {  // timing probe: no matrix instructions (wrong sums)
-          acc[g][0][0] += Ac[0] ^ B[0];
-          acc[g][1][0] += Ad[1] ^ B[1];
-        } else {
-          acc[g][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ac, B, acc[g][0], 0, 0, 0);
-          acc[g][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Ad, B, acc[g][1], 0, 0, 0);
-        }
-      }
-    }
-    if (++ks < KS) continue;
-    // ---- the unit's last step: fold. Lane (slot l31, half h) holds rows a = (i & 3) + 8 (i >> 2) + 4 h of
-    // C[a][slot] in acc[.][i]; G_m = sum_t C[4 m + t] 2^(8 t) (m = 2 (i >> 2) + h) at weight 2^(32 m).
-    // v_permlane32_swap(c, d) leaves every lane the G's of coefficient cd = h for both halves: r[0] = the
-    // h = 0 (even m) value, r[1] the odd one. Registers only: the ring keeps streaming the next unit.
-    const Unit fu = unit_of(j);
-    ks = 0;
-    j++;
-    if (fu.live) {
-      const uint32_t cd = h, lane_r = 8 * fu.e8 + wave;
-      const uint64_t r0 = fu.blk * 64 + lane_r;
-#pragma unroll
-      for (int g = 0; g < NGR; g++) {
-        int64_t Gm[8];
-#pragma unroll
-        for (int jj = 0; jj < 4; jj++) {
-          int64_t gc = 0, gd = 0;
-#pragma unroll
-          for (int tt = 0; tt < 4; tt++) {
-            gc += (int64_t)acc[g][0][4 * jj + tt] * (int64_t)(1u << (8 * tt));
-            gd += (int64_t)acc[g][1][4 * jj + tt] * (int64_t)(1u << (8 * tt));
-          }
-          const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)gc, (uint32_t)gd, false, false);
-          const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)((uint64_t)gc >> 32),
-                                                           (uint32_t)((uint64_t)gd >> 32), false, false);
-          Gm[2 * jj] = (int64_t)(((uint64_t)hi[0] << 32) | lo[0]);
-          Gm[2 * jj + 1] = (int64_t)(((uint64_t)hi[1] << 32) | lo[1]);
-        }
-        // V = sum_m G_m 2^(32 m): 288-bit two's complement, then mod p
-        uint32_t L[9];
-        int64_t carry = 0;
-#pragma unroll
-        for (int m = 0; m < 8; m++) {
-          const int64_t tv = Gm[m] + carry;
-          L[m] = (uint32_t)tv;
-          carry = tv >> 32;
-        }
-        L[8] = (uint32_t)carry;
-        f128 v = reduce192(L[8], 0, 0);
-#pragma unroll
-        for (int i = 3; i >= 0; i--) v = reduce192((uint64_t)L[2 * i] | ((uint64_t)L[2 * i + 1] << 32), v.lo, v.hi);
-        if (carry < 0) v = sub128(v, c288);  // V = U - 2^288
-        v = add128(v, corr);
-        const uint32_t sl = fu.s0 + 32 * g + l31;
-        if (sl < chunk && r0 < b.n) st_il(b.xs, fu.blk, 2 * chunk, 2 * sl + cd, lane_r, v);
-      }
-    }
-    acc_zero();
-  }
-}
-
-// Gadget 0's group finish on the MFMA path: one wave per (64-report block, PPW-slot group), lane = report;
-// the R-scaled wire sums come from Bufs::xs (flp_psum_mfma_kernel).
-template <int PPW, bool LEADER>
-__global__ __launch_bounds__(64) void flp_psum_wires_kernel(Cfg c, Bufs b) {
-  const uint32_t NG = c.ngroups;
-  const uint32_t bid = blockIdx.x, xcd = bid & 7u, q = bid >> 3;
-  const uint32_t g = q % NG;
-  const uint64_t blk = (uint64_t)(q / NG) * 8 + xcd;
-  if (blk >= (b.n + 63) / 64) return;
-  const uint32_t lane = threadIdx.x;
-  f128 xe[PPW], xo[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; i++) {
-    const uint32_t j = g * PPW + i;
-    const uint32_t jj = j < c.chunk ? j : 0;
-    xo[i] = ld_il(b.xs, blk, 2 * c.chunk, 2 * jj, lane);
-    xe[i] = ld_il(b.xs, blk, 2 * c.chunk, 2 * jj + 1, lane);
-  }
-  psum_part_finish<PPW, false, LEADER>(c, b, blk, g, lane, xe, xo, make128(0, 0));
+  psum_part_finish<PPW, HIST, LEADER>(c, b, blk, g, lane, C, ae, ao, sx);
 }
 
 template <bool HIST, bool LEADER>
@@ -3254,41 +2875,10 @@ static void launch_psum_part(const Cfg& c, const Bufs& b, hipStream_t s, uint32_
     hipLaunchKernelGGL((flp_psum_part_kernel<PPW, HIST, LEADER>), dim3(grid), dim3(64), 0, s, c, b);
   }
 }
-// gadget 0 on the matrix cores (Cfg::mfma): the wire sums, then the per-group finish (no HIST)
-template <int PPW, bool LEADER>
-static void launch_psum_mfma(const Cfg& c, const Bufs& b, hipStream_t s, uint32_t grid) {
-  // persistent: one workgroup per CU (its LDS ring fills most of a CU), a multiple of 8 (XCDs)
-  static const uint32_t cus = [] {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    return n > 0 ? (uint32_t)n : 256u;
-  }();
-  static const int probe = getenv("JX_MF_PROBE") ? atoi(getenv("JX_MF_PROBE")) : 0;  // experiment (temporary)
-  const uint32_t ng = probe == 2 ? 2 : MF_NG;
-  const uint32_t nb = nblk_of(b.n), nsc = (c.chunk + 32 * ng - 1) / (32 * ng);
-  const uint64_t units = (uint64_t)((nb + 7) / 8) * 8 * 8 * nsc;
-  const uint32_t wmax = ((cus + 7) / 8 * 8) * (probe == 2 ? 2 : 1);
-  const uint32_t mgrid = (uint32_t)(units < wmax ? units : wmax);
-  if (probe == 2)
-    hipLaunchKernelGGL((flp_psum_mfma_kernel<2, 3, 0, 2, 2>), dim3(mgrid), dim3(64 * MF_WAVES), 0, s, c, b);
-  else if (probe == 1)
-    hipLaunchKernelGGL((flp_psum_mfma_kernel<MF_NG, 3, 1>), dim3(mgrid), dim3(64 * MF_WAVES), 0, s, c, b);
-  else
-    hipLaunchKernelGGL((flp_psum_mfma_kernel<MF_NG, 3>), dim3(mgrid), dim3(64 * MF_WAVES), 0, s, c, b);
-  hipLaunchKernelGGL((flp_psum_wires_kernel<PPW, LEADER>), dim3(grid), dim3(64), 0, s, c, b);
-}
 template <int PPW, bool HIST, bool LEADER>
 static void launch_psum_r(const Cfg& c, const Bufs& b, hipStream_t s) {
   const uint32_t nb = nblk_of(b.n);
-  if constexpr (!HIST) {
-    if (c.mfma)
-      launch_psum_mfma<PPW, LEADER>(c, b, s, ((nb + 7) / 8) * 8 * c.ngroups);
-    else
-      launch_psum_part<PPW, HIST, LEADER>(c, b, s, ((nb + 7) / 8) * 8 * c.ngroups);
-  } else {
-    launch_psum_part<PPW, HIST, LEADER>(c, b, s, ((nb + 7) / 8) * 8 * c.ngroups);
-  }
+  launch_psum_part<PPW, HIST, LEADER>(c, b, s, ((nb + 7) / 8) * 8 * c.ngroups);
   hipLaunchKernelGGL((flp_psum_final_kernel<HIST, LEADER>), dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s,
                      c, b);
 }
@@ -3309,10 +2899,7 @@ static hipError_t launch_psum_t(const Cfg& c, const Bufs& b, hipStream_t s) {
 template <int PPW, bool LEADER>
 static void launch_fp_r(const Cfg& c, const Bufs& b, hipStream_t s) {
   const uint32_t nb = nblk_of(b.n);
-  if (c.mfma)
-    launch_psum_mfma<PPW, LEADER>(c, b, s, ((nb + 7) / 8) * 8 * c.ngroups);
-  else
-    launch_psum_part<PPW, false, LEADER>(c, b, s, ((nb + 7) / 8) * 8 * c.ngroups);
+  launch_psum_part<PPW, false, LEADER>(c, b, s, ((nb + 7) / 8) * 8 * c.ngroups);
   hipLaunchKernelGGL((flp_norm_part_kernel<2, LEADER>), dim3(((nb + 7) / 8) * 8 * c.ngroups1), dim3(64), 0, s, c,
                      b);
   hipLaunchKernelGGL((flp_fp_final_kernel<LEADER>), dim3((uint32_t)((b.n + 255) / 256)), dim3(256), 0, s, c, b);

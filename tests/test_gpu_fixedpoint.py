@@ -10,8 +10,6 @@ own end-to-end measurements decodes to the reference's expected result.
 """
 from __future__ import annotations
 
-import os
-
 import numpy as np
 import pytest
 
@@ -46,21 +44,9 @@ def _batch(orc, vdaf, vk, n, seed, tamper_every=7):
     return meas, nonces, ps, his, lps
 
 
-def _engine(vdaf, vk, k3="mfma"):
-    """Gadget 0's wire sums on the matrix cores (default) or the VALU ring (JX_K3_MFMA=0 at configure)."""
-    if k3 == "mfma":
-        return HelperEngine(vdaf, vk)
-    os.environ["JX_K3_MFMA"] = "0"
-    try:
-        return HelperEngine(vdaf, vk)
-    finally:
-        del os.environ["JX_K3_MFMA"]
-
-
-@pytest.mark.parametrize("slow,k3", [(False, "mfma"), (True, "mfma"), (False, "valu")],
-                         ids=["fast", "slowpath", "valu_k3"])
+@pytest.mark.parametrize("slow", [False, True], ids=["fast", "slowpath"])
 @pytest.mark.parametrize("name", list(CASES))
-def test_helper_vs_oracle(name, slow, k3):
+def test_helper_vs_oracle(name, slow):
     bits, length = CASES[name]
     vdaf = Prio3.fixedpoint_boundedl2_vec_sum(bits, length)
     vk = bytes(range(50, 66))
@@ -68,7 +54,7 @@ def test_helper_vs_oracle(name, slow, k3):
     n = 48 if length >= 10000 else (96 if length >= 1000 else 200)
     _, nonces, ps, his, lps = _batch(orc, vdaf, vk, n, seed=sum(map(ord, name)))
     want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
-    with _engine(vdaf, vk, k3) as eng:
+    with HelperEngine(vdaf, vk) as eng:
         assert (eng.prep_share_len, eng.output_len) == (orc.sizes.prep_share, length)
         if slow:
             eng.debug(1, 1)

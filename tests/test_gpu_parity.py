@@ -291,26 +291,11 @@ def test_k1_split_variants(name, split):
         np.testing.assert_array_equal(res.verdicts, want["verdicts"])
 
 
-def k3_engine(vdaf, vk, k3):
-    """An engine whose ParallelSum gadget-0 wire sums run on the matrix cores ("mfma": the default for
-    SumVec and FixedPoint) or on the VALU ring ("valu": JX_K3_MFMA=0 while the engine is configured)."""
-    if k3 == "mfma":
-        return HelperEngine(vdaf, vk)
-    os.environ["JX_K3_MFMA"] = "0"
-    try:
-        return HelperEngine(vdaf, vk)
-    finally:
-        del os.environ["JX_K3_MFMA"]
-
-
-@pytest.mark.parametrize("k3", ["mfma", "valu"])
-@pytest.mark.parametrize("name", ["sumvec_8x1000_88", "histogram_256_16", "sumvec_64x20_9", "sumvec_small",
-                                  "sumvec_33x5_7"])
-def test_k3_ring_padded_groups(name, k3):
-    """Both ParallelSum FLP paths == the oracle, helper (verdicts, messages, output shares, aggregate) and
-    leader (prep shares): the matrix-core wire sums (flp_psum_mfma_kernel + the wires kernel) and the VALU
-    depth-4 LDS-DMA ring (4 slot groups per workgroup; Histogram always). sumvec_64x20_9 and sumvec_small
-    have a padded last group and workgroup; sumvec_33x5_7 (bits > 32) an odd call count."""
+@pytest.mark.parametrize("name", ["sumvec_8x1000_88", "histogram_256_16", "sumvec_64x20_9", "sumvec_small"])
+def test_k3_ring_padded_groups(name):
+    """The ParallelSum FLP part kernel (the depth-4 LDS-DMA ring, 4 slot groups per workgroup) == the
+    oracle, helper (verdicts, messages, output shares, aggregate) and leader (prep shares).
+    sumvec_64x20_9 and sumvec_small have a padded last group and workgroup."""
     pf = 21
     vdaf = CASES[name]
     vk = bytes(range(90, 106))
@@ -318,7 +303,7 @@ def test_k3_ring_padded_groups(name, k3):
     n = 150
     nonces, ps, his, lps = _random_batch(orc, vk, n, seed=pf * 11 + sum(map(ord, name)))
     want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
-    with k3_engine(vdaf, vk, k3) as eng:
+    with HelperEngine(vdaf, vk) as eng:
         res = eng.helper_initialized_batch(nonces, ps, his, lps, want_out_shares=True)
         np.testing.assert_array_equal(res.verdicts, want["verdicts"])
         fin = want["verdicts"] == 0
@@ -333,7 +318,7 @@ def test_k3_ring_padded_groups(name, k3):
     rands = rng.integers(0, 256, size=(24, orc.sizes.client_rand), dtype=np.uint8)
     shards = [orc.shard(meas[i], ln[i].tobytes(), rands[i].tobytes()) for i in range(24)]
     lps_, lis_ = (np.stack([np.frombuffer(s[k], np.uint8) for s in shards]) for k in (0, 1))
-    with k3_engine(vdaf, vk, k3) as eng:
+    with HelperEngine(vdaf, vk) as eng:
         init = eng.leader_initialized_batch(ln, lps_, lis_)
     for i in range(24):
         rc, share, _, _ = orc.prep_init(vk, 0, ln[i].tobytes(), lps_[i].tobytes(), lis_[i].tobytes())

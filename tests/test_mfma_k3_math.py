@@ -1,7 +1,8 @@
-"""Host replay of the matrix-core wire sums (flp_psum_mfma_kernel, DESIGN.md §5) with Python integers.
+"""Host replay of the matrix-core wire sums (flp_psum_mfma_kernel, DESIGN.md §7.1) with Python integers.
 
-The kernel computes gadget 0's R-scaled wire sums  x_s = sum_k v_k x_{k,s}  (v_k = c_k R or d_k R, mod p)
-as an int8 GEMM per report:
+The kernel was built, parity-tested on MI355X and measured slower than the VALU ring (git 3299f0a); it is not
+in the library. This test keeps its arithmetic pinned for a later revisit. The kernel computed gadget 0's
+R-scaled wire sums  x_s = sum_k v_k x_{k,s}  (v_k = c_k R or d_k R, mod p) as an int8 GEMM per report:
   * mf_digits(v): s = v if v <= 127 J else v - p; u = s + 128 J; digits d_i = byte_i(u) XOR 0x80 as int8,
     so sum_i d_i 256^i = s == v (mod p) (J = 0x0101..01, 16 bytes);
   * B[16 h + j][slot] = byte_j(x_{call h, slot}) XOR 0x80 (the int8 digits of x - 128 J);
