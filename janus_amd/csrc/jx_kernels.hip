@@ -40,11 +40,21 @@ __device__ __forceinline__ f128 w4_to_f(uint32_t a, uint32_t b, uint32_t c, uint
 __device__ __forceinline__ uint64_t il_idx(uint64_t blk, uint32_t len, uint32_t e, uint32_t lane) {
   return (blk * len + e) * IL + lane;
 }
+// (the staging is global memory: the address-space casts keep these global_load/store even inside the
+// non-inlined XOF tail, where a generic pointer would make them flat accesses that wait with vmcnt(0) and
+// lgkmcnt(0) each)
+// global (not flat) pointers for the staging in the non-inlined XOF tail: flat accesses count in both
+// vmcnt and lgkmcnt and force full waits; the host pass of hipcc keeps plain pointers
+#ifdef __HIP_DEVICE_COMPILE__
+typedef __attribute__((address_space(1))) uint4 g_uint4;
+#else
+typedef uint4 g_uint4;
+#endif
 __device__ __forceinline__ f128 ld_il(const uint4* base, uint64_t blk, uint32_t len, uint32_t e, uint32_t lane) {
-  return u4_to_f(base[il_idx(blk, len, e, lane)]);
+  return u4_to_f(((const g_uint4*)base)[il_idx(blk, len, e, lane)]);
 }
 __device__ __forceinline__ void st_il(uint4* base, uint64_t blk, uint32_t len, uint32_t e, uint32_t lane, f128 v) {
-  base[il_idx(blk, len, e, lane)] = f_to_u4(v);
+  ((g_uint4*)base)[il_idx(blk, len, e, lane)] = f_to_u4(v);
 }
 // The measurement share as the FLP kernels read it: the interleaved staging (element e of the lane's
 // report at p[e * IL]) or, for the leader, its explicit input share in place (p[e], report-major).
@@ -342,25 +352,59 @@ __device__ __forceinline__ void emit_proof(const Cfg& c, uint4* pp, uint32_t e, 
 // Barycentric weights of one gadget on the P-th roots of unity w^k (Montgomery form):
 //   c_k = w^k / (t - w^k) for k = 1..C at slot sk + stride*(k-1), c_0 = 1/(t - 1) at slot s0,
 // by one batch inversion (prefix products parked in the c_k slots, then one inversion chain).
-// Returns sum_{k>=1} c_k.
+// With with_d (ParallelSum gadget 0, stride 2; rcR = r^chunk R): also d_k = c_k rc^(k-1) at slot sk + 2(k-1) + 1, rc = r^chunk,
+// in the same backward pass: rc joins the inverted product, so 1/rc costs two products, and the powers
+// descend from rc^(C-1). The backward pass keeps four prefix-product loads in flight (a prefix in slot k-1
+// is overwritten only at step k-1, after its read). Returns sum_{k>=1} c_k.
 __device__ f128 bary_coeffs(uint4* coef, uint64_t blk, uint32_t NC, uint32_t lane, f128 tR, const uint4* omega,
-                            uint32_t C, uint32_t s0, uint32_t sk, uint32_t stride) {
+                            uint32_t C, uint32_t s0, uint32_t sk, uint32_t stride, bool with_d = false,
+                            f128 rcR = f128{0, 0}) {
   auto slot = [&](uint32_t k) { return k == 0 ? s0 : sk + stride * (k - 1); };
-  f128 acc = sub128(tR, u4_to_f(omega[0]));
+  const g_uint4* gom = (const g_uint4*)omega;
+  f128 acc = sub128(tR, u4_to_f(gom[0]));
   st_il(coef, blk, NC, slot(0), lane, acc);
   for (uint32_t k = 1; k <= C; k++) {
-    acc = mont128(acc, sub128(tR, u4_to_f(omega[k])));
+    acc = mont128(acc, sub128(tR, u4_to_f(gom[k])));
     st_il(coef, blk, NC, slot(k), lane, acc);
   }
-  f128 inv = minv(acc);
+  f128 inv, rp = make128(R1_128_LO, R1_128_HI), rinv = rp;
+  if (with_d) {
+    const f128 ie = minv(mont128(acc, rcR));  // 1 / (prefix * rc)
+    inv = mont128(ie, rcR);                     // 1 / prefix
+    rinv = mont128(ie, acc);                    // 1 / rc
+    rp = mpow(rcR, C - 1);                      // rc^(C-1)
+  } else {
+    inv = minv(acc);
+  }
   f128 sumc = make128(0, 0);
+  // step k needs the prefix of slot k-1 and w^k: both loaded four steps ahead (vmcnt counts in order, so a
+  // load issued just before its use would also wait for every prefetch)
+  auto pref = [&](int k) { return k >= 1 ? ld_il(coef, blk, NC, slot((uint32_t)k - 1), lane) : make128(0, 0); };
+  auto wk = [&](int k) { return k >= 1 ? u4_to_f(gom[k]) : make128(0, 0); };
+  const int Ci = (int)C;
+  f128 q0 = pref(Ci), q1 = pref(Ci - 1), q2 = pref(Ci - 2), q3 = pref(Ci - 3);
+  f128 o0 = wk(Ci), o1 = wk(Ci - 1), o2 = wk(Ci - 2), o3 = wk(Ci - 3);
   for (uint32_t k = C; k >= 1; k--) {
-    f128 pre = ld_il(coef, blk, NC, slot(k - 1), lane);
-    f128 w = u4_to_f(omega[k]);
+    const f128 pre = q0, w = o0;
+    q0 = q1;
+    q1 = q2;
+    q2 = q3;
+    o0 = o1;
+    o1 = o2;
+    o2 = o3;
+    // unconditional loads (a clamped index past the end: the value is never used) keep the loop
+    // branch-free, so the wait before the first use counts only the older loads
+    const uint32_t kn = k > 4 ? k - 4 : 1;
+    q3 = ld_il(coef, blk, NC, slot(kn - 1), lane);
+    o3 = u4_to_f(gom[kn]);
     f128 invden = mont128(inv, pre);
     inv = mont128(inv, sub128(tR, w));
     f128 ck = mont128(w, invden);
     st_il(coef, blk, NC, slot(k), lane, ck);
+    if (with_d) {
+      st_il(coef, blk, NC, slot(k) + 1, lane, mont128(ck, rp));
+      rp = mont128(rp, rinv);
+    }
     sumc = add128(sumc, ck);
   }
   st_il(coef, blk, NC, s0, lane, inv);  // c_0 = 1/(t - 1)
@@ -477,19 +521,11 @@ __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t
   // batch inversion of den_k = t - w^k, k = 0..calls
   const uint32_t C = c.calls;
   const uint32_t stride = c.algo == ALGO_SUM ? 1u : 2u;
-  const f128 sumc = bary_coeffs(coef, blk, NC, lane, tR, omega, C, COEF_C0, COEF_K, stride);
+  const f128 rcR = mpow(rR, c.chunk);  // r^chunk (ParallelSum's d_k = c_k r^((k-1) chunk))
+  const f128 sumc = bary_coeffs(coef, blk, NC, lane, tR, omega, C, COEF_C0, COEF_K, stride, c.algo != ALGO_SUM, rcR);
   // (1/2) * sum c_k, canonical: mont(sumc*R, 1/2) = sumc/2
   st_il(coef, blk, NC, COEF_HALFSUM, lane, mont128(sumc, u4_to_f(misc[1])));
   if (c.algo != ALGO_SUM) {
-    // d_k = c_k * r^{(k-1)*chunk}
-    f128 rc = mpow(rR, c.chunk);
-    f128 rp = R1;
-    for (uint32_t k = 1; k <= C; k++) {
-      const uint32_t sk = COEF_K + 2 * (k - 1);
-      f128 ck = ld_il(coef, blk, NC, sk, lane);
-      st_il(coef, blk, NC, sk + 1, lane, mont128(ck, rp));
-      rp = mont128(rp, rc);
-    }
     // power tables of the ParallelSum group finish (psum_part_finish): r^(j+1) canonical for the even
     // wires of slot j (a chain of mont products starting from the canonical r), and t^(g * per) R for
     // group g's share of G(t)
