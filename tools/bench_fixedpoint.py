@@ -45,16 +45,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bits", type=int, default=16)
     ap.add_argument("--length", type=int, default=10000)
-    ap.add_argument("--reports", type=int, default=32768, help="reports per ping-pong step (both roles on the GPU)")
+    ap.add_argument("--reports", type=int, default=40960, help="reports per ping-pong job (both roles on the GPU)")
     ap.add_argument("--role-reports", type=int, default=65536, help="reports per single-role step")
     ap.add_argument("--pool", type=int, default=48)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--skip", default="", help="comma list of legs to skip: pingpong,pipelined,helper,leader,cpu")
-    ap.add_argument("--helper-staging-gb", type=int, default=0,
-                    help="staging budget of the helper engine in the two-role legs (default: the engine's own, 1/3 "
-                         "of HBM); raise it so one launch holds --reports")
+    ap.add_argument("--helper-staging-gb", type=int, default=-1,
+                    help="staging budget of the helper engine in the two-role legs (default: sized so one launch "
+                         "holds --reports; 0: the engine's own, 1/3 of HBM)")
     ap.add_argument("--leader-staged", action="store_true",
                     help="the leader stages its measurement share (debug option 6) instead of reading it in place")
     a = ap.parse_args()
@@ -107,6 +107,9 @@ def main():
 
     def per_launch(kt, stage):
         return round(kt[stage]["ms"] / max(1, kt[stage]["launches"]), 3)
+
+    if a.helper_staging_gb < 0:  # the helper stages its measurement share (16 B per element) plus ~10 %
+        a.helper_staging_gb = -(-int(a.reports * vdaf.meas_len * 16 * 1.15) // (1 << 30)) + 2
 
     def helper_engine():
         if not a.helper_staging_gb:
