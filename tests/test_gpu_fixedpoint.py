@@ -169,3 +169,67 @@ def test_reference_e2e_result(bits):
     total = b"".join(((int.from_bytes(agg_l[i:i + 16], "little") + int.from_bytes(agg_h[i:i + 16], "little")) % P128)
                      .to_bytes(16, "little") for i in range(0, 48, 16))
     assert vdaf.decode_fixedpoint_result(total, 4) == [0.5, 0.5, 0.6875]
+
+
+@pytest.mark.parametrize("split", [0, 3, 6, 5], ids=["auto", "lanes", "pairs", "fused"])
+def test_two_jobs_in_flight(split):
+    """configs[4]'s bench shape (tools/bench_fixedpoint.py, two jobs in flight): while the helper engine
+    prepares job i-1 on its stream, the leader engine initializes job i on its own; then the leader
+    finishes job i-1. Inputs live in HBM (a 24-report pool tiled to 4,096 reports per job), the helper's
+    K1 is each of its kernels in turn, and after three jobs the verdicts of the last job and both
+    aggregates must be exactly the oracle's (24-report pool x multiplicity x 3 jobs)."""
+    import torch
+
+    bits, length = CASES["fp16_len10000"]
+    vdaf = Prio3.fixedpoint_boundedl2_vec_sum(bits, length)
+    vk = bytes(range(30, 46))
+    orc = O.Prio3Oracle(O.FIXEDPOINT_L2, bits, length, 0)
+    K, R, jobs = 24, 4096, 3
+    rng = np.random.default_rng(91)
+    meas = fixedpoint_measurements(bits, length, rng, K)
+    nonces = rng.integers(0, 256, size=(K, 16), dtype=np.uint8)
+    rands = rng.integers(0, 256, size=(K, orc.sizes.client_rand), dtype=np.uint8)
+    shards = [orc.shard(meas[i], nonces[i].tobytes(), rands[i].tobytes()) for i in range(K)]
+    ps, lis, his = (np.frombuffer(b"".join(s[k] for s in shards), np.uint8).reshape(K, -1) for k in range(3))
+    lps = np.stack([np.frombuffer(orc.prep_init(vk, 0, nonces[i].tobytes(), ps[i].tobytes(), lis[i].tobytes())[1],
+                                  np.uint8) for i in range(K)])
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16)
+    fin = want["verdicts"] == 0
+    assert 0 < fin.sum() < K  # the pool holds norm violators
+    dev = torch.device("cuda", 0)
+
+    def tile(x):
+        return torch.from_numpy(np.array(x).reshape(K, -1)).to(dev).repeat(-(-R // K), 1)[:R].contiguous()
+
+    d_n, d_ps, d_lis, d_his = tile(nonces), tile(ps), tile(lis), tile(his)
+    d_lps = [torch.empty((R, vdaf.prep_share_len), dtype=torch.uint8, device=dev) for _ in range(2)]
+    d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
+    d_hv = torch.empty(R, dtype=torch.uint8, device=dev)
+    d_lv = torch.empty(R, dtype=torch.uint8, device=dev)
+    with HelperEngine(vdaf, vk) as leader, HelperEngine(vdaf, vk) as helper:
+        if split:
+            helper.debug(3, split)
+        prev = None
+        for i in range(jobs + 1):
+            bid = leader.leader_init_device(R, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(),
+                                            d_lps[i % 2].data_ptr()) if i < jobs else None
+            if prev is not None:
+                helper.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(),
+                                                 d_lps[(i - 1) % 2].data_ptr(), R, 0, d_msgs.data_ptr(),
+                                                 d_hv.data_ptr())
+                helper.sync()
+                leader.leader_finish_device(prev, R, d_msgs.data_ptr(), d_hv.data_ptr(), d_lv.data_ptr())
+                leader.accumulate_device(prev, R)
+            leader.sync()
+            prev = bid
+        agg_l, cnt_l, cs_l = leader.aggregate_share(0)
+        agg_h, cnt_h, cs_h = helper.aggregate_share(0)
+    tiled_v = np.tile(want["verdicts"], -(-R // K))[:R]
+    np.testing.assert_array_equal(d_hv.cpu().numpy(), tiled_v)
+    np.testing.assert_array_equal(d_lv.cpu().numpy() == 0, tiled_v == 0)
+    mult = np.bincount(np.arange(R) % K, minlength=K) * jobs
+    enc = meas.astype(object) ^ (1 << (bits - 1))
+    total = [(int.from_bytes(agg_l[16 * j:16 * j + 16], "little") + int.from_bytes(agg_h[16 * j:16 * j + 16], "little"))
+             % P128 for j in range(length)]
+    assert total == [int((enc[fin, j] * mult[fin]).sum()) % P128 for j in range(length)]
+    assert cnt_l == cnt_h == int(mult[fin].sum()) and cs_l == cs_h
