@@ -1,0 +1,11 @@
+# Final check on the committed tree: the whole GPU suite, then the default bench (CPU baseline included;
+# the committed PMC summary fills roofline.traffic when the kernel sources match it)
+# usage: bash scripts/gpu_final.sh <name>   (outputs under gpurun_out/<name>/)
+set -o pipefail
+export TMPDIR=/tmp
+OUT=gpurun_out/${1:?name}
+mkdir -p $OUT
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo PYTEST_FAIL; grep -E "FAILED|Error" $OUT/pytest.log | head; tail -30 $OUT/pytest.log; exit 1; }
+tail -1 $OUT/pytest.log
+timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo BENCH_FAIL; tail -20 $OUT/bench.err; exit 1; }
+tail -1 $OUT/bench.json
