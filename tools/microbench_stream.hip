@@ -5,6 +5,7 @@
 //         64-report block, 2 elements per wave per call, depth-4 ring, one barrier per call), XOR only;
 //   flat: plain global_load_dwordx4 sweep, 4 loads in flight per lane, grid-stride;
 //   slice_*: the MFMA K3's per-eighth stream (interleaved vs eighth-major staging, ring depth 4 / 6);
+//   ring_mad<N>: the ring with N v_mad_u64_u32 per call per wave (K3's products without the rest);
 // and prints one JSON line per kernel with the achieved GB/s. Tells whether K3 (8.4 ms per 250k reports)
 // is bound by its stream or by its VALU work.
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/bin/microbench_stream tools/microbench_stream.hip
@@ -78,6 +79,64 @@ __global__ __launch_bounds__(256, 4) void ring(const uint4* meas, const uint4* c
   out[(blk * NG + g) * 64 + lane] = acc;
 }
 
+
+// The same ring with NM independent v_mad_u64_u32 per call per wave on the loaded words (K3 does 100 limb
+// products per call per wave plus ~50 other VALU instructions): how the stream rate falls as the ring's
+// compute grows, i.e. how much of K3's time its products add on top of the ring.
+template <int NM>
+__global__ __launch_bounds__(256, 4) void ring_mad(const uint4* meas, const uint4* coef, uint64_t nblk, uint4* out) {
+  constexpr int ROWS = 2 + W * PPW;
+  __shared__ uint4 rb[D][ROWS][64];
+  const uint32_t NW = NG / W;
+  const uint32_t bid = blockIdx.x, xcd = bid & 7u, q = bid >> 3;
+  const uint32_t wg = q % NW;
+  const uint64_t blk = (uint64_t)(q / NW) * 8 + xcd;
+  if (blk >= nblk) return;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = wg * W + wave, j0 = g * PPW;
+  const uint4* mb = meas + blk * M * 64 + lane;
+  const uint4* cb = coef + blk * NC * 64 + lane;
+  auto issue = [&](uint32_t k) {
+    if (wave < 2)
+      __builtin_amdgcn_global_load_lds((const void*)(cb + (uint64_t)(8 + 2 * (k - 1) + wave) * 64),
+                                       (void*)&rb[(k - 1) % D][wave][0], 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < PPW; i++)
+      __builtin_amdgcn_global_load_lds((const void*)(mb + (uint64_t)((k - 1) * CHUNK + j0 + i) * 64),
+                                       (void*)&rb[(k - 1) % D][2 + wave * PPW + i][0], 16, 0, 0);
+  };
+  for (uint32_t k = 1; k < D; k++) issue(k);
+  uint64_t acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const uint32_t base = lds_addr(&rb[0][0][lane]);
+  for (uint32_t k = 1; k <= CALLS; k++) {
+    if (k + D - 2 > CALLS)
+      wait_vmcnt<0>();
+    else if (wave < 2)
+      wait_vmcnt<(D - 2) * (PPW + 1)>();
+    else
+      wait_vmcnt<(D - 2) * PPW>();
+    __builtin_amdgcn_s_barrier();
+    if (k + D - 1 <= CALLS) issue(k + D - 1);
+    const uint32_t a = base + ((k - 1) % D) * ROWS * 1024;
+    uint4 cv, dv, v0, v1;
+    asm volatile(
+        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\tds_read_b128 %2, %6\n\tds_read_b128 %3, %7\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(cv), "=&v"(dv), "=&v"(v0), "=&v"(v1)
+        : "v"(a), "v"(a + 1024), "v"(a + (2 + wave * PPW) * 1024), "v"(a + (3 + wave * PPW) * 1024)
+        : "memory");
+    const uint32_t xs[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    const uint32_t cs[8] = {cv.x, cv.y, cv.z, cv.w, dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+    for (int m = 0; m < NM; m++) {
+      acc[m % 10] += (uint64_t)xs[m % 8] * cs[(m / 8) % 8];
+      asm("" : "+v"(acc[m % 10]));
+    }
+  }
+  uint64_t t = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) t ^= acc[i];
+  out[(blk * NG + g) * 64 + lane] = make_uint4((uint32_t)t, (uint32_t)(t >> 32), 0, 0);
+}
 
 // The MFMA K3's access pattern: a workgroup of 8 waves streams K-steps of 2 calls x 96 slots x 8 reports
 // (an eighth of a 64-report block; 24 KiB) through a depth-D LDS ring, one barrier per step. CONTIG = 0:
@@ -163,7 +222,7 @@ int main(int argc, char** argv) {
   const uint64_t slice_grid = ((nblk + 7) / 8) * 8 * 8;
   uint4* out2;
   CHK(hipMalloc(&out2, slice_grid * 512 * 16));
-  for (int kern = 0; kern < 6; kern++) {
+  for (int kern = 0; kern < 10; kern++) {
     float best = 1e30f;
     for (int rep = 0; rep < 4; rep++) {
       CHK(hipEventRecord(e0, 0));
@@ -177,8 +236,16 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((slice<1, 4>), dim3(slice_grid), dim3(512), 0, 0, meas, nblk, out2);
       else if (kern == 4)
         hipLaunchKernelGGL((slice<0, 6>), dim3(slice_grid), dim3(512), 0, 0, meas, nblk, out2);
-      else
+      else if (kern == 5)
         hipLaunchKernelGGL((slice<1, 6>), dim3(slice_grid), dim3(512), 0, 0, meas, nblk, out2);
+      else if (kern == 6)
+        hipLaunchKernelGGL((ring_mad<50>), dim3(ring_grid), dim3(256), 0, 0, meas, coef, nblk, out);
+      else if (kern == 7)
+        hipLaunchKernelGGL((ring_mad<100>), dim3(ring_grid), dim3(256), 0, 0, meas, coef, nblk, out);
+      else if (kern == 8)
+        hipLaunchKernelGGL((ring_mad<150>), dim3(ring_grid), dim3(256), 0, 0, meas, coef, nblk, out);
+      else
+        hipLaunchKernelGGL((ring_mad<200>), dim3(ring_grid), dim3(256), 0, 0, meas, coef, nblk, out);
       CHK(hipEventRecord(e1, 0));
       CHK(hipEventSynchronize(e1));
       float ms;
@@ -187,7 +254,9 @@ int main(int argc, char** argv) {
     }
     printf("{\"kernel\": \"%s\", \"reports\": %llu, \"bytes\": %.0f, \"ms\": %.3f, \"GBps\": %.1f}\n",
            kern == 0 ? "ring" : kern == 1 ? "flat" : kern == 2 ? "slice_il_d4" : kern == 3 ? "slice_contig_d4"
-                                  : kern == 4 ? "slice_il_d6" : "slice_contig_d6",
+                                  : kern == 4 ? "slice_il_d6" : kern == 5 ? "slice_contig_d6"
+                                  : kern == 6 ? "ring_mad50" : kern == 7 ? "ring_mad100" : kern == 8 ? "ring_mad150"
+                                  : "ring_mad200",
            (unsigned long long)nrep, bytes, best, bytes / (best * 1e6));
     fflush(stdout);
   }
