@@ -184,6 +184,17 @@ __global__ __launch_bounds__(512, 1) void slice(const uint4* meas, uint64_t nblk
   out[(uint64_t)bid * 512 + threadIdx.x] = acc;
 }
 
+// pseudo-random fill (splitmix64 of the index): the multipliers see K3-like operand bits, not a constant
+__global__ __launch_bounds__(256) void fill_random(uint4* p, uint64_t n16, uint64_t seed) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256) {
+    uint64_t z = (i + seed) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    const uint64_t a = z ^ (z >> 31), b = a * 0xD6E8FEB86659FD93ull ^ (a >> 29);
+    p[i] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32) & 0x7FFFFFFFu);
+  }
+}
+
 __global__ __launch_bounds__(256) void flat(const uint4* p, uint64_t n16, uint4* out) {
   const uint64_t tid = (uint64_t)blockIdx.x * 256 + threadIdx.x, nt = (uint64_t)gridDim.x * 256;
   uint4 acc = make_uint4(0, 0, 0, 0);
@@ -222,7 +233,14 @@ int main(int argc, char** argv) {
   const uint64_t slice_grid = ((nblk + 7) / 8) * 8 * 8;
   uint4* out2;
   CHK(hipMalloc(&out2, slice_grid * 512 * 16));
+  const bool rnd = argc > 2 && argv[2][0] == 'r';  // random operands (K3-like switching) instead of a constant
+  if (rnd) {
+    hipLaunchKernelGGL(fill_random, dim3(8192), dim3(256), 0, 0, meas, n16, 1);
+    hipLaunchKernelGGL(fill_random, dim3(8192), dim3(256), 0, 0, coef, nblk * NC * 64, 77);
+    CHK(hipDeviceSynchronize());
+  }
   for (int kern = 0; kern < 10; kern++) {
+    if (rnd && kern >= 1 && kern <= 5) continue;  // the pure streams do not multiply
     float best = 1e30f;
     for (int rep = 0; rep < 4; rep++) {
       CHK(hipEventRecord(e0, 0));
@@ -252,11 +270,12 @@ int main(int argc, char** argv) {
       CHK(hipEventElapsedTime(&ms, e0, e1));
       if (rep > 0 && ms < best) best = ms;
     }
-    printf("{\"kernel\": \"%s\", \"reports\": %llu, \"bytes\": %.0f, \"ms\": %.3f, \"GBps\": %.1f}\n",
+    printf("{\"kernel\": \"%s\", \"data\": \"%s\", \"reports\": %llu, \"bytes\": %.0f, \"ms\": %.3f, \"GBps\": %.1f}\n",
            kern == 0 ? "ring" : kern == 1 ? "flat" : kern == 2 ? "slice_il_d4" : kern == 3 ? "slice_contig_d4"
                                   : kern == 4 ? "slice_il_d6" : kern == 5 ? "slice_contig_d6"
                                   : kern == 6 ? "ring_mad50" : kern == 7 ? "ring_mad100" : kern == 8 ? "ring_mad150"
                                   : "ring_mad200",
+           rnd ? "random" : "constant",
            (unsigned long long)nrep, bytes, best, bytes / (best * 1e6));
     fflush(stdout);
   }
