@@ -144,7 +144,13 @@ def pmc_traffic(kernel: str, reports_per_launch: float):
         f"{wl['reports_per_launch']}-report launches"
 
 
+POOL_BLOCK = 256  # pool reports per stored block aggregate (CyclicPool prefix sums)
+
+
 def make_pool(vdaf, vk, K, seed=0x5EED, threads=16):
+    """K distinct client reports and the oracle's helper results: verdicts, prep messages, the pool
+    aggregate and the aggregate of every POOL_BLOCK-report block (for expectations over any range of
+    the cyclic tiling, CyclicPool)."""
     from oracle import oracle as O  # input generation (client + leader), see module docstring
     orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
     rng = np.random.default_rng(seed)
@@ -155,15 +161,83 @@ def make_pool(vdaf, vk, K, seed=0x5EED, threads=16):
     for i in range(0, K, 100):  # 1% invalid: one flipped bit in the leader prep share
         j = int(rng.integers(0, lps.shape[1]))
         lps[i, j] ^= 1 << int(rng.integers(0, 8))
-    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=threads)
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=threads, want_out_shares=True)
+    outs, fin = want.pop("out_shares"), want["verdicts"] == 0
+    nb = -(-K // POOL_BLOCK)
+    want["blocks"] = np.stack([np.frombuffer(orc.aggregate(
+        [outs[i].tobytes() for i in range(b * POOL_BLOCK, min(K, (b + 1) * POOL_BLOCK)) if fin[i]]), np.uint8)
+        for b in range(nb)])
     return orc, nonces, ps, his, lps, want
+
+
+class CyclicPool:
+    """Expected aggregates over any range of the cyclic tiling report g -> pool[g % K] (each rank's
+    shard [start, start + R) of the global report index, and the merged range of all ranks).
+
+    With F(g) = the aggregate of reports [0, g): F(g) = (g // K) * pool total + prefix(g % K), and the
+    aggregate of [lo, hi) is F(hi) - F(lo) mod p. prefix(r) adds the stored block aggregates below r
+    and `partial(a, r)` (the aggregate of pool[a:r], fewer than `block` reports) above them. Counts
+    the same way from the per-report finished flags."""
+
+    def __init__(self, fin, block_aggs, block: int, partial, p: int):
+        self.K, self.block, self.partial, self.p = len(fin), block, partial, p
+        width = len(block_aggs[0])
+        self.cum = [[0] * width]
+        for b in block_aggs:
+            self.cum.append([(x + y) % p for x, y in zip(self.cum[-1], b)])
+        self.fin_cum = np.concatenate([[0], np.cumsum(np.asarray(fin, dtype=np.int64))])
+
+    def prefix(self, r: int):
+        b, t = divmod(r, self.block)
+        vec = list(self.cum[b])
+        if t:
+            vec = [(x + y) % self.p for x, y in zip(vec, self.partial(b * self.block, r))]
+        return vec, int(self.fin_cum[r])
+
+    def F(self, g: int):
+        q, r = divmod(g, self.K)
+        vec, c = self.prefix(r)
+        tot = self.cum[-1]
+        return [(q * t + x) % self.p for t, x in zip(tot, vec)], q * int(self.fin_cum[-1]) + c
+
+    def range(self, lo: int, hi: int, times: int = 1):
+        """(aggregate as field elements, count) of reports [lo, hi), accumulated `times` times."""
+        (a, ca), (b, cb) = self.F(lo), self.F(hi)
+        return [(y - x) * times % self.p for x, y in zip(a, b)], (cb - ca) * times
+
+
+def field_elems(b: bytes, fb: int) -> list[int]:
+    return [int.from_bytes(b[i:i + fb], "little") for i in range(0, len(b), fb)]
+
+
+def prio3_work(v, role: str = "helper") -> dict:
+    """Instruction model of one report's K1 (XOF stage) and K3 (FLP stage) for any TurboSHAKE Prio3
+    instance (the SumVec numbers of sumvec_work, generalised): Keccak-p[1600,12] permutations at
+    OPS_PER_PERM, Montgomery products at OPS_PER_MONT, lazy FLP products at OPS_PER_FMUL. The helper
+    squeezes its measurement and proof shares and absorbs the joint-rand part; the leader absorbs
+    only (its shares are explicit)."""
+    fb = v.field_bytes
+    MB = v.meas_len * fb
+    jr = v.joint_rand_len > 0
+    helper = role == "helper"
+    perms = (-(-MB // 168) if helper else 0) + ((42 + MB) // 168 + 1 if jr else 0) + \
+        (-(-(v.proof_len * fb) // 168) if helper else 0) + 4
+    calls, chunk = v.calls, max(1, v.gadget_chunk)
+    mont_k1 = 6 + 3 * (calls + 1) + 143 + 2 * calls + 8 + chunk + -(-chunk // 2)
+    if v.algo_id == 5:  # FixedPointBoundedL2VecSum's second gadget
+        mont_k1 += 3 * (v.norm_calls + 1) + 143 + 2 * v.norm_calls
+    fmul_k3 = 2 * v.meas_len + (2 * v.length if v.algo_id == 5 else 0)
+    mont_k3 = 8 * chunk + 2 * (2 * v.P - 1) + 20
+    return dict(perms=perms, mont_k1=mont_k1, fmul_k3=fmul_k3, mont_k3=mont_k3,
+                ops_k1=perms * OPS_PER_PERM + mont_k1 * OPS_PER_MONT,
+                ops_k3=fmul_k3 * OPS_PER_FMUL + mont_k3 * OPS_PER_MONT)
 
 
 def pool_cache_path(vdaf, vk, K, seed=0x5EED) -> str:
     import hashlib
 
     key = hashlib.sha256(f"{vdaf.algo_id}/{vdaf.bits}/{vdaf.length}/{vdaf.chunk_length}/{K}/{seed}/{vk.hex()}/"
-                         "pool-v1".encode()).hexdigest()[:16]
+                         f"pool-v2/{POOL_BLOCK}".encode()).hexdigest()[:16]
     return os.path.join(os.environ.get("JX_POOL_CACHE", "/tmp"), f"janus_amd_bench_pool_{key}.npz")
 
 
@@ -179,6 +253,7 @@ def load_or_make_pool(vdaf, vk, K, threads, local_rank: int, wait_s: float = 900
             orc, nonces, ps, his, lps, want = make_pool(vdaf, vk, K, threads=threads)
             tmp = f"{path}.{os.getpid()}.tmp.npz"
             np.savez(tmp, nonces=nonces, ps=ps, his=his, lps=lps, verdicts=want["verdicts"],
+                     prep_msgs=want["prep_msgs"], blocks=want["blocks"],
                      agg=np.frombuffer(want["agg"], np.uint8), count=np.array([want["count"]], np.int64))
             os.replace(tmp, path)
             return orc, nonces, ps, his, lps, want, "generated"
@@ -189,7 +264,8 @@ def load_or_make_pool(vdaf, vk, K, threads, local_rank: int, wait_s: float = 900
             time.sleep(0.5)
     d = np.load(path)  # allow_pickle=False: plain arrays this script wrote
     orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
-    want = {"verdicts": d["verdicts"], "agg": d["agg"].tobytes(), "count": int(d["count"][0])}
+    want = {"verdicts": d["verdicts"], "prep_msgs": d["prep_msgs"], "blocks": d["blocks"], "agg": d["agg"].tobytes(),
+            "count": int(d["count"][0])}
     return orc, d["nonces"], d["ps"], d["his"], d["lps"], want, "cached"
 
 
@@ -299,6 +375,9 @@ def main():
     ap.add_argument("--bits", type=int, default=8)
     ap.add_argument("--length", type=int, default=1000)
     ap.add_argument("--chunk", type=int, default=88)
+    ap.add_argument("--no-secondary", dest="secondary", action="store_false",
+                    help="skip the other BASELINE configs (configs[0-2], configs[4]) that the N=1 run measures after "
+                         "the headline")
     ap.add_argument("--no-dist", dest="dist", action="store_false",
                     help="at N=1, skip the RCCL (nccl) process group and the shard-record all-gather + device merge "
                          "that every step otherwise ends with (by default the N=1 step carries the N>1 step's work)")
@@ -337,13 +416,22 @@ def main():
     log(f"pool of {args.pool} reports {how} in {startup_s:.1f}s; {int(want['count'])} valid")
 
     R = args.reports_per_gpu
-    reps = -(-R // args.pool)
+    K = args.pool
+    # Rank r prepares the global reports [r R, (r + 1) R) of the cyclic tiling g -> pool[g % K]: ranks hold
+    # different reports (shard_range over world R reports), and the expected results follow from the
+    # offsets (CyclicPool), so a rank that merged a duplicate or a neighbour's record fails verification.
+    from janus_amd.distributed import shard_range
+
+    start, stop = shard_range(R * world, rank, world)
+    assert stop - start == R
+    idx = (start + np.arange(R)) % K
+    d_idx = torch.from_numpy(idx).to(dev)
 
     def dev_tile(a):
-        t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-        return t.repeat(reps, 1)[:R].contiguous()
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dev).index_select(0, d_idx).contiguous()
 
     d_n, d_ps, d_his, d_lps = dev_tile(nonces), dev_tile(ps), dev_tile(his), dev_tile(lps)
+    del d_idx
     d_verdicts = torch.empty(R, dtype=torch.uint8, device=dev)
     d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
     eng = HelperEngine(vdaf, vk, device=local_rank)
@@ -375,24 +463,29 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
-    # ---- verification: aggregate == (steps + warmup) * (q * pool aggregate + aggregate of the first
-    # R - q K pool reports), R = q K + rem; count likewise; every verdict == the oracle's
+    # ---- verification against the oracle, from the pool's block aggregates (CyclicPool): this rank's
+    # aggregate == (steps + warmup) x the aggregate of its global range; the merged record == the same
+    # over every rank's range; every verdict and every finished report's Finish{prep_msg} == the oracle's
     agg, count, _ = eng.aggregate_share(0)
     total_steps = args.steps + args.warmup
-    q, rem = divmod(R, args.pool)
-    head = orc.helper_prep_batch(vk, nonces[:rem], ps[:rem], his[:rem], lps[:rem], nthreads=threads) if rem else \
-        {"agg": bytes(16 * vdaf.output_len), "count": 0}
-    dec = lambda b: [int.from_bytes(b[16 * j:16 * j + 16], "little") for j in range(vdaf.output_len)]  # noqa: E731
-    pool_agg, head_agg = dec(want["agg"]), dec(head["agg"])
-    acc = [(q * a + h) * total_steps % P128 for a, h in zip(pool_agg, head_agg)]
-    exp = b"".join(x.to_bytes(16, "little") for x in acc)
-    exp_count = total_steps * (q * want["count"] + head["count"])
-    verified = agg == exp and count == exp_count
-    verdict_ok = bool(np.array_equal(d_verdicts.cpu().numpy(), np.tile(want["verdicts"], reps)[:R]))
+
+    def partial(a, r):
+        h = orc.helper_prep_batch(vk, nonces[a:r], ps[a:r], his[a:r], lps[a:r], nthreads=threads)
+        return field_elems(h["agg"], 16)
+
+    cyc = CyclicPool(want["verdicts"] == 0, [field_elems(b.tobytes(), 16) for b in want["blocks"]], POOL_BLOCK,
+                     partial, P128)
+    enc = lambda v: b"".join(x.to_bytes(16, "little") for x in v)  # noqa: E731
+    exp_agg, exp_count = cyc.range(start, stop, total_steps)
+    verified = agg == enc(exp_agg) and count == exp_count
+    got_v = d_verdicts.cpu().numpy()
+    verdict_ok = bool(np.array_equal(got_v, want["verdicts"][idx]))
+    fin_rows = got_v == 0
+    msgs_ok = bool(np.array_equal(d_msgs.cpu().numpy()[fin_rows], want["prep_msgs"][idx][fin_rows]))
     if combiner is not None:
         c_agg, c_count, _ = combiner.result()
-        exp_c = b"".join(((x * world) % P128).to_bytes(16, "little") for x in acc)
-        verified = verified and c_agg == exp_c and c_count == world * exp_count
+        all_agg, all_count = cyc.range(0, R * world, total_steps)
+        verified = verified and c_agg == enc(all_agg) and c_count == all_count
 
     total_reports = R * world * args.steps
     value = total_reports / elapsed
@@ -467,16 +560,94 @@ def main():
                     "k1_hbm_GBps": round(work["hbm_k1"] * chunk_reports / (k1_ms * 1e-3) / 1e9, 1),
                     "k3_hbm_GBps": round(work["hbm_k3"] * chunk_reports / (k3_ms * 1e-3) / 1e9, 1),
                     "work_per_report": work},
-        "verified": bool(verified and verdict_ok),
+        "verified": bool(verified and verdict_ok and msgs_ok),
+        "verification": {"aggregate_and_count": bool(verified), "verdicts": verdict_ok,
+                         "prep_msgs_of_finished_reports": msgs_ok,
+                         "rank_range": [start, stop], "note": "rank r holds global reports [r R, (r+1) R) of the "
+                         "cyclic pool tiling; expected aggregates from the pool's block aggregates (CyclicPool)"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(orc, vdaf, vk, nonces, ps, his, lps, args.cpu_seconds, cpu["threads"])
         out["cpu_baseline"].update(cpu)
+    eng.close()
+    del d_n, d_ps, d_his, d_lps, d_verdicts, d_msgs
+    if combiner is not None:
+        del combiner
+    torch.cuda.empty_cache()
+    if world == 1 and args.secondary:
+        out["secondary"] = secondary_configs(cpu, threads)
+        out["verified_all_configs"] = bool(out["verified"] and all(v.get("verified") for v in out["secondary"].values()))
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
     if use_dist:
         dist.destroy_process_group()
+
+
+def secondary_configs(cpu: dict, threads: int) -> dict:
+    """The other BASELINE.json configs, measured after the headline with the SumVec engine freed
+    (tools/bench_configs.py, tools/bench_fixedpoint.py): Prio3Count at 100k
+    reports (configs[0]), Prio3Sum bits=32 at 1M (configs[1]), Prio3Histogram 256/16 at 1M (configs[2]),
+    Prio3FixedPointBoundedL2VecSum 16-bit x 10000 leader+helper ping-pong (configs[4]: two 40,960-report
+    jobs in flight, and one job at a time). Each entry: reports/s, kernel ms, the issue-roofline
+    fraction of its dominant kernel (prio3_work), a CPU baseline at 1 and N threads, and verification
+    against the oracle (verdicts, prep messages of finished reports, aggregate and count)."""
+    from janus_amd.vdaf import Prio3
+    from tools import bench_configs as BC
+    from tools import bench_fixedpoint as BF
+
+    t0 = time.perf_counter()
+    sec = {}
+    specs = [
+        ("configs[0]", "Prio3Count (configs[0]: 100k reports)", Prio3.count(),
+         lambda rng, K: rng.integers(0, 2, size=(K, 1), dtype=np.uint64), 100_000),
+        ("configs[1]", "Prio3Sum bits=32 (configs[1])", Prio3.sum(32),
+         lambda rng, K: rng.integers(0, 1 << 32, size=(K, 1), dtype=np.uint64), 1_000_000),
+        ("configs[2]", "Prio3Histogram length=256 chunk_length=16 (configs[2])", Prio3.histogram(256, 16),
+         lambda rng, K: rng.integers(0, 256, size=(K, 1), dtype=np.uint64), 1_000_000),
+    ]
+    for key, name, v, fn, R in specs:
+        t = time.perf_counter()
+        r = BC.run(name, v, fn, R, 4096, 3, 1, 3.0, threads, cpu)
+        r["roofline"] = issue_roofline(v, "helper", R, r["kernels"])
+        r["driver_seconds"] = round(time.perf_counter() - t, 1)
+        sec[key] = r
+        log(f"{key}: {r['value']:.0f} reports/s verified={r['verified']} ({r['driver_seconds']} s)")
+    t = time.perf_counter()
+    v = Prio3.fixedpoint_boundedl2_vec_sum(16, 10000)
+    fp = BF.run(16, 10000, reports=40960, pool=48, steps=3, warmup=1, cpu_seconds=6.0,
+                skip=("helper", "leader"))
+    fp["serial"] = {"reports_per_s": fp.pop("value"), "ms_per_step": fp.pop("ms_per_step"),
+                    "kernels": fp.pop("kernels"), "role_ms_per_step": fp.pop("role_ms_per_step")}
+    fp["value"] = fp["pipelined"]["reports_per_s"]
+    fp["value_note"] = "two 40,960-report aggregation jobs in flight (leader init of job i beside the helper of " \
+                       "job i-1); 'serial' = one job at a time through leader init, helper, leader finish"
+    fp["roofline"] = issue_roofline(v, "helper", 40960, {"k1_ms_per_launch": fp["pipelined"]["kernels"]["helper"]["xof"]},
+                                    kernel="K1 helper xof_lanes_kernel (two-jobs shape)")
+    fp["roofline_leader"] = issue_roofline(v, "leader", 40960,
+                                           {"k1_ms_per_launch": fp["pipelined"]["kernels"]["leader"]["xof"]},
+                                           kernel="K1 leader xof_leader_kernel (two-jobs shape)")
+    fp["driver_seconds"] = round(time.perf_counter() - t, 1)
+    sec["configs[4]"] = fp
+    log(f"configs[4]: {fp['value']:.0f} reports/s (two jobs), verified={fp['verified']} ({fp['driver_seconds']} s)")
+    sec["_seconds"] = round(time.perf_counter() - t0, 1)
+    return sec
+
+
+def issue_roofline(v, role: str, reports: int, kernels: dict, kernel: str | None = None) -> dict:
+    """Instruction-issue fraction of the dominant kernel of one launch of `reports` reports, from the
+    prio3_work model and the HIP-event kernel time."""
+    w = prio3_work(v, role)
+    k1 = kernels.get("k1_ms_per_launch") or 0.0
+    k3 = kernels.get("k3_ms_per_launch") or 0.0
+    reports = min(reports, kernels.get("reports_per_launch", reports))
+    k1_dom = k1 >= k3
+    ms = k1 if k1_dom else k3
+    ops = w["ops_k1"] if k1_dom else w["ops_k3"]
+    ach = ops * reports / (ms * 1e-3) / 1e12 if ms else 0.0
+    return {"bound": "valu", "kernel": kernel or ("K1 (XOF)" if k1_dom else "K3 (FLP)"), "achieved": round(ach, 3),
+            "peak": round(VALU_PEAK_TOPS, 2), "unit": "TOP/s int32 instruction issue (model: bench.py prio3_work)",
+            "frac": round(ach / VALU_PEAK_TOPS, 4), "ms_per_launch": ms, "reports_per_launch": reports,
+            "ops_per_report": ops}
 
 
 if __name__ == "__main__":

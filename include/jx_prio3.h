@@ -23,6 +23,14 @@
  *    engine's mutex for the duration of the call, so one engine per GPU can serve concurrent
  *    aggregation jobs from several host threads; the device work of the calls is serialized on the
  *    engine stream. What a job keeps between calls (its prepared reports) is a batch handle.
+ *  - Host-buffer entry points are synchronous. Device-pointer entry points (*_device) are
+ *    asynchronous on the engine stream, a NON-BLOCKING stream that orders itself after nothing:
+ *    PRODUCER ORDERING is the caller's. Before a *_device call whose inputs were written by work
+ *    queued on another stream, call jx_engine_wait_stream(e, producer) (or jx_engine_wait_event on an
+ *    event recorded after the producer's writes); after it, jx_engine_join_stream(e, consumer) (or
+ *    jx_engine_record_event + a wait) before the consumer reads the outputs or reuses the inputs.
+ *    Neither blocks the host. Creating an engine synchronizes only the engine stream.
+ *  - jx_last_error returns the message of the calling thread's last failed call.
  *  - Byte layouts are the DAP/VDAF encodings (fixed stride per report):
  *      nonces               n x 16   (report ids; VDAF nonce, aggregator.rs:1951)
  *      public_shares        n x PS   (Prio3PublicShare: joint-rand parts, 0 or 32 B)
@@ -170,7 +178,10 @@ int32_t jx_leader_prep_init_batch(jx_engine* e, uint64_t n, const uint8_t* nonce
 int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t* prep_msgs,
                                     uint8_t* out_verdicts, uint8_t* out_output_shares);
 /* Device-pointer leader role (inputs resident in HBM; asynchronous on the engine stream, n <= the
- * engine capacity, grown on demand; the report ids are copied into the batch).
+ * engine capacity, grown on demand; the report ids are copied into the batch). For Prio3Sum, SumVec
+ * and FixedPointBoundedL2VecSum the FLP kernels read the measurement share in place from
+ * d_leader_input_shares in 16-byte vectors: that pointer must be 16-byte aligned (JX_E_INVALID
+ * otherwise); the stride LIS is a multiple of 16 for every Field128 instance.
  * d_out_verdicts nullable. Finish: d_peer_verdicts (nullable) are the helper's verdicts; a report
  * the helper rejected gets JX_HELPER_STEP_FAILURE. */
 int32_t jx_leader_prep_init_device(jx_engine* e, uint64_t n, const void* d_nonces, const void* d_public_shares,
@@ -243,6 +254,23 @@ int32_t jx_engine_sync(jx_engine* e);
 /* The engine's HIP stream (hipStream_t), for callers that order their own work after it. */
 int32_t jx_engine_stream(jx_engine* e, void** stream);
 
+/* Producer / consumer ordering of the device-pointer entry points (see Conventions). None blocks the
+ * host; all are stream-ordered.
+ * jx_engine_wait_stream: engine work queued after this call starts only after all work queued on
+ *   `stream` (hipStream_t; NULL = the null stream) so far has completed.
+ * jx_engine_join_stream: work queued on `stream` after this call starts only after all engine work
+ *   queued so far has completed.
+ * jx_engine_wait_event / jx_engine_record_event: the same with a caller-owned hipEvent_t (the engine
+ *   stream waits on the event's last record / records the event). With several host threads on one
+ *   engine, a wait or join issued by one thread may also order another thread's calls: that only
+ *   adds ordering, never removes it.
+ * The reference needs none of this: Janus calls prio synchronously on owned values
+ * (aggregator/src/aggregator.rs:1945-1967). */
+int32_t jx_engine_wait_stream(jx_engine* e, void* stream);
+int32_t jx_engine_join_stream(jx_engine* e, void* stream);
+int32_t jx_engine_wait_event(jx_engine* e, void* event);
+int32_t jx_engine_record_event(jx_engine* e, void* event);
+
 /* Kernel timing with HIP events recorded on the engine stream around each stage.
  * enable != 0 starts collecting (and clears the totals). ms[0] = XOF stage (K1),
  * ms[1] = FLP stage (K3), ms[2] = accumulate (K4), ms[3] = slow-path kernel;
@@ -250,12 +278,13 @@ int32_t jx_engine_stream(jx_engine* e, void** stream);
 int32_t jx_engine_timing(jx_engine* e, int32_t enable);
 int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]);
 
-/* Debug knobs (tests and measurements): option 1 = route every report through the slow XOF kernel;
- * 2 = accumulate chunking; 3 = helper K1 kernel (0 automatic: the fused two-sponge kernel, the
- * lane-split kernel for launches under one fused wave per SIMD, the lane-pair kernel under one lane-split
- * wave per SIMD; 3 lane-split; 5 fused, forced; 6 lane pairs); 6 = leader measurement share staged by K1
- * (1) instead of read in place by the FLP kernels (0, default);
- * 5 = overlapped two-stream fused path. JX_K1_SPLIT sets option 3 at create. */
+/* Debug knobs (tests and measurements); any other option returns JX_E_INVALID.
+ *   option 1: value != 0 routes every report through the slow XOF kernel K1';
+ *   option 2: accumulate report chunks, 1..4096 (frees the staging);
+ *   option 3: helper K1 kernel: 0 automatic (the fused two-sponge kernel; the lane-split kernel for
+ *             launches under one fused wave per SIMD; the lane-pair kernel under one lane-split wave
+ *             per SIMD), 3 lane-split, 5 fused, 6 lane pairs (bits <= 32).
+ * The environment variable JX_K1_SPLIT sets option 3 at create. */
 int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value);
 
 const char* jx_status_str(int32_t status);

@@ -22,6 +22,7 @@ EXPORTED_SYMBOLS = (
     "jx_aggregate_combine_device", "jx_shard_record_bytes", "jx_shard_record_export_device",
     "jx_shard_record_combine_device", "jx_engine_sync", "jx_engine_stream", "jx_engine_timing",
     "jx_engine_timing_read", "jx_engine_debug", "jx_status_str", "jx_last_error",
+    "jx_engine_wait_stream", "jx_engine_join_stream", "jx_engine_wait_event", "jx_engine_record_event",
 )
 
 _lib = None
@@ -86,6 +87,10 @@ def load():
         "jx_shard_record_combine_device": (i32, [vp, vp, u32, vp]),
         "jx_engine_sync": (i32, [vp]),
         "jx_engine_stream": (i32, [vp, P(vp)]),
+        "jx_engine_wait_stream": (i32, [vp, vp]),
+        "jx_engine_join_stream": (i32, [vp, vp]),
+        "jx_engine_wait_event": (i32, [vp, vp]),
+        "jx_engine_record_event": (i32, [vp, vp]),
         "jx_engine_timing": (i32, [vp, i32]),
         "jx_engine_timing_read": (i32, [vp, P(ctypes.c_float), P(u64)]),
         "jx_engine_debug": (i32, [vp, i32, ctypes.c_int64]),

@@ -116,7 +116,8 @@ def handle_aggregate_init(engine: HelperEngine, prepare_inits: list[PrepareInit]
             seg[j] = segments[i] if segments else 0
             finished[i] = True
         if writer is None:
-            engine.accumulate(m, accept, seg, batch_id=res.batch_id)
+            with engine.resident(res.batch_id):  # accumulate consumes the batch; on an error it is released
+                engine.accumulate(m, accept, seg, batch_id=res.batch_id)
     if writer is not None:
         times = [(int(segments[i]) if segments else 0, p.report_share.metadata.time)
                  for i, p in enumerate(prepare_inits)] + list(extra_report_times)
@@ -194,12 +195,36 @@ def leader_aggregate_init(engine: HelperEngine, reports: list[LeaderReport], seg
             inits.append(PrepareInit(ReportShare(r.metadata, r.public_share, r.helper_encrypted_input_share),
                                      PingPongMessage.initialize(res.prep_shares[j].tobytes())))
             stepped.append(i)
+    times = [(int(segments[i]) if segments else 0, r.metadata.time) for i, r in enumerate(reports)]
+    if writer is not None:  # InitialWrite of the in-progress job: no finished report yet
+        try:
+            collected = writer.write_job(engine, 0, 0, None, None, [], times, initial_write=True, terminal=False)
+        except BaseException:
+            if ok:
+                engine.release(res.batch_id, missing_ok=True)
+            raise
+        # fail_report_aggregations_for_collected_batches on the initial write (aggregation_job_writer.rs:
+        # 557-605): a report of an already collected batch fails with BatchCollected and is not sent to
+        # the helper (its engine row is never continued, so it is never accumulated)
+        if collected:
+            keep = [k for k, i in enumerate(stepped) if (int(segments[i]) if segments else 0) not in collected]
+            for k, i in enumerate(stepped):
+                if (int(segments[i]) if segments else 0) in collected:
+                    failed[i] = PrepareError.BatchCollected
+            inits = [inits[k] for k in keep]
+            stepped = [stepped[k] for k in keep]
     step = LeaderStep(inits, stepped, failed, len(ok), failures, res if ok else None)
     step._batch_index = {i: j for j, i in enumerate(ok)}  # report index -> engine batch row
-    step._times = [(int(segments[i]) if segments else 0, r.metadata.time) for i, r in enumerate(reports)]
-    if writer is not None:  # InitialWrite of the in-progress job: no finished report yet
-        writer.write_job(engine, 0, 0, None, None, [], step._times, initial_write=True, terminal=False)
+    step._times = times
     return step
+
+
+def leader_abandon(engine: HelperEngine, step: LeaderStep) -> None:
+    """Drop an aggregation job's leader state (the job was abandoned, or its helper exchange failed
+    for good): its resident engine batch is released. A later leader_process_helper_response for
+    the step fails with JX_E_STATE."""
+    if step.init is not None:
+        engine.release(step.init.batch_id, missing_ok=True)
 
 
 def leader_process_helper_response(engine: HelperEngine, step: LeaderStep, prepare_resps: list[PrepareResp],
@@ -212,6 +237,9 @@ def leader_process_helper_response(engine: HelperEngine, step: LeaderStep, prepa
     if len(prepare_resps) != len(step.stepped) or any(
             resp.report_id != step.prepare_inits[k].report_share.metadata.report_id
             for k, resp in enumerate(prepare_resps)):
+        # the job step fails (process_response_from_helper's error): its device state is released, and
+        # the job is stepped again from leader_aggregate_init
+        leader_abandon(engine, step)
         raise ValueError("missing, duplicate, out-of-order, or unexpected prepare steps in response")
     failures = Counter(step.step_failures)
     nrep = max([*step.stepped, *step.failed, -1]) + 1
@@ -243,7 +271,11 @@ def leader_process_helper_response(engine: HelperEngine, step: LeaderStep, prepa
         responses = [PrepareResp(step.prepare_inits[k].report_share.metadata.report_id,
                                  PrepareStepResult(2, error=results[i])) for k, i in enumerate(step.stepped)]
         return AggregateInitOutcome(responses, finished, failures)
-    fin = engine.leader_continued_batch(msgs[:, :pm] if pm else None, init=step.init)
+    try:
+        fin = engine.leader_continued_batch(msgs[:, :pm] if pm else None, init=step.init)
+    except BaseException:
+        leader_abandon(engine, step)
+        raise
     accept = np.zeros(step.n, np.uint8)
     seg = np.zeros(step.n, np.uint32)
     for i, row in step._batch_index.items():
@@ -258,7 +290,8 @@ def leader_process_helper_response(engine: HelperEngine, step: LeaderStep, prepa
         seg[row] = segments[i] if segments else 0
         finished[i] = True
     if writer is None:
-        engine.accumulate(step.n, accept, seg, batch_id=step.init.batch_id)
+        with engine.resident(step.init.batch_id):
+            engine.accumulate(step.n, accept, seg, batch_id=step.init.batch_id)
     else:
         row_seg = [0] * step.n
         for i, row in step._batch_index.items():

@@ -126,12 +126,17 @@ struct jx_engine {
   uint64_t launches[NST] = {0, 0, 0, 0};
   uint32_t force_slow = 0;
   uint32_t k1_split = 0;  // helper K1: 0 automatic, 3 lane-split, 5 fused, 6 lane pairs (JX_K1_SPLIT, debug option 3)
-  uint32_t leader_staged = 0;  // debug option 6: the leader stages its measurement share (no in-place reads)
-  std::string err;
+  // producer / consumer ordering (jx_engine_wait_stream / jx_engine_join_stream): reused events
+  hipEvent_t ev_wait = nullptr, ev_join = nullptr;
 };
 
+// The message of the last failing call, per calling thread: an engine serves several host threads,
+// and each reads the error of its own call (jx_last_error), never another thread's.
+static thread_local std::string t_err;
+
 static int32_t fail(jx_engine* e, int32_t code, const std::string& msg) {
-  if (e) e->err = msg;
+  (void)e;
+  t_err = msg;
   return code;
 }
 #define HIPCHK(e, call)                                                                                   \
@@ -141,7 +146,10 @@ static int32_t fail(jx_engine* e, int32_t code, const std::string& msg) {
       return fail((e), _st == hipErrorOutOfMemory ? JX_E_NOMEM : JX_E_HIP,                                \
                   std::string(#call) + ": " + hipGetErrorString(_st));                                    \
   } while (0)
-#define LOCK(e) std::lock_guard<std::mutex> _lk((e)->mu)
+// every entry point: the engine mutex for the call, and a fresh per-thread error message
+#define LOCK(e)                                   \
+  std::lock_guard<std::mutex> _lk((e)->mu);       \
+  t_err.clear()
 
 
 // ---------------------------------------------------------------------------- host field helpers
@@ -488,13 +496,43 @@ static uint32_t acc_nchunks(const jx_engine* e) {
   return want < 16u ? 16u : (want > 4096u ? 4096u : want);
 }
 
+// Device allocation. On out-of-memory the released-batch pool is handed back to the device and the
+// allocation tried once more, so idle pooled batches never cause a JX_E_NOMEM.
+static void trim_batch_pool(jx_engine* e) {
+  if (e->batch_pool.empty()) return;
+  (void)hipStreamSynchronize(e->stream);  // queued work may still use a pooled allocation
+  for (auto& kv : e->batch_pool) (void)hipFree(kv.second);
+  e->batch_pool.clear();
+}
+static hipError_t dev_alloc(jx_engine* e, void** p, size_t bytes) {
+  hipError_t st = hipMalloc(p, bytes ? bytes : 16);
+  if (st == hipErrorOutOfMemory && !e->batch_pool.empty()) {
+    (void)hipGetLastError();
+    trim_batch_pool(e);
+    st = hipMalloc(p, bytes ? bytes : 16);
+  }
+  if (st != hipSuccess) *p = nullptr;
+  return st;
+}
+
+// JX_E_NOMEM naming what holds the device memory (resident batches are the caller's to release).
+static int32_t nomem(jx_engine* e, const char* what, size_t bytes) {
+  uint64_t held = 0;
+  for (auto& kv : e->batches) held += kv.second.bytes;
+  return fail(e, JX_E_NOMEM,
+              std::string(what) + ": out of device memory allocating " + std::to_string(bytes) + " B; " +
+                  std::to_string(e->batches.size()) + " resident batches hold " + std::to_string(held) +
+                  " B (release finished or abandoned jobs with jx_batch_release)");
+}
+
 static int32_t ensure_capacity(jx_engine* e, uint64_t n, bool need_meas = true) {
   if (n <= e->cap) {
     if (!need_meas || e->meas_cap >= e->cap) return JX_OK;
     HIPCHK(e, hipStreamSynchronize(e->stream));
     if (e->d_meas) (void)hipFree(e->d_meas);
     e->d_meas = nullptr;
-    HIPCHK(e, hipMalloc((void**)&e->d_meas, e->cap * e->cfg.meas_len * stage_eb(e->cfg)));
+    const size_t mb = e->cap * e->cfg.meas_len * stage_eb(e->cfg);
+    if (dev_alloc(e, (void**)&e->d_meas, mb) != hipSuccess) return nomem(e, "staging", mb);
     e->meas_cap = e->cap;
     return JX_OK;
   }
@@ -502,7 +540,7 @@ static int32_t ensure_capacity(jx_engine* e, uint64_t n, bool need_meas = true) 
   free_staging(e);
   const Cfg& c = e->cfg;
   uint64_t cap = (n + 63) / 64 * 64;
-  auto A = [&](void** p, size_t bytes) -> hipError_t { return hipMalloc(p, bytes ? bytes : 16); };
+  auto A = [&](void** p, size_t bytes) -> hipError_t { return dev_alloc(e, p, bytes); };
   HIPCHK(e, A((void**)&e->d_nonces, cap * 16));
   HIPCHK(e, A((void**)&e->d_ps, cap * c.ps_bytes));
   HIPCHK(e, A((void**)&e->d_his, cap * c.his_bytes));
@@ -578,7 +616,7 @@ static int32_t batch_new(jx_engine* e, uint64_t n, bool leader, uint64_t* id, Ba
     b.bytes = it->first;
     e->batch_pool.erase(it);
   } else {
-    HIPCHK(e, hipMalloc(&b.mem, bytes ? bytes : 256));
+    if (dev_alloc(e, &b.mem, bytes ? bytes : 256) != hipSuccess) return nomem(e, "new batch", bytes);
     b.bytes = bytes;
   }
   uint8_t* m = (uint8_t*)b.mem;
@@ -655,7 +693,7 @@ static int32_t drain_timing(jx_engine* e) {
   return JX_OK;
 }
 
-static bool use_inplace(const jx_engine* e) { return leader_inplace(e->cfg) && !e->leader_staged; }
+static bool use_inplace(const jx_engine* e) { return leader_inplace(e->cfg); }
 
 // ---------------------------------------------------------------------------- core sequencing
 
@@ -747,9 +785,9 @@ static int32_t ensure_leader_capacity(jx_engine* e, uint64_t n) {
   }
   const Cfg& c = e->cfg;
   const uint64_t cap = e->cap;
-  HIPCHK(e, hipMalloc((void**)&e->d_lis, cap * c.lis_bytes));
-  HIPCHK(e, hipMalloc((void**)&e->d_lps_out, cap * c.lps_bytes));
-  HIPCHK(e, hipMalloc((void**)&e->d_in_msgs, cap * c.seed));
+  HIPCHK(e, dev_alloc(e, (void**)&e->d_lis, cap * c.lis_bytes));
+  HIPCHK(e, dev_alloc(e, (void**)&e->d_lps_out, cap * c.lps_bytes));
+  HIPCHK(e, dev_alloc(e, (void**)&e->d_in_msgs, cap * c.seed));
   e->leader_cap = cap;
   return JX_OK;
 }
@@ -1003,8 +1041,14 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
     return JX_E_HIP;
   }
   std::vector<uint4> consts = make_consts(e->cfg);
+  // On the engine stream, synchronized on it alone: creating an engine orders nothing with the caller's
+  // streams (that is jx_engine_wait_stream's job).
   if (hipMalloc((void**)&e->d_consts, consts.size() * sizeof(uint4)) != hipSuccess ||
-      hipMemcpy(e->d_consts, consts.data(), consts.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess) {
+      hipMemcpyAsync(e->d_consts, consts.data(), consts.size() * sizeof(uint4), hipMemcpyHostToDevice, e->stream) !=
+          hipSuccess ||
+      hipStreamSynchronize(e->stream) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_wait, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess) {
     jx_engine_destroy(e);
     return JX_E_HIP;
   }
@@ -1072,6 +1116,8 @@ void jx_engine_destroy(jx_engine* e) {
     if (e->h_ptrs[k]) (void)hipHostFree(e->h_ptrs[k]);
     if (e->ev_ptrs[k]) (void)hipEventDestroy(e->ev_ptrs[k]);
   }
+  if (e->ev_wait) (void)hipEventDestroy(e->ev_wait);
+  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1239,6 +1285,9 @@ int32_t jx_leader_prep_init_device(jx_engine* e, uint64_t n, const void* d_nonce
   LOCK(e);
   const Cfg& c = e->cfg;
   if (n && c.ps_bytes && !d_public_shares) return JX_E_INVALID;
+  // the in-place FLP kernels read the measurement share in 16-byte vectors (header contract)
+  if (n && use_inplace(e) && (reinterpret_cast<uintptr_t>(d_leader_input_shares) & 15u))
+    return fail(e, JX_E_INVALID, "leader init: d_leader_input_shares must be 16-byte aligned");
   HIPCHK(e, hipSetDevice(e->device));
   uint64_t id = 0;
   Batch* B = nullptr;
@@ -1279,8 +1328,10 @@ int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t batch_id, uint64_t n,
   int32_t rc = leader_batch(e, batch_id, n, &B);
   if (rc) return rc;
   if (n && c.jr_len && !prep_msgs) return JX_E_INVALID;
-  B->finished = true;
-  if (n == 0) return JX_OK;
+  if (n == 0) {
+    B->finished = true;
+    return JX_OK;
+  }
   HIPCHK(e, hipSetDevice(e->device));
   rc = ensure_leader_capacity(e, n);
   if (rc) return rc;
@@ -1292,6 +1343,8 @@ int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t batch_id, uint64_t n,
     b.msgs = B->msgs;
     HIPCHK(e, launch_leader_finish(c, b, e->d_in_msgs, nullptr, e->stream));
   }
+  // finished once prepare_next is queued: a failure above leaves the batch finishable (or releasable)
+  B->finished = true;
   HIPCHK(e, hipMemcpyAsync(out_verdicts, B->verdicts, n, hipMemcpyDeviceToHost, e->stream));
   if (out_output_shares) {
     rc = copy_out_shares(e, B->outs, n, out_output_shares);
@@ -1310,14 +1363,17 @@ int32_t jx_leader_prep_finish_device(jx_engine* e, uint64_t batch_id, uint64_t n
   int32_t rc = leader_batch(e, batch_id, n, &B);
   if (rc) return rc;
   if (n && c.jr_len && !d_prep_msgs) return JX_E_INVALID;
-  B->finished = true;
-  if (n == 0) return JX_OK;
+  if (n == 0) {
+    B->finished = true;
+    return JX_OK;
+  }
   HIPCHK(e, hipSetDevice(e->device));
   Bufs b{};
   b.n = n;
   b.verdicts = B->verdicts;
   b.msgs = B->msgs;
   HIPCHK(e, launch_leader_finish(c, b, (const uint8_t*)d_prep_msgs, (const uint8_t*)d_peer_verdicts, e->stream));
+  B->finished = true;
   if (d_out_verdicts) HIPCHK(e, hipMemcpyAsync(d_out_verdicts, B->verdicts, n, hipMemcpyDeviceToDevice, e->stream));
   return JX_OK;
 }
@@ -1646,6 +1702,41 @@ int32_t jx_engine_sync(jx_engine* e) {
   return JX_OK;
 }
 
+int32_t jx_engine_wait_event(jx_engine* e, void* event) {
+  if (!e || !event) return JX_E_INVALID;
+  LOCK(e);
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamWaitEvent(e->stream, (hipEvent_t)event, 0));
+  return JX_OK;
+}
+
+int32_t jx_engine_record_event(jx_engine* e, void* event) {
+  if (!e || !event) return JX_E_INVALID;
+  LOCK(e);
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipEventRecord((hipEvent_t)event, e->stream));
+  return JX_OK;
+}
+
+int32_t jx_engine_wait_stream(jx_engine* e, void* stream) {
+  if (!e) return JX_E_INVALID;
+  LOCK(e);
+  HIPCHK(e, hipSetDevice(e->device));
+  // hipStreamWaitEvent captures the event's current record, so one reused event serves every call
+  HIPCHK(e, hipEventRecord(e->ev_wait, (hipStream_t)stream));
+  HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_wait, 0));
+  return JX_OK;
+}
+
+int32_t jx_engine_join_stream(jx_engine* e, void* stream) {
+  if (!e) return JX_E_INVALID;
+  LOCK(e);
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipEventRecord(e->ev_join, e->stream));
+  HIPCHK(e, hipStreamWaitEvent((hipStream_t)stream, e->ev_join, 0));
+  return JX_OK;
+}
+
 int32_t jx_engine_stream(jx_engine* e, void** stream) {
   if (!e || !stream) return JX_E_INVALID;
   *stream = (void*)e->stream;
@@ -1691,11 +1782,6 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
     e->k1_split = (uint32_t)value;
     return JX_OK;
   }
-  if (option == 6) {  // leader measurement share: 0 read in place (default), 1 staged by K1
-    if (value != 0 && value != 1) return JX_E_INVALID;
-    e->leader_staged = (uint32_t)value;
-    return JX_OK;
-  }
   if (option == 2) {  // accumulate chunking (tests)
     if (value < 1 || value > 4096) return JX_E_INVALID;
     HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -1727,6 +1813,9 @@ const char* jx_status_str(int32_t s) {
   }
 }
 
-const char* jx_last_error(const jx_engine* e) { return e ? e->err.c_str() : ""; }
+const char* jx_last_error(const jx_engine* e) {
+  (void)e;
+  return t_err.c_str();
+}
 
 }  // extern "C"

@@ -133,7 +133,7 @@ class ShardCombiner:
         import torch.distributed as dist
 
         cur = torch.cuda.current_stream(self.dev)
-        self.engine.export_record_device(segment, self.record.data_ptr())
+        self.engine.export_record_device(segment, self.record.data_ptr(), stream=False)
         # the all-gather reads the exported record and overwrites `gathered`, which the previous merge
         # (queued before the export on the engine stream) has read
         cur.wait_stream(self.stream)
@@ -142,7 +142,7 @@ class ShardCombiner:
         else:  # RCCL over xGMI into the persistent buffer; ready on the current stream when the call returns
             dist.all_gather(list(self.gathered.unbind(0)), self.record, group=self.group)
         self.stream.wait_stream(cur)  # the merge reads the gathered records
-        self.engine.combine_records_device(self.gathered.data_ptr(), self.world, self.merged.data_ptr())
+        self.engine.combine_records_device(self.gathered.data_ptr(), self.world, self.merged.data_ptr(), stream=False)
         return self.merged
 
     def result(self) -> tuple[bytes, int, bytes]:

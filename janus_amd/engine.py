@@ -16,11 +16,24 @@ models.rs:1275-1330) without changing the engine, so a retried datastore transac
 recompute them; `accumulate` merges a batch into the engine's running aggregations (the
 engine as one shard) and releases it.
 
+Device-pointer methods (`*_device`) order themselves against a torch stream (default: the current
+stream of the engine's device): the engine's work waits for everything queued on that stream before
+the call (the producer of the inputs), and work queued on that stream afterwards waits for the
+engine's (the consumer of the outputs, and torch's allocator reusing the inputs). So tensors produced
+and consumed on torch's current stream need no `sync()`. Pass `stream=False` to order by hand
+(`wait_stream` / `join_stream` / events), e.g. to keep two engines' jobs overlapping.
+
+Resident batches hold device memory until released: `helper_initialized_batch(keep=False)` drops the
+batch at once, `resident(batch_id)` is a context manager that releases it on exit, and the aggregator
+paths release in `finally`.
+
 All compute runs in the HIP kernels of libjanus_prio3.so; nothing here falls back to the CPU.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import threading
 from dataclasses import dataclass
 
 import numpy as np
@@ -97,6 +110,9 @@ class HelperEngine:
     _leader_id = 0
 
     def __init__(self, vdaf: Prio3, verify_key: bytes, device: int = 0):
+        # guards the per-instance defaults (last leader batch) when threads share the engine; the
+        # C engine serializes the calls themselves
+        self._lock = threading.Lock()
         if len(verify_key) != vdaf.verify_key_len:
             raise ValueError(f"verify key must be {vdaf.verify_key_len} bytes for {vdaf.name()} "
                              "(VERIFY_KEY_LENGTH / VERIFY_KEY_LENGTH_HMACSHA256_AES128, core/src/vdaf.rs:16,24)")
@@ -141,14 +157,60 @@ class HelperEngine:
     def handle(self):
         return self._h
 
+    # ------------------------------------------------------------------ stream ordering
+    def _stream_handle(self, stream):
+        """hipStream_t of `stream` (None: torch's current stream on the engine's device; a torch
+        stream; or an integer handle); None when the caller orders by hand (stream=False)."""
+        if stream is False:
+            return None
+        if stream is None:
+            import torch
+
+            stream = torch.cuda.current_stream(self.device)
+        return int(getattr(stream, "cuda_stream", stream))
+
+    def wait_stream(self, stream=None):
+        """Engine work queued from now on waits for all work queued on `stream` so far."""
+        h = self._stream_handle(stream)
+        check(self._L.jx_engine_wait_stream(self._h, h or None), self._h, "jx_engine_wait_stream")
+
+    def join_stream(self, stream=None):
+        """Work queued on `stream` from now on waits for all engine work queued so far."""
+        h = self._stream_handle(stream)
+        check(self._L.jx_engine_join_stream(self._h, h or None), self._h, "jx_engine_join_stream")
+
+    def wait_event(self, event):
+        """The engine stream waits on a torch.cuda.Event (or hipEvent_t handle) recorded by the caller."""
+        check(self._L.jx_engine_wait_event(self._h, int(getattr(event, "cuda_event", event))), self._h,
+              "jx_engine_wait_event")
+
+    def record_event(self, event):
+        """Record a torch.cuda.Event (or hipEvent_t handle) on the engine stream."""
+        check(self._L.jx_engine_record_event(self._h, int(getattr(event, "cuda_event", event))), self._h,
+              "jx_engine_record_event")
+
+    @contextlib.contextmanager
+    def _ordered(self, stream):
+        if stream is False:
+            yield
+            return
+        h = self._stream_handle(stream)
+        check(self._L.jx_engine_wait_stream(self._h, h or None), self._h, "jx_engine_wait_stream")
+        try:
+            yield
+        finally:
+            check(self._L.jx_engine_join_stream(self._h, h or None), self._h, "jx_engine_join_stream")
+
     # ------------------------------------------------------------------ prepare
     def helper_initialized_batch(self, nonces, public_shares, helper_input_shares, leader_prep_shares,
-                                 want_out_shares: bool = False) -> BatchResult:
+                                 want_out_shares: bool = False, keep: bool = True) -> BatchResult:
         """prio ping-pong helper_initialized + evaluate for n reports (host buffers).
 
         leader_prep_shares are the prep_share payloads of the leaders'
         PingPongMessage::Initialize (fixed length; the aggregator layer rejects other
-        lengths as leader_prep_share_decode_failure before calling this)."""
+        lengths as leader_prep_share_decode_failure before calling this). keep=False releases the
+        new resident batch before returning (callers that want only verdicts / prep messages /
+        output shares); the result's batch_id is then 0."""
         n = len(nonces) // 16 if isinstance(nonces, (bytes, bytearray)) else int(np.asarray(nonces).shape[0])
         nn = _u8(nonces, n, 16, "nonces")
         ps = _u8(public_shares, n, self.public_share_len, "public_shares")
@@ -162,6 +224,9 @@ class HelperEngine:
                                           _ptr(his), _ptr(lps), _ptr(msgs) if self.prep_msg_len else None,
                                           _ptr(verdicts), _ptr(outs), ctypes.byref(bid))
         check(st, self._h, "jx_helper_prep_batch")
+        if not keep:
+            self.release(bid.value)
+            bid.value = 0
         return BatchResult(verdicts[:n], msgs[:n, : self.prep_msg_len], outs[:n] if outs is not None else None,
                            bid.value)
 
@@ -177,9 +242,22 @@ class HelperEngine:
         check(self._L.jx_engine_batches(self._h, ctypes.byref(n), ctypes.byref(b)), self._h, "jx_engine_batches")
         return n.value, b.value
 
-    def release(self, batch_id: int):
-        """Drop a resident batch (an aggregation job that is done or abandoned)."""
-        check(self._L.jx_batch_release(self._h, batch_id), self._h, "jx_batch_release")
+    def release(self, batch_id: int, missing_ok: bool = False):
+        """Drop a resident batch (an aggregation job that is done or abandoned). missing_ok: a batch
+        that is no longer resident (already accumulated or released) is not an error."""
+        st = self._L.jx_batch_release(self._h, batch_id)
+        if st == -5 and missing_ok:  # JX_E_STATE
+            return
+        check(st, self._h, "jx_batch_release")
+
+    @contextlib.contextmanager
+    def resident(self, batch_id: int):
+        """Scope of a resident batch: released on exit unless accumulate already consumed it."""
+        try:
+            yield batch_id
+        finally:
+            if batch_id:
+                self.release(batch_id, missing_ok=True)
 
     def aggregate_records(self, batch_id: int, n: int, accept_mask: np.ndarray | None = None,
                           segment_index: np.ndarray | None = None, nsegments: int = 1) -> list[tuple[bytes, int, bytes]]:
@@ -197,11 +275,13 @@ class HelperEngine:
         return [unpack_record(out[k * rb:(k + 1) * rb], self.field_bytes) for k in range(nsegments)]
 
     def aggregate_records_device(self, batch_id: int, n: int, d_accept_mask: int | None, d_segment_index: int | None,
-                                 nsegments: int, d_out_records: int):
-        """aggregate_records with device arrays; asynchronous on the engine stream."""
-        check(self._L.jx_batch_aggregate_records_device(self._h, batch_id, n, d_accept_mask, d_segment_index,
-                                                        nsegments, d_out_records),
-              self._h, "jx_batch_aggregate_records_device")
+                                 nsegments: int, d_out_records: int, stream=None):
+        """aggregate_records with device arrays; asynchronous on the engine stream, ordered against
+        `stream`."""
+        with self._ordered(stream):
+            check(self._L.jx_batch_aggregate_records_device(self._h, batch_id, n, d_accept_mask, d_segment_index,
+                                                            nsegments, d_out_records),
+                  self._h, "jx_batch_aggregate_records_device")
 
     # ------------------------------------------------------------------ leader role
     def leader_initialized_batch(self, nonces, public_shares, leader_input_shares) -> "LeaderInit":
@@ -220,7 +300,8 @@ class HelperEngine:
         st = self._L.jx_leader_prep_init_batch(self._h, n, _ptr(nn), _ptr(ps) if self.public_share_len else None,
                                                _ptr(lis), _ptr(shares), _ptr(verdicts), ctypes.byref(bid))
         check(st, self._h, "jx_leader_prep_init_batch")
-        self._leader_n, self._leader_id = n, bid.value
+        with self._lock:
+            self._leader_n, self._leader_id = n, bid.value
         return LeaderInit(verdicts[:n], shares[:n], bid.value)
 
     def leader_continued_batch(self, prep_msgs, want_out_shares: bool = False,
@@ -228,8 +309,11 @@ class HelperEngine:
         """prio ping-pong leader_continued on the helper's Finish{prep_msg} (aggregation_job_driver.rs:
         588-602): prepare_next for the batch of `init` (default: the last leader_initialized_batch).
         Raises EngineError (JX_E_STATE) if that batch was released or already finished."""
-        n = self._leader_n if init is None else len(init.verdicts)
-        bid = self._leader_id if init is None else init.batch_id
+        if init is None:  # the last leader batch: callers sharing the engine across threads pass `init`
+            with self._lock:
+                n, bid = self._leader_n, self._leader_id
+        else:
+            n, bid = len(init.verdicts), init.batch_id
         msgs = None
         if self.prep_msg_len:
             msgs = _u8(prep_msgs, n, self.prep_msg_len, "prep_msgs") if n else np.zeros((1, self.prep_msg_len), np.uint8)
@@ -252,27 +336,33 @@ class HelperEngine:
 
     # ------------------------------------------------------------------ device-pointer paths (inputs in HBM)
     def leader_init_device(self, n: int, d_nonces: int, d_public_shares: int | None, d_leader_input_shares: int,
-                           d_out_prep_shares: int, d_out_verdicts: int | None = None) -> int:
-        """leader_initialized for n reports resident in HBM; returns the batch id. Asynchronous."""
+                           d_out_prep_shares: int, d_out_verdicts: int | None = None, stream=None) -> int:
+        """leader_initialized for n reports resident in HBM; returns the batch id. Asynchronous,
+        ordered against `stream` (module docstring)."""
         bid = ctypes.c_uint64()
-        st = self._L.jx_leader_prep_init_device(self._h, n, d_nonces, d_public_shares, d_leader_input_shares,
-                                                d_out_prep_shares, d_out_verdicts, ctypes.byref(bid))
-        check(st, self._h, "jx_leader_prep_init_device")
+        with self._ordered(stream):
+            st = self._L.jx_leader_prep_init_device(self._h, n, d_nonces, d_public_shares, d_leader_input_shares,
+                                                    d_out_prep_shares, d_out_verdicts, ctypes.byref(bid))
+            check(st, self._h, "jx_leader_prep_init_device")
         return bid.value
 
     def leader_finish_device(self, batch_id: int, n: int, d_prep_msgs: int | None, d_peer_verdicts: int | None = None,
-                             d_out_verdicts: int | None = None):
+                             d_out_verdicts: int | None = None, stream=None):
         """leader_continued on the helper's prep messages in HBM; reports the helper rejected
-        (d_peer_verdicts != 0) fail with helper_step_failure. Asynchronous."""
-        check(self._L.jx_leader_prep_finish_device(self._h, batch_id, n, d_prep_msgs, d_peer_verdicts, d_out_verdicts),
-              self._h, "jx_leader_prep_finish_device")
+        (d_peer_verdicts != 0) fail with helper_step_failure. Asynchronous, ordered against `stream`."""
+        with self._ordered(stream):
+            check(self._L.jx_leader_prep_finish_device(self._h, batch_id, n, d_prep_msgs, d_peer_verdicts,
+                                                       d_out_verdicts),
+                  self._h, "jx_leader_prep_finish_device")
 
     def accumulate_device(self, batch_id: int, n: int, d_accept_mask: int | None = None, d_segments: int | None = None,
-                          segment_ids=(0,)):
-        """accumulate with device arrays: d_segments[i] indexes segment_ids. Asynchronous."""
+                          segment_ids=(0,), stream=None):
+        """accumulate with device arrays: d_segments[i] indexes segment_ids. Asynchronous, ordered
+        against `stream`."""
         ids, ptr = _seg_table(segment_ids)
-        check(self._L.jx_accumulate_device(self._h, batch_id, n, d_accept_mask, d_segments, ptr, ids.size), self._h,
-              "jx_accumulate_device")
+        with self._ordered(stream):
+            check(self._L.jx_accumulate_device(self._h, batch_id, n, d_accept_mask, d_segments, ptr, ids.size),
+                  self._h, "jx_accumulate_device")
 
     def prep_and_aggregate(self, nonces, public_shares, helper_input_shares, leader_prep_shares,
                            segment: int = 0, want_results: bool = True):
@@ -294,16 +384,17 @@ class HelperEngine:
     def prep_and_aggregate_device(self, d_nonces: int, d_public_shares: int | None, d_helper_input_shares: int,
                                   d_leader_prep_shares: int, n: int, segment: int = 0,
                                   d_out_prep_msgs: int | None = None, d_out_verdicts: int | None = None,
-                                  d_segments: int | None = None, segment_ids=None):
+                                  d_segments: int | None = None, segment_ids=None, stream=None):
         """Same, with inputs already resident in HBM (device pointers, e.g. tensor.data_ptr()).
         Every report goes to `segment`, or, with d_segments, report i to segment_ids[d_segments[i]].
-        Asynchronous: call sync() before reading outputs."""
+        Asynchronous, ordered against `stream` (default: torch's current stream), so outputs read on
+        that stream need no sync(); with stream=False call sync() (or join_stream) first."""
         ids, ptr = _seg_table([segment] if segment_ids is None else segment_ids)
-        self._seg_keep = ids  # the table is read during the call only; keep it alive anyway
-        st = self._L.jx_helper_prep_aggregate_device(self._h, n, d_nonces, d_public_shares, d_helper_input_shares,
-                                                     d_leader_prep_shares, d_segments, ptr, ids.size,
-                                                     d_out_prep_msgs, d_out_verdicts)
-        check(st, self._h, "jx_helper_prep_aggregate_device")
+        with self._ordered(stream):
+            st = self._L.jx_helper_prep_aggregate_device(self._h, n, d_nonces, d_public_shares, d_helper_input_shares,
+                                                         d_leader_prep_shares, d_segments, ptr, ids.size,
+                                                         d_out_prep_msgs, d_out_verdicts)
+            check(st, self._h, "jx_helper_prep_aggregate_device")
 
     # ------------------------------------------------------------------ aggregation state
     def aggregate_share(self, segment: int = 0) -> tuple[bytes, int, bytes]:
@@ -319,27 +410,31 @@ class HelperEngine:
     def reset_aggregates(self):
         check(self._L.jx_aggregate_reset(self._h), self._h, "jx_aggregate_reset")
 
-    def export_aggregate_device(self, segment: int, d_dst: int):
-        check(self._L.jx_aggregate_export_device(self._h, segment, d_dst), self._h, "jx_aggregate_export_device")
+    def export_aggregate_device(self, segment: int, d_dst: int, stream=None):
+        with self._ordered(stream):
+            check(self._L.jx_aggregate_export_device(self._h, segment, d_dst), self._h, "jx_aggregate_export_device")
 
-    def combine_device(self, d_parts: int, nparts: int, d_out: int):
-        check(self._L.jx_aggregate_combine_device(self._h, d_parts, nparts, d_out), self._h,
-              "jx_aggregate_combine_device")
+    def combine_device(self, d_parts: int, nparts: int, d_out: int, stream=None):
+        with self._ordered(stream):
+            check(self._L.jx_aggregate_combine_device(self._h, d_parts, nparts, d_out), self._h,
+                  "jx_aggregate_combine_device")
 
     def record_bytes(self) -> int:
         b = ctypes.c_uint32()
         check(self._L.jx_shard_record_bytes(self._h, ctypes.byref(b)), self._h, "jx_shard_record_bytes")
         return b.value
 
-    def export_record_device(self, segment: int, d_dst: int):
+    def export_record_device(self, segment: int, d_dst: int, stream=None):
         """Write this engine's shard record (agg share || count || checksum) to device memory."""
-        check(self._L.jx_shard_record_export_device(self._h, segment, d_dst), self._h,
-              "jx_shard_record_export_device")
+        with self._ordered(stream):
+            check(self._L.jx_shard_record_export_device(self._h, segment, d_dst), self._h,
+                  "jx_shard_record_export_device")
 
-    def combine_records_device(self, d_records: int, nrecords: int, d_out: int):
+    def combine_records_device(self, d_records: int, nrecords: int, d_out: int, stream=None):
         """Merge nrecords back-to-back shard records on the device (compute_aggregate_share)."""
-        check(self._L.jx_shard_record_combine_device(self._h, d_records, nrecords, d_out), self._h,
-              "jx_shard_record_combine_device")
+        with self._ordered(stream):
+            check(self._L.jx_shard_record_combine_device(self._h, d_records, nrecords, d_out), self._h,
+                  "jx_shard_record_combine_device")
 
     def set_capacity(self, reports: int):
         check(self._L.jx_engine_set_capacity(self._h, reports), self._h, "jx_engine_set_capacity")

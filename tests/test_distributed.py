@@ -124,3 +124,84 @@ def test_bench_refuses_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"],
                        env=dict(os.environ, WORLD_SIZE="3"), capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+
+
+def _bench_shard_rank(rank, world, port, name, R, q):
+    """One rank of bench.py's N > 1 verification on CPU: the rank's global reports [r R, (r+1) R) of the
+    cyclic pool tiling (here prepared by the oracle instead of the engine), its shard record checked
+    against bench.CyclicPool's expectation, the records all-gathered (gloo) and merged, the merge
+    checked against the expectation over every rank's range."""
+    try:
+        import sys
+
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import bench
+        from oracle import oracle as O
+
+        doc, K, nonces, ps, his, lps = _load(name)
+        v = doc["vdaf"]
+        vk = bytes.fromhex(doc["verify_key"])
+        orc = O.Prio3Oracle(v["algo_id"], v["bits"], v["length"], v["chunk_length"])
+        fb = orc.sizes.field_bytes
+        p = D.P64 if fb == 8 else D.P128
+        prep = lambda a, b: orc.helper_prep_batch(vk, nonces[a:b], ps[a:b], his[a:b], lps[a:b])  # noqa: E731
+        full = prep(0, K)
+        block = 3
+        blocks = [bench.field_elems(prep(b, min(K, b + block))["agg"], fb) for b in range(0, K, block)]
+        cyc = bench.CyclicPool(full["verdicts"] == 0, blocks, block, lambda a, r: bench.field_elems(prep(a, r)["agg"], fb), p)
+        start, stop = D.shard_range(R * world, rank, world)
+        idx = (start + np.arange(stop - start)) % K
+        mine = orc.helper_prep_batch(vk, nonces[idx], ps[idx], his[idx], lps[idx])  # what the rank's engine computes
+        exp, cnt = cyc.range(start, stop)
+        enc = b"".join(x.to_bytes(fb, "little") for x in exp)
+        own_ok = mine["agg"] == enc and mine["count"] == cnt
+        rec = torch.from_numpy(D.pack_record(mine["agg"], mine["count"], mine["checksum"]))
+        agg, count, _ = D.merge_records(D.all_gather_records(rec).numpy(), fb)
+        all_exp, all_cnt = cyc.range(0, R * world)
+        merged_ok = agg == b"".join(x.to_bytes(fb, "little") for x in all_exp) and count == all_cnt
+        # a rank that merged its own record twice instead of its neighbour's would not match
+        dup = D.merge_aggregate_shares([mine["agg"]] * world, fb)
+        q.put((rank, own_ok, merged_ok, dup != agg or world == 1, ""))
+        dist.destroy_process_group()
+    except Exception as e:  # surface the failure in the parent
+        q.put((rank, False, False, False, repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("name,R", [("sumvec_small.json", 23), ("count.json", 17)])
+def test_bench_distinct_shard_expectations(world, name, R):
+    """bench.py's N > 1 verification: ranks hold distinct global report ranges, and the expected rank
+    and merged aggregates follow from the range offsets (bench.CyclicPool), not from `x world`."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_shard_rank, args=(r, world, port, name, R, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, own_ok, merged_ok, distinct, err in out:
+        assert not err, err
+        assert own_ok and merged_ok and distinct, (rank, own_ok, merged_ok, distinct)
+
+
+def test_cyclic_pool_ranges_match_direct_sums():
+    """CyclicPool.range == the direct sum over the tiled range, for ranges crossing block and pool
+    boundaries (small integers instead of field elements)."""
+    import bench
+
+    rng = np.random.default_rng(3)
+    K, block, p = 11, 4, 2**61 - 1
+    vals = rng.integers(0, 1000, size=(K, 3))
+    fin = rng.random(K) < 0.8
+    contrib = [[int(x) if fin[i] else 0 for x in vals[i]] for i in range(K)]
+    blocks = [[sum(contrib[i][j] for i in range(b, min(K, b + block))) for j in range(3)] for b in range(0, K, block)]
+    partial = lambda a, r: [sum(contrib[i][j] for i in range(a, r)) for j in range(3)]  # noqa: E731
+    cyc = bench.CyclicPool(fin, blocks, block, partial, p)
+    for lo, hi in [(0, 0), (0, 5), (3, 9), (7, 30), (12, 13), (0, 44), (5, 100), (40, 41)]:
+        want = [sum(contrib[g % K][j] for g in range(lo, hi)) % p for j in range(3)]
+        assert cyc.range(lo, hi) == (want, sum(int(fin[g % K]) for g in range(lo, hi))), (lo, hi)
+        assert cyc.range(lo, hi, 3) == ([3 * w % p for w in want], 3 * sum(int(fin[g % K]) for g in range(lo, hi)))

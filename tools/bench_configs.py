@@ -89,8 +89,14 @@ def run(name, vdaf, meas_fn, R, K, steps, warmup, cpu_seconds, threads, cpu):
         for j in range(OL):
             acc[j] += m * int.from_bytes(outs[i, j].tobytes(), "little")
     exp = b"".join((x % p).to_bytes(fb, "little") for x in acc)
-    verified = agg == exp and count == total * int(mult[fin].sum()) and \
-        bool(np.array_equal(d_v.cpu().numpy(), np.tile(want["verdicts"], reps)[:R]))
+    got_v = d_v.cpu().numpy()
+    verdicts_ok = bool(np.array_equal(got_v, np.tile(want["verdicts"], reps)[:R]))
+    msgs_ok = True
+    if vdaf.prep_msg_len:  # every finished report's Finish{prep_msg} == the oracle's
+        f = got_v == 0
+        msgs_ok = bool(np.array_equal(d_m.cpu().numpy()[f], np.tile(want["prep_msgs"], (reps, 1))[:R][f]))
+    agg_ok = agg == exp and count == total * int(mult[fin].sum())
+    verified = agg_ok and verdicts_ok and msgs_ok
 
     # CPU baseline: the C++ CPU engine (cpu_baseline/jc_cpu_engine.cpp, byte-checked against the fixtures)
     # at 1 thread and at the host's thread budget on ~cpu_seconds of work each; the literal C oracle
@@ -128,8 +134,10 @@ def run(name, vdaf, meas_fn, R, K, steps, warmup, cpu_seconds, threads, cpu):
         "ms_per_step": round(dt / steps * 1e3, 3), "higher_is_better": True,
         "config": {"workload": name, "reports": R, "pool": K},
         "kernels": {"k1_ms_per_launch": per_launch("xof"), "k3_ms_per_launch": per_launch("flp"),
-                    "k4_ms_per_launch": per_launch("accumulate"), "launches_per_step": kt["xof"]["launches"] // steps},
+                    "k4_ms_per_launch": per_launch("accumulate"), "launches_per_step": kt["xof"]["launches"] // steps,
+                    "reports_per_launch": R * steps // max(1, kt["xof"]["launches"])},
         "verified": verified,
+        "verification": {"aggregate_and_count": agg_ok, "verdicts": verdicts_ok, "prep_msgs_of_finished_reports": msgs_ok},
         "cpu_baseline": {"value": round(rN, 1), "unit": "reports/s", "cores": cpu["threads"], "kind": "port",
                          "engine": "cpu_baseline/jc_cpu_engine.cpp", "value_1_thread": round(r1, 1),
                          "oracle_port_reports_per_s": round(r_oracle, 1), **cpu,

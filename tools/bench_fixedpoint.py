@@ -41,52 +41,47 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--bits", type=int, default=16)
-    ap.add_argument("--length", type=int, default=10000)
-    ap.add_argument("--reports", type=int, default=40960, help="reports per ping-pong job (both roles on the GPU)")
-    ap.add_argument("--role-reports", type=int, default=65536, help="reports per single-role step")
-    ap.add_argument("--pool", type=int, default=48)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--skip", default="", help="comma list of legs to skip: pingpong,pipelined,helper,leader,cpu")
-    ap.add_argument("--helper-staging-gb", type=int, default=-1,
-                    help="staging budget of the helper engine in the two-role legs (default: sized so one launch "
-                         "holds --reports; 0: the engine's own, 1/3 of HBM)")
-    ap.add_argument("--leader-staged", action="store_true",
-                    help="the leader stages its measurement share (debug option 6) instead of reading it in place")
-    a = ap.parse_args()
-    skip = set(filter(None, a.skip.split(",")))
-
-    import torch
-
-    from janus_amd.engine import HelperEngine
-    from janus_amd.vdaf import Prio3
-    from oracle import oracle as O  # input generation, checker and CPU baseline only
+def make_pool(bits, length, K, vk, threads):
+    """K distinct C-oracle client reports (shard + the leader's prepare_init) and the oracle's helper
+    results; 1 in 6 measurements claims a false norm (tests/golden/make_golden.py)."""
+    from oracle import oracle as O  # input generation and the checker only
     from tests.golden.make_golden import fixedpoint_measurements
 
-    threads = min(16, os.cpu_count() or 1)
-    vdaf = Prio3.fixedpoint_boundedl2_vec_sum(a.bits, a.length)
-    orc = O.Prio3Oracle(O.FIXEDPOINT_L2, a.bits, a.length, 0)
-    vk = bytes(range(16))
-    K = a.pool
+    orc = O.Prio3Oracle(O.FIXEDPOINT_L2, bits, length, 0)
     rng = np.random.default_rng(0x5EED)
-    meas = fixedpoint_measurements(a.bits, a.length, rng, K)
+    meas = fixedpoint_measurements(bits, length, rng, K)
     nonces = rng.integers(0, 256, size=(K, 16), dtype=np.uint8)
     rands = rng.integers(0, 256, size=(K, orc.sizes.client_rand), dtype=np.uint8)
-    t0 = time.perf_counter()
     shards = [orc.shard(meas[i], nonces[i].tobytes(), rands[i].tobytes()) for i in range(K)]
     ps, lis, his = (np.frombuffer(b"".join(s[k] for s in shards), np.uint8).reshape(K, -1) for k in range(3))
     lps = np.stack([np.frombuffer(orc.prep_init(vk, 0, nonces[i].tobytes(), ps[i].tobytes(), lis[i].tobytes())[1],
                                   np.uint8) for i in range(K)])
     want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=threads)
+    return orc, meas, nonces, ps, lis, his, lps, want
+
+
+def run(bits=16, length=10000, reports=40960, role_reports=65536, pool=48, steps=3, warmup=1, cpu_seconds=10.0,
+        skip=(), helper_staging_gb=-1):
+    """The configs[4] legs (ping-pong one job at a time, two jobs in flight, each role alone, CPU
+    baseline); returns one JSON-able dict. Every leg is verified against the oracle."""
+    import torch
+
+    from janus_amd.engine import HelperEngine
+    from janus_amd.vdaf import Prio3
+
+    skip = set(skip)
+    threads = min(16, os.cpu_count() or 1)
+    vdaf = Prio3.fixedpoint_boundedl2_vec_sum(bits, length)
+    vk = bytes(range(16))
+    K = pool
+    t0 = time.perf_counter()
+    orc, meas, nonces, ps, lis, his, lps, want = make_pool(bits, length, K, vk, threads)
+    pool_s = time.perf_counter() - t0
     fin = want["verdicts"] == 0
-    enc = meas.astype(object) ^ (1 << (a.bits - 1))
-    log(f"pool of {K} generated in {time.perf_counter() - t0:.1f}s; oracle verdicts {want['verdicts'].tolist()}")
+    enc = meas.astype(object) ^ (1 << (bits - 1))
+    log(f"pool of {K} generated in {pool_s:.1f}s; oracle verdicts {want['verdicts'].tolist()}")
     dev = torch.device("cuda", 0)
-    total = a.steps + a.warmup
+    total = steps + warmup
 
     def tile(x, R):
         x = np.ascontiguousarray(x)
@@ -97,61 +92,63 @@ def main():
     def tiled(x, R):
         return np.tile(x, -(-R // K))[:R]
 
-    def expected(R):
+    def expected(R, jobs):
         mult = np.bincount(np.arange(R) % K, minlength=K)
-        return ([int((enc[fin, j] * mult[fin]).sum()) * total % P128 for j in range(a.length)],
-                total * int(mult[fin].sum()))
+        return ([int((enc[fin, j] * mult[fin]).sum()) * jobs % P128 for j in range(length)],
+                jobs * int(mult[fin].sum()))
 
     def add_shares(*aggs):
-        return [sum(int.from_bytes(g[16 * j:16 * j + 16], "little") for g in aggs) % P128 for j in range(a.length)]
+        return [sum(int.from_bytes(g[16 * j:16 * j + 16], "little") for g in aggs) % P128 for j in range(length)]
 
     def per_launch(kt, stage):
         return round(kt[stage]["ms"] / max(1, kt[stage]["launches"]), 3)
 
-    if a.helper_staging_gb < 0:  # the helper stages its measurement share (16 B per element) plus ~10 %
-        a.helper_staging_gb = -(-int(a.reports * vdaf.meas_len * 16 * 1.15) // (1 << 30)) + 2
+    def msgs_ok(d_msgs, R):  # the helper's Finish{prep_msg} of every finished report == the oracle's
+        f = tiled(fin, R)
+        return bool(np.array_equal(d_msgs.cpu().numpy()[f], tiled(want["prep_msgs"], R)[f]))
+
+    if helper_staging_gb < 0:  # the helper stages its measurement share (16 B per element) plus ~10 %
+        helper_staging_gb = -(-int(reports * vdaf.meas_len * 16 * 1.15) // (1 << 30)) + 2
 
     def helper_engine():
-        if not a.helper_staging_gb:
+        if not helper_staging_gb:
             return HelperEngine(vdaf, vk)
-        os.environ["JX_STAGING_GB"] = str(a.helper_staging_gb)
+        os.environ["JX_STAGING_GB"] = str(helper_staging_gb)
         try:
             return HelperEngine(vdaf, vk)
         finally:
             del os.environ["JX_STAGING_GB"]
 
     def timed_steps(step, engines):
-        for _ in range(a.warmup):
+        for _ in range(warmup):
             step(False)
         for e in engines:
             e.timing(True)
         torch.cuda.synchronize()
         t = time.perf_counter()
-        for _ in range(a.steps):
+        for _ in range(steps):
             step(True)
         torch.cuda.synchronize()
         return time.perf_counter() - t
 
     out = {
-        "leader_measurement": "staged by K1" if a.leader_staged else "read in place by the FLP kernels",
         "metric": "leader+helper ping-pong reports/sec (prep_init+prep_next+aggregate, both roles), "
-                  f"Prio3FixedPointBoundedL2VecSum {a.bits}-bit length={a.length} (configs[4])",
-        "unit": "reports/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup, "higher_is_better": True,
+                  f"Prio3FixedPointBoundedL2VecSum {bits}-bit length={length} (configs[4])",
+        "unit": "reports/s", "n_gpus": 1, "steps": steps, "warmup": warmup, "higher_is_better": True,
         "data": f"synthetic: {K} distinct C-oracle client reports (1 in 6 with a false norm claim) tiled on device",
+        "pool_seconds": round(pool_s, 1),
     }
     verified = True
 
     # ---------------------------------------------------------------- ping-pong, both roles on one GPU
     if "pingpong" not in skip:
-        R = a.reports
+        R = reports
         d_n, d_ps, d_lis, d_his = tile(nonces, R), tile(ps, R), tile(lis, R), tile(his, R)
         d_lps = torch.empty((R, vdaf.prep_share_len), dtype=torch.uint8, device=dev)
         d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
         d_hv = torch.empty(R, dtype=torch.uint8, device=dev)
         d_lv = torch.empty(R, dtype=torch.uint8, device=dev)
         leader, helper = HelperEngine(vdaf, vk), helper_engine()
-        if a.leader_staged:
-            leader.debug(6, 1)
         role_s = {"leader_init": 0.0, "helper": 0.0, "leader_finish_acc": 0.0}
 
         def step(timed):
@@ -176,21 +173,21 @@ def main():
         kl, kh = leader.timing_read(), helper.timing_read()
         agg_l, cnt_l, cs_l = leader.aggregate_share(0)
         agg_h, cnt_h, cs_h = helper.aggregate_share(0)
-        exp, exp_count = expected(R)
+        exp, exp_count = expected(R, total)
         ok = add_shares(agg_l, agg_h) == exp and cnt_l == cnt_h == exp_count and cs_l == cs_h and \
             np.array_equal(d_hv.cpu().numpy(), tiled(want["verdicts"], R)) and \
-            np.array_equal(d_lv.cpu().numpy() == 0, tiled(fin, R))
+            np.array_equal(d_lv.cpu().numpy() == 0, tiled(fin, R)) and msgs_ok(d_msgs, R)
         verified &= bool(ok)
         leader.close()
         helper.close()
         del d_n, d_ps, d_lis, d_his, d_lps, d_msgs, d_hv, d_lv
         torch.cuda.empty_cache()
         out.update({
-            "value": round(R * a.steps / dt, 1), "ms_per_step": round(dt / a.steps * 1e3, 3),
-            "helper_reports_per_s_in_pingpong": round(R * a.steps / role_s["helper"], 1),
-            "role_ms_per_step": {k: round(v / a.steps * 1e3, 3) for k, v in role_s.items()},
-            "config": {"workload": f"FixedPointBoundedL2VecSum bitsize={a.bits} length={a.length}", "reports": R,
-                       "pool": K, "launches_per_step_helper": kh["xof"]["launches"] // a.steps},
+            "value": round(R * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 3),
+            "helper_reports_per_s_in_pingpong": round(R * steps / role_s["helper"], 1),
+            "role_ms_per_step": {k: round(v / steps * 1e3, 3) for k, v in role_s.items()},
+            "config": {"workload": f"FixedPointBoundedL2VecSum bitsize={bits} length={length}", "reports": R,
+                       "pool": K, "launches_per_step_helper": kh["xof"]["launches"] // steps},
             "kernels": {"helper": {s: per_launch(kh, s) for s in ("xof", "flp", "accumulate", "slow")},
                         "leader": {s: per_launch(kl, s) for s in ("xof", "flp", "accumulate")}},
             "pingpong_verified": bool(ok),
@@ -202,29 +199,34 @@ def main():
     # the two aggregators are independent processes: while the helper prepares job i-1 (helper engine,
     # its own stream), the leader initializes job i (leader engine, its own stream); then the leader
     # finishes job i-1. Each role alone leaves most SIMDs idle at these launch sizes (one report's sponge
-    # chain is serial), so the two roles' kernels run side by side.
+    # chain is serial), so the two roles' kernels run side by side. The engines are ordered by hand
+    # (stream=False): ordering both through torch's stream would serialize them. The inputs are resident
+    # before the first step; job i-1's leader prep shares are complete (leader.sync) before its helper step.
     if "pipelined" not in skip:
-        R = a.reports
+        R = reports
         d_n, d_ps, d_lis, d_his = tile(nonces, R), tile(ps, R), tile(lis, R), tile(his, R)
         d_lps = [torch.empty((R, vdaf.prep_share_len), dtype=torch.uint8, device=dev) for _ in range(2)]
         d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
         d_hv = torch.empty(R, dtype=torch.uint8, device=dev)
         d_lv = torch.empty(R, dtype=torch.uint8, device=dev)
         leader, helper = HelperEngine(vdaf, vk), helper_engine()
-        if a.leader_staged:
-            leader.debug(6, 1)
+        torch.cuda.synchronize()
         state = {"i": 0, "prev": None, "done": 0}
+        nf = False
 
         def pstep(timed):
             i = state["i"]
-            bid = leader.leader_init_device(R, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(), d_lps[i % 2].data_ptr())
+            bid = leader.leader_init_device(R, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(),
+                                            d_lps[i % 2].data_ptr(), stream=nf)
             if state["prev"] is not None:
                 helper.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(),
-                                                 d_lps[(i - 1) % 2].data_ptr(), R, 0, d_msgs.data_ptr(), d_hv.data_ptr())
+                                                 d_lps[(i - 1) % 2].data_ptr(), R, 0, d_msgs.data_ptr(),
+                                                 d_hv.data_ptr(), stream=nf)
             helper.sync()
             if state["prev"] is not None:
-                leader.leader_finish_device(state["prev"], R, d_msgs.data_ptr(), d_hv.data_ptr(), d_lv.data_ptr())
-                leader.accumulate_device(state["prev"], R)
+                leader.leader_finish_device(state["prev"], R, d_msgs.data_ptr(), d_hv.data_ptr(), d_lv.data_ptr(),
+                                            stream=nf)
+                leader.accumulate_device(state["prev"], R, stream=nf)
                 state["done"] += 1
             leader.sync()
             state["prev"] = bid
@@ -234,26 +236,26 @@ def main():
         dt = timed_steps(pstep, (leader, helper))
         # drain: the last job's helper step and leader finish (untimed)
         helper.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(),
-                                         d_lps[(state["i"] - 1) % 2].data_ptr(), R, 0, d_msgs.data_ptr(), d_hv.data_ptr())
+                                         d_lps[(state["i"] - 1) % 2].data_ptr(), R, 0, d_msgs.data_ptr(),
+                                         d_hv.data_ptr(), stream=nf)
         helper.sync()
-        leader.leader_finish_device(state["prev"], R, d_msgs.data_ptr(), d_hv.data_ptr(), d_lv.data_ptr())
-        leader.accumulate_device(state["prev"], R)
+        leader.leader_finish_device(state["prev"], R, d_msgs.data_ptr(), d_hv.data_ptr(), d_lv.data_ptr(), stream=nf)
+        leader.accumulate_device(state["prev"], R, stream=nf)
         leader.sync()
         jobs = state["done"] + 1
         kl, kh = leader.timing_read(), helper.timing_read()
         agg_l, cnt_l, cs_l = leader.aggregate_share(0)
         agg_h, cnt_h, cs_h = helper.aggregate_share(0)
-        mult = np.bincount(np.arange(R) % K, minlength=K)
-        exp = [int((enc[fin, j] * mult[fin]).sum()) * jobs % P128 for j in range(a.length)]
-        ok = add_shares(agg_l, agg_h) == exp and cnt_l == cnt_h == jobs * int(mult[fin].sum()) and cs_l == cs_h and \
+        exp, exp_count = expected(R, jobs)
+        ok = add_shares(agg_l, agg_h) == exp and cnt_l == cnt_h == exp_count and cs_l == cs_h and \
             np.array_equal(d_hv.cpu().numpy(), tiled(want["verdicts"], R)) and \
-            np.array_equal(d_lv.cpu().numpy() == 0, tiled(fin, R))
+            np.array_equal(d_lv.cpu().numpy() == 0, tiled(fin, R)) and msgs_ok(d_msgs, R)
         verified &= bool(ok)
         leader.close()
         helper.close()
         del d_n, d_ps, d_lis, d_his, d_lps, d_msgs, d_hv, d_lv
         torch.cuda.empty_cache()
-        out["pipelined"] = {"reports_per_s": round(R * a.steps / dt, 1), "ms_per_step": round(dt / a.steps * 1e3, 3),
+        out["pipelined"] = {"reports_per_s": round(R * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 3),
                             "reports_per_job": R, "jobs_in_flight": 2, "verified": bool(ok),
                             "kernels": {"helper": {s: per_launch(kh, s) for s in ("xof", "flp", "accumulate")},
                                         "leader": {s: per_launch(kl, s) for s in ("xof", "flp", "accumulate")}}}
@@ -261,7 +263,7 @@ def main():
 
     # ---------------------------------------------------------------- each role alone, full-device launch
     roles = {}
-    R = a.role_reports
+    R = role_reports
     if "helper" not in skip:
         d_n, d_ps, d_his, d_lps = tile(nonces, R), tile(ps, R), tile(his, R), tile(lps, R)
         d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
@@ -281,12 +283,13 @@ def main():
         dt = timed_steps(hstep, (helper,))
         kh = helper.timing_read()
         _, cnt_h, _ = helper.aggregate_share(0)
-        _, exp_count = expected(R)
-        ok = cnt_h == exp_count and np.array_equal(d_hv.cpu().numpy(), tiled(want["verdicts"], R))
+        _, exp_count = expected(R, total)
+        ok = cnt_h == exp_count and np.array_equal(d_hv.cpu().numpy(), tiled(want["verdicts"], R)) and \
+            msgs_ok(d_msgs, R)
         verified &= bool(ok)
-        roles["helper"] = {"reports_per_s": round(R * a.steps / dt, 1), "reports": R,
-                           "ms_per_step": round(dt / a.steps * 1e3, 3),
-                           "launches_per_step": kh["xof"]["launches"] // a.steps,
+        roles["helper"] = {"reports_per_s": round(R * steps / dt, 1), "reports": R,
+                           "ms_per_step": round(dt / steps * 1e3, 3),
+                           "launches_per_step": kh["xof"]["launches"] // steps,
                            "kernels_ms_per_launch": {s: per_launch(kh, s) for s in ("xof", "flp", "accumulate", "slow")},
                            "verified": bool(ok)}
         helper.close()
@@ -300,8 +303,6 @@ def main():
         d_hv = tile(want["verdicts"], R).reshape(R).contiguous()
         d_lv = torch.empty(R, dtype=torch.uint8, device=dev)
         leader = HelperEngine(vdaf, vk)
-        if a.leader_staged:
-            leader.debug(6, 1)
 
         def lstep(timed):
             bid = leader.leader_init_device(R, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(), d_lps.data_ptr())
@@ -312,12 +313,12 @@ def main():
         dt = timed_steps(lstep, (leader,))
         kl = leader.timing_read()
         _, cnt_l, _ = leader.aggregate_share(0)
-        _, exp_count = expected(R)
+        _, exp_count = expected(R, total)
         ok = cnt_l == exp_count and np.array_equal(d_lv.cpu().numpy() == 0, tiled(fin, R)) and \
             np.array_equal(d_lps[:K].cpu().numpy(), lps)  # prep shares == the oracle's prepare_init
         verified &= bool(ok)
-        roles["leader"] = {"reports_per_s": round(R * a.steps / dt, 1), "reports": R,
-                           "ms_per_step": round(dt / a.steps * 1e3, 3),
+        roles["leader"] = {"reports_per_s": round(R * steps / dt, 1), "reports": R,
+                           "ms_per_step": round(dt / steps * 1e3, 3),
                            "kernels_ms_per_launch": {s: per_launch(kl, s) for s in ("xof", "flp", "accumulate")},
                            "verified": bool(ok)}
         leader.close()
@@ -334,44 +335,69 @@ def main():
 
     # ---------------------------------------------------------------- CPU baseline
     if "cpu" not in skip:
-        # the C++ CPU engine's leader prep_init -> helper prep + aggregate -> leader finish + aggregate
-        # (cpu_baseline/jc_cpu_engine.cpp, byte-checked against the oracle) at 1 thread and at the host's
-        # thread budget; the literal C oracle (leader prep_init + helper prep) per core beside it
-        from bench import cpu_threads
-        from cpu_baseline import cpu_engine as CE
+        out["cpu_baseline"] = cpu_baseline(bits, length, vk, K, nonces, ps, lis, his, lps, want, orc, cpu_seconds,
+                                           vdaf.prep_share_len)
+    return out
 
-        cpu = cpu_threads()
 
-        def cpu_ping_pong(nth, m):
-            idx = np.arange(m) % K
-            t = time.perf_counter()
-            ld = CE.leader_prep_init(5, a.bits, a.length, 0, vk, nonces[idx], ps[idx], lis[idx], vdaf.prep_share_len,
-                                     nthreads=nth)
-            hp = CE.helper_prep_aggregate(5, a.bits, a.length, 0, vk, nonces[idx], ps[idx], his[idx],
-                                          ld["prep_shares"], nthreads=nth)
-            fn = CE.leader_finish_aggregate(5, a.bits, a.length, 0, nonces[idx], lis[idx], ld["seeds"], ld["verdicts"],
-                                            hp["prep_msgs"], hp["verdicts"], nthreads=nth)
-            dt_ = time.perf_counter() - t
-            assert np.array_equal(hp["verdicts"], want["verdicts"][idx]) and np.array_equal(fn["verdicts"] == 0, fin[idx])
-            return m / dt_, dt_
+def cpu_baseline(bits, length, vk, K, nonces, ps, lis, his, lps, want, orc, cpu_seconds, lps_len):
+    """The C++ CPU engine's leader prep_init -> helper prep + aggregate -> leader finish + aggregate
+    (cpu_baseline/jc_cpu_engine.cpp, byte-checked against the oracle) at 1 thread and at the host's
+    thread budget; the literal C oracle (leader prep_init + helper prep) per core beside it."""
+    from bench import cpu_threads
+    from cpu_baseline import cpu_engine as CE
 
-        r1, d1 = cpu_ping_pong(1, min(K, 8))
-        mN = max(cpu["threads"], int(a.cpu_seconds * r1 * cpu["threads"] * 0.8))
-        rN, dN = cpu_ping_pong(cpu["threads"], mN)
-        m = min(K, 2)
+    cpu = cpu_threads()
+    fin = want["verdicts"] == 0
+
+    def cpu_ping_pong(nth, m):
+        idx = np.arange(m) % K
         t = time.perf_counter()
-        for i in range(m):
-            orc.prep_init(vk, 0, nonces[i].tobytes(), ps[i].tobytes(), lis[i].tobytes())
-        th = time.perf_counter()
-        orc.helper_prep_batch(vk, nonces[:m], ps[:m], his[:m], lps[:m], nthreads=1)
-        per_l, per_h = (th - t) / m, (time.perf_counter() - th) / m
-        out["cpu_baseline"] = {
-            "value": round(rN, 2), "unit": "reports/s", "cores": cpu["threads"], "kind": "port",
-            "engine": "cpu_baseline/jc_cpu_engine.cpp (leader init + helper prep/aggregate + leader finish/aggregate, "
-                      "both roles)", "value_1_thread": round(r1, 2), **cpu,
-            "oracle_port_reports_per_s_1_core": round(1.0 / (per_l + per_h), 3),
-            "sample": f"{mN} reports at {cpu['threads']} threads ({dN:.1f} s), {min(K, 8)} at 1 thread ({d1:.1f} s); "
-                      f"C oracle {m} reports ({per_l * 1e3:.0f} + {per_h * 1e3:.0f} ms per report)"}
+        ld = CE.leader_prep_init(5, bits, length, 0, vk, nonces[idx], ps[idx], lis[idx], lps_len, nthreads=nth)
+        hp = CE.helper_prep_aggregate(5, bits, length, 0, vk, nonces[idx], ps[idx], his[idx], ld["prep_shares"],
+                                      nthreads=nth)
+        fn = CE.leader_finish_aggregate(5, bits, length, 0, nonces[idx], lis[idx], ld["seeds"], ld["verdicts"],
+                                        hp["prep_msgs"], hp["verdicts"], nthreads=nth)
+        dt_ = time.perf_counter() - t
+        assert np.array_equal(hp["verdicts"], want["verdicts"][idx]) and np.array_equal(fn["verdicts"] == 0, fin[idx])
+        return m / dt_, dt_
+
+    r1, d1 = cpu_ping_pong(1, min(K, 8))
+    mN = max(cpu["threads"], int(cpu_seconds * r1 * cpu["threads"] * 0.8))
+    rN, dN = cpu_ping_pong(cpu["threads"], mN)
+    m = min(K, 2)
+    t = time.perf_counter()
+    for i in range(m):
+        orc.prep_init(vk, 0, nonces[i].tobytes(), ps[i].tobytes(), lis[i].tobytes())
+    th = time.perf_counter()
+    orc.helper_prep_batch(vk, nonces[:m], ps[:m], his[:m], lps[:m], nthreads=1)
+    per_l, per_h = (th - t) / m, (time.perf_counter() - th) / m
+    return {
+        "value": round(rN, 2), "unit": "reports/s", "cores": cpu["threads"], "kind": "port",
+        "engine": "cpu_baseline/jc_cpu_engine.cpp (leader init + helper prep/aggregate + leader finish/aggregate, "
+                  "both roles)", "value_1_thread": round(r1, 2), **cpu,
+        "oracle_port_reports_per_s_1_core": round(1.0 / (per_l + per_h), 3),
+        "sample": f"{mN} reports at {cpu['threads']} threads ({dN:.1f} s), {min(K, 8)} at 1 thread ({d1:.1f} s); "
+                  f"C oracle {m} reports ({per_l * 1e3:.0f} + {per_h * 1e3:.0f} ms per report)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bits", type=int, default=16)
+    ap.add_argument("--length", type=int, default=10000)
+    ap.add_argument("--reports", type=int, default=40960, help="reports per ping-pong job (both roles on the GPU)")
+    ap.add_argument("--role-reports", type=int, default=65536, help="reports per single-role step")
+    ap.add_argument("--pool", type=int, default=48)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--skip", default="", help="comma list of legs to skip: pingpong,pipelined,helper,leader,cpu")
+    ap.add_argument("--helper-staging-gb", type=int, default=-1,
+                    help="staging budget of the helper engine in the two-role legs (default: sized so one launch "
+                         "holds --reports; 0: the engine's own, 1/3 of HBM)")
+    a = ap.parse_args()
+    out = run(a.bits, a.length, a.reports, a.role_reports, a.pool, a.steps, a.warmup, a.cpu_seconds,
+              set(filter(None, a.skip.split(","))), a.helper_staging_gb)
     print(json.dumps(out), flush=True)
 
 
