@@ -414,22 +414,30 @@ __device__ f128 bary_coeffs(uint4* coef, uint64_t blk, uint32_t NC, uint32_t lan
 // `cnt` (<= 2) Field128 samples from an XOF stream whose first block is in S. Fast path: the first
 // two 16-byte chunks, FLAG_SLOW if one is >= p; slow path: rejection sampling (a rejection stays in
 // the first block except with probability ~2^-600, beyond which chunks straddling blocks are skipped).
-__device__ void sample2_f128(uint32_t* S, f128 out[2], uint32_t cnt, bool slow, uint32_t& flags) {
+// Every index is static (the chunks are unrolled and a sample lands in out[0] / out[1] by select), so
+// the state and the samples stay in registers: a data-dependent index would put both in scratch.
+__device__ __forceinline__ void sample2_f128(uint32_t* S, f128 out[2], uint32_t cnt, bool slow, uint32_t& flags) {
   if (!slow) {
     out[0] = w4_to_f(S[0], S[1], S[2], S[3]);
     out[1] = w4_to_f(S[4], S[5], S[6], S[7]);
     if (ge_p128(out[0]) || (cnt > 1 && ge_p128(out[1]))) flags |= FLAG_SLOW;
     return;
   }
-  out[1] = make128(0, 0);
+  f128 o0 = make128(0, 0), o1 = make128(0, 0);
   uint32_t k = 0;
   for (int guard = 0; guard < 64 && k < cnt; guard++) {
-    for (int ci = 0; ci < 10 && k < cnt; ci++) {
-      f128 v = w4_to_f(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]);
-      if (!ge_p128(v)) out[k++] = v;
+#pragma unroll
+    for (int ci = 0; ci < 10; ci++) {
+      const f128 v = w4_to_f(S[4 * ci], S[4 * ci + 1], S[4 * ci + 2], S[4 * ci + 3]);
+      const bool take = k < cnt && !ge_p128(v);
+      if (take && k == 0) o0 = v;
+      if (take && k == 1) o1 = v;
+      k += take ? 1u : 0u;
     }
     if (k < cnt) keccak_p12(S);
   }
+  out[0] = o0;
+  out[1] = o1;
 }
 
 // Tail of the XOF stage shared by the fast and slow kernels: joint randomness,
@@ -2082,14 +2090,36 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
     wacc_zero(ao[i]);
   }
   acc_zero(sx);
+  // The leader reads its explicit measurement share in place (report-major rows, Bufs::meas_rs): per call
+  // the workgroup needs the W*PPW = 8 consecutive elements (128 bytes) of its slots from each of the 64
+  // rows. Loaded per lane as the staged layout is (one 16-byte element of 64 rows per instruction) every
+  // instruction touches 64 lines for 16 bytes each, and the other waves' parts of those lines come back
+  // from HBM once L1/L2 have dropped them (4.0 MB of traffic per FixedPoint 16 x 10000 report against
+  // 2.67 MB for the helper's staged stream). Here instruction q (wave q / PPW) reads rows 8q..8q+7 whole:
+  // lane l = 8 pp + a takes row 8q + a, part p = pp ^ (q & 1), so eight lanes cover one row's 128 bytes.
+  // The part swap on odd q puts rows r and r + 8 in opposite halves of a 256-byte LDS bank window, so the
+  // consumers' ds_read_b128 (16 lanes per pass, lane = row) stay conflict-free.
+  const bool inpl = LEADER && !HIST && b.meas_rs != 0;
   // loads of call k into ring slot (k - 1) % D
   auto issue = [&](uint32_t k) {
     const uint32_t sl = (k - 1) % D;
     if (wave < 2) glds16(coefb + (uint64_t)(COEF_K + 2 * (k - 1) + wave) * IL, &ring[sl][wave][0]);
+    if (inpl) {
+      static_assert(W * PPW == 8, "one 128-byte row segment per report per call");
 #pragma unroll
-    for (int i = 0; i < PPW; i++) {
-      const uint32_t e = (k - 1) * chunk + j0 + i;
-      glds16(real[i] && e < M ? &measb[e] : zero, &ring[sl][2 + wave * PPW + i][0]);
+      for (int u = 0; u < PPW; u++) {
+        const uint32_t q = wave * PPW + u, a = lane & 7u, p = (lane >> 3) ^ (q & 1u);
+        const uint32_t slot = wg * (W * PPW) + p, e = (k - 1) * chunk + slot;
+        const uint64_t r0 = blk * 64 + 8 * q + a, r = r0 < b.n ? r0 : b.n - 1;
+        const uint4* src = slot < chunk && e < M ? reinterpret_cast<const uint4*>(b.meas_src + r * b.meas_rs) + e : zero;
+        glds16(src, &ring[sl][2 + q][0]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < PPW; i++) {
+        const uint32_t e = (k - 1) * chunk + j0 + i;
+        glds16(real[i] && e < M ? &measb[e] : zero, &ring[sl][2 + wave * PPW + i][0]);
+      }
     }
   };
   // loads a wave issues per call: 1 (coefficient, waves 0/1) + PPW (measurement)
@@ -2105,6 +2135,14 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
   for (uint32_t k = 1; k < D && k <= kfw; k++) issue(k);
   const uint32_t ring_base = lds_addr(&ring[0][0][lane]);
   constexpr uint32_t SLOT_BYTES = ROWS * 64 * 16, ROW_BYTES = 64 * 16;
+  // this lane's measurement elements in a ring slot (relative to ring_base)
+  uint32_t xoff[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; i++) {
+    const uint32_t q = lane >> 3, p = wave * PPW + i;
+    xoff[i] = inpl ? (2 + q) * ROW_BYTES + ((8 * (p ^ (q & 1u)) + (lane & 7u)) * 16) - lane * 16
+                   : (2 + wave * PPW + i) * ROW_BYTES;
+  }
 #pragma unroll 1
   for (uint32_t k = 1; k <= kfw; k++) {
     wait_call(k + D - 2 > kfw);  // near the end fewer calls are in flight: wait for all
@@ -2113,8 +2151,7 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
     if (g < NG) {
       const uint32_t a = ring_base + ((k - 1) % D) * SLOT_BYTES;
       uint4 cv, dv, xv[PPW];
-      lds_read4(a, a + ROW_BYTES, a + (2 + wave * PPW) * ROW_BYTES, a + (3 + wave * PPW) * ROW_BYTES, cv, dv, xv[0],
-                xv[1]);
+      lds_read4(a, a + ROW_BYTES, a + xoff[0], a + xoff[1], cv, dv, xv[0], xv[1]);
       const limbs26 ck = to_limbs26(u4_to_f(cv));
       const limbs26 dk = to_limbs26(u4_to_f(dv));
 #pragma unroll

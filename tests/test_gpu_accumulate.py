@@ -452,3 +452,68 @@ def test_handler_batch_aggregations_with_writer():
         assert (r.aggregate_share, r.report_count, r.checksum) == (agg, cnt, cs)
         t = [times[i] for i in idx]
         assert r.client_timestamp_interval == Interval(min(t), max(t) + 1 - min(t))
+
+
+def test_leader_collected_batch_fails_at_init_and_batches_are_released():
+    """Leader with a BatchAggregationWriter: reports of an already collected batch fail with
+    BatchCollected at the initial write and are not sent to the helper (aggregation_job_writer.rs:
+    557-605); a mismatched helper response releases the job's engine batch; the finished job leaves no
+    resident batch behind."""
+    from janus_amd.aggregator import (LeaderReport, handle_aggregate_init, leader_aggregate_init,
+                                      leader_process_helper_response)
+    from janus_amd.batch_aggregation import AGGREGATING, BatchAggregation, BatchAggregationWriter
+    from janus_amd.messages import HpkeCiphertext, PrepareError, ReportMetadata
+
+    vdaf = Prio3.sum_vec(2, 10, 4)
+    vk = bytes(range(16))
+    n = 30
+    orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
+    rng = np.random.default_rng(77)
+    meas = rng.integers(0, 4, size=(n, vdaf.length), dtype=np.uint64)
+    nonces = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+    rands = rng.integers(0, 256, size=(n, orc.sizes.client_rand), dtype=np.uint8)
+    shards = [orc.shard(meas[i], nonces[i].tobytes(), rands[i].tobytes()) for i in range(n)]
+    reports = [LeaderReport(ReportMetadata(nonces[i].tobytes(), 1_700_000_000 + i), shards[i][0], shards[i][1],
+                            HpkeCiphertext(1, b"e", b"c")) for i in range(n)]
+    segs = [7 if i % 3 == 0 else 8 for i in range(n)]
+    w = BatchAggregationWriter(field_bytes=16)
+    w.datastore.rows[(7, 0)] = BatchAggregation(7, 0, state=AGGREGATING).collected()  # batch 7 was collected
+    with HelperEngine(vdaf, vk) as leader, HelperEngine(vdaf, vk) as helper:
+        step = leader_aggregate_init(leader, reports, segs, writer=w)
+        assert {i for i, e in step.failed.items() if e == PrepareError.BatchCollected} == {i for i in range(n)
+                                                                                          if segs[i] == 7}
+        assert all(segs[i] == 8 for i in step.stepped) and len(step.stepped) == sum(s == 8 for s in segs)
+        # a helper response that does not match the request: the step fails and its engine batch is released
+        with pytest.raises(ValueError):
+            leader_process_helper_response(leader, step, [], segs, writer=w)
+        assert leader.resident_batches()[0] == 0
+        # a fresh step of the same job goes through
+        w2 = BatchAggregationWriter(field_bytes=16)
+        step = leader_aggregate_init(leader, reports, segs, writer=w2)
+        hout = handle_aggregate_init(helper, step.prepare_inits, [shards[i][2] for i in step.stepped],
+                                     [segs[i] for i in step.stepped])
+        out = leader_process_helper_response(leader, step, hout.responses, segs, writer=w2)
+        assert out.finished.sum() == n and leader.resident_batches()[0] == 0 and helper.resident_batches()[0] == 0
+        assert w2.batch_aggregation(8).report_count == sum(s == 8 for s in segs)
+
+
+def test_helper_batch_keep_false_and_resident_scope():
+    """helper_initialized_batch(keep=False) leaves no resident batch; resident() releases on exit unless
+    accumulate consumed the batch; releasing a consumed batch is an error unless missing_ok."""
+    vdaf = Prio3.sum_vec(2, 10, 4)
+    vk = bytes(range(16))
+    orc, nonces, ps, his, lps = _batch(vdaf, vk, 40, seed=5)
+    with HelperEngine(vdaf, vk) as eng:
+        res = eng.helper_initialized_batch(nonces, ps, his, lps, keep=False)
+        assert res.batch_id == 0 and eng.resident_batches()[0] == 0
+        res = eng.helper_initialized_batch(nonces, ps, his, lps)
+        with eng.resident(res.batch_id):
+            assert eng.resident_batches()[0] == 1
+        assert eng.resident_batches()[0] == 0
+        res = eng.helper_initialized_batch(nonces, ps, his, lps)
+        with eng.resident(res.batch_id):
+            eng.accumulate(40, batch_id=res.batch_id)  # consumes it; the scope's release is a no-op
+        assert eng.resident_batches()[0] == 0
+        with pytest.raises(EngineError, match="no resident"):
+            eng.release(res.batch_id)
+        eng.release(res.batch_id, missing_ok=True)
