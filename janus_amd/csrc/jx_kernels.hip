@@ -2172,6 +2172,17 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
     }
   }
   if (g >= NG) return;
+#ifdef JX_K3_PROBE  // measurement build only (tools/k3_probe.sh): the ring without the group finish
+  {
+    uint64_t h = 0;
+#pragma unroll
+    for (int i = 0; i < PPW; i++)
+#pragma unroll
+      for (int q = 0; q < 9; q++) h ^= ae[i].col[q] ^ ao[i].col[q];
+    b.part[((blk * c.ngt + g) * 4) * IL + lane] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), 0, 0);
+    return;
+  }
+#endif
   psum_part_finish<PPW, HIST, LEADER>(c, b, blk, g, lane, C, ae, ao, sx);
 }
 

@@ -9,3 +9,4 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout
 tail -1 $OUT/pytest.log
 timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || { echo BENCH_FAIL; tail -20 $OUT/bench.err; exit 1; }
 tail -c 3000 $OUT/bench.json
+timeout -k 10 400 bash tools/k3_probe.sh gpurun_out/r04b/k3probe || { echo PROBE_FAIL; exit 1; }
