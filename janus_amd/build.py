@@ -52,8 +52,10 @@ def build(force: bool = False, verbose: bool = False, variant: str = "", defines
             raise RuntimeError(f"hipcc failed: {' '.join(cmd)}")
         if verbose and out:
             sys.stderr.write(out.decode())
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs
+    tmp = f"{out}.{os.getpid()}.tmp"  # link aside, then rename: a reader never sees a partial library
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     subprocess.run(cmd, check=True)
+    os.replace(tmp, out)
     for o in objs:
         os.remove(o)
     return out

@@ -794,6 +794,9 @@ __device__ __forceinline__ uint32_t lower_to_upper(uint32_t v) {
 
 template <bool WIDE>  // WIDE (bits > 32) carries 4 more truncation words: built for 2 waves/SIMD
 __global__ __launch_bounds__(64 * K1_WAVES, WIDE ? 2 : 4) void xof_lanes_kernel(Cfg c, Bufs b) {
+#ifdef JX_HELPER_PRIO  // measurement build: the helper's sponge waves win issue arbitration on shared SIMDs
+  __builtin_amdgcn_s_setprio(JX_HELPER_PRIO);
+#endif
   const uint32_t lane = threadIdx.x & 63;
   const bool jh = lane >= 32;
   const uint64_t gw = (uint64_t)blockIdx.x * K1_WAVES + (threadIdx.x >> 6);  // 32 reports per wave

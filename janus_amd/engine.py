@@ -186,8 +186,11 @@ class HelperEngine:
 
     def record_event(self, event):
         """Record a torch.cuda.Event (or hipEvent_t handle) on the engine stream."""
-        check(self._L.jx_engine_record_event(self._h, int(getattr(event, "cuda_event", event))), self._h,
-              "jx_engine_record_event")
+        h = int(getattr(event, "cuda_event", event))
+        if h == 0 and hasattr(event, "record"):  # torch creates its event on the first record
+            event.record()
+            h = int(event.cuda_event)
+        check(self._L.jx_engine_record_event(self._h, h), self._h, "jx_engine_record_event")
 
     @contextlib.contextmanager
     def _ordered(self, stream):

@@ -89,8 +89,8 @@ def run(bits=16, length=10000, reports=40960, role_reports=65536, pool=48, steps
         reps = -(-R // K)
         return torch.from_numpy(x2).to(dev).repeat(reps, 1)[:R].contiguous()
 
-    def tiled(x, R):
-        return np.tile(x, -(-R // K))[:R]
+    def tiled(x, R):  # host copy of tile(x, R): report g is pool report g % K
+        return np.asarray(x)[np.arange(R) % K]
 
     def expected(R, jobs):
         mult = np.bincount(np.arange(R) % K, minlength=K)
