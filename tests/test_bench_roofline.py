@@ -33,3 +33,18 @@ def test_pmc_summary_refused_on_other_sources(tmp_path, monkeypatch):
     traffic, _, _ = bench.pmc_traffic("jx::xof_kernel<0, false>", 500)
     assert traffic == 1_000_000_000  # 2e9 bytes over 1000 reports, scaled to 500
     assert bench.pmc_clock("jx::xof_kernel<0, false>") == 2.1
+
+
+def test_prio3_work_matches_sumvec_model_and_roofline_picks_dominant():
+    from janus_amd.vdaf import Prio3
+
+    g, s = bench.prio3_work(Prio3.sum_vec(8, 1000, 88)), bench.sumvec_work(8, 1000, 88)
+    assert g["perms"] == s["perms"] and abs(g["ops_k1"] - s["ops_k1"]) / s["ops_k1"] < 0.01
+    fp_h, fp_l = bench.prio3_work(Prio3.fixedpoint_boundedl2_vec_sum(16, 10000)), \
+        bench.prio3_work(Prio3.fixedpoint_boundedl2_vec_sum(16, 10000), "leader")
+    assert 30000 < fp_h["perms"] < 31000 and 15000 < fp_l["perms"] < 16000  # two sponges vs the absorb only
+    r = bench.issue_roofline(Prio3.sum(32), "helper", 1000, {"k1_ms_per_launch": 1.0, "k3_ms_per_launch": 2.0})
+    assert r["kernel"] == "K3 (FLP)" and 0 < r["frac"] < 1
+    r = bench.issue_roofline(Prio3.count(), "helper", 1000, {"k1_ms_per_launch": 1.0, "k3_ms_per_launch": 0.0})
+    assert r["kernel"] == "K1 (XOF)"
+    json.dumps(r)  # the bench line is JSON
