@@ -46,12 +46,12 @@ def build(force: bool = False, verbose: bool = False, variant: str = "", defines
         procs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), cmd))
         objs.append(obj)
     for p, cmd in procs:
-        out, _ = p.communicate()
+        log, _ = p.communicate()
         if p.returncode != 0:
-            sys.stderr.write(out.decode())
+            sys.stderr.write(log.decode())
             raise RuntimeError(f"hipcc failed: {' '.join(cmd)}")
-        if verbose and out:
-            sys.stderr.write(out.decode())
+        if verbose and log:
+            sys.stderr.write(log.decode())
     tmp = f"{out}.{os.getpid()}.tmp"  # link aside, then rename: a reader never sees a partial library
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     subprocess.run(cmd, check=True)

@@ -115,6 +115,7 @@ struct Bufs {
   uint8_t* msgs;
   const uint4* consts;
   uint32_t force_slow;  // debug: route every report through the slow XOF kernel
+  uint32_t k3_split;    // ParallelSum K3 (PPW 2, not Histogram): the group finish as its own kernel
   uint32_t k1_split;    // helper K1 kernel: 3 = lane-split (xof_lanes_kernel), 6 = lane pairs (xof_pairs_kernel,
                         // bits <= 32), otherwise the fused kernel
 };

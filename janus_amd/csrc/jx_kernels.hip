@@ -1842,6 +1842,9 @@ __global__ __launch_bounds__(256) void flp_sum_kernel(Cfg c, Bufs b) {
 // group) with guarded direct loads, then the wires at t, the leader's verifier share and the gadget
 // polynomial's share of v and G(t) for group g of block blk.
 template <int PPW, bool HIST, bool LEADER>
+__device__ __forceinline__ void psum_group_finish(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t g, uint32_t lane,
+                                                  const f128* E, const f128* O, f128 sxr);
+template <int PPW, bool HIST, bool LEADER>
 __device__ __forceinline__ void psum_part_finish(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t g, uint32_t lane,
                                                  uint32_t kf, wacc26* ae, wacc26* ao, acc192& sx) {
   const uint32_t NG = c.ngroups;
@@ -1874,6 +1877,27 @@ __device__ __forceinline__ void psum_part_finish(const Cfg& c, const Bufs& b, ui
       }
     }
   }
+  f128 E[PPW], O[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; i++) {
+    E[i] = wacc_reduce(ae[i]);
+    O[i] = wacc_reduce(ao[i]);
+  }
+  psum_group_finish<PPW, HIST, LEADER>(c, b, blk, g, lane, E, O, HIST ? acc_reduce(sx) : make128(0, 0));
+}
+
+// The group finish from the reduced wire sums E_i = (sum_k d_k x_{k,i}) R, O_i = (sum_k c_k x_{k,i}) R of
+// its PPW slots: wires at t (plus the leader's verifier share), this group's share of v and G(t), written
+// as the four partial sums of the group (Histogram: sxr = its sum of x).
+template <int PPW, bool HIST, bool LEADER>
+__device__ __forceinline__ void psum_group_finish(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t g, uint32_t lane,
+                                                  const f128* E, const f128* O, f128 sxr) {
+  const uint32_t NG = c.ngroups;
+  const uint64_t r0 = blk * 64 + lane;
+  const uint64_t r = r0 < b.n ? r0 : b.n - 1;
+  const uint32_t NC = c.ncoef, chunk = c.chunk, A = 2 * chunk;
+  const uint32_t j0 = g * PPW;
+  const uint4* coefb = b.coef + il_idx(blk, NC, 0, lane);
   // ---- wires at t for this group's slots, plus the leader's verifier share
   const f128 LR = u4_to_f(coefb[COEF_L * IL]), c0R = u4_to_f(coefb[COEF_C0 * IL]);
   const f128 hs = u4_to_f(coefb[COEF_HALFSUM * IL]);
@@ -1888,9 +1912,9 @@ __device__ __forceinline__ void psum_part_finish(const Cfg& c, const Bufs& b, ui
       // the sums are R-scaled (c_k, d_k are stored in Montgomery form): mont(sum, r^(j+1)) with the
       // canonical table power is E r^(j+1), and O = mont(sum, 1) (canonical)
       const f128 rpow = u4_to_f(coefb[(c.c_rpow + j) * IL]);
-      f128 Er = mont128(wacc_reduce(ae[i]), rpow), O = mont128(wacc_reduce(ao[i]), make128(1, 0));
+      f128 Er = mont128(E[i], rpow), Oc = mont128(O[i], make128(1, 0));
       f128 We = mont128(add128(mont128(se, c0R), Er), LR);
-      f128 Wo = mont128(sub128(add128(mont128(so, c0R), O), hs), LR);
+      f128 Wo = mont128(sub128(add128(mont128(so, c0R), Oc), hs), LR);
       if (LEADER) {  // the leader's verifier share: wire values at t
         if (r0 < b.n) {
           uint4* o = reinterpret_cast<uint4*>(b.lps_out + (uint64_t)c.lps_bytes * r);
@@ -1923,7 +1947,7 @@ __device__ __forceinline__ void psum_part_finish(const Cfg& c, const Bufs& b, ui
   pp[0] = f_to_u4(prod);
   pp[IL] = f_to_u4(vpart);
   pp[2 * IL] = f_to_u4(gpart);
-  if (HIST) pp[3 * IL] = f_to_u4(acc_reduce(sx));
+  if (HIST) pp[3 * IL] = f_to_u4(sxr);
   if (dfail && r0 < b.n) atomicOr(&b.flags[r0], FLAG_DFAIL);
 }
 
@@ -2186,7 +2210,37 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
     return;
   }
 #endif
+  if (!HIST && b.k3_split) {  // the group finish runs in flp_psum_finish_kernel: store the reduced sums
+    uint4* pp = b.part + ((blk * c.ngt + g) * 4) * IL + lane;
+#pragma unroll
+    for (int i = 0; i < PPW; i++) {
+      pp[(2 * i) * IL] = f_to_u4(wacc_reduce(ae[i]));
+      pp[(2 * i + 1) * IL] = f_to_u4(wacc_reduce(ao[i]));
+    }
+    return;
+  }
   psum_part_finish<PPW, HIST, LEADER>(c, b, blk, g, lane, C, ae, ao, sx);
+}
+
+// The group finish as its own pass (Bufs::k3_split): one wave per (64-report block, slot group), the
+// XCD-aware map of the part kernels, reading the reduced wire sums the ring kernel left in the group's
+// partial slots and overwriting them with the partials.
+template <int PPW, bool LEADER>
+__global__ __launch_bounds__(64) void flp_psum_finish_kernel(Cfg c, Bufs b) {
+  const uint32_t NG = c.ngroups;
+  const uint32_t bid = blockIdx.x, xcd = bid & 7u, q = bid >> 3;
+  const uint32_t g = q % NG;
+  const uint64_t blk = (uint64_t)(q / NG) * 8 + xcd;
+  if (blk >= (b.n + 63) / 64) return;
+  const uint32_t lane = threadIdx.x;
+  const uint4* pp = b.part + ((blk * c.ngt + g) * 4) * IL + lane;
+  f128 E[PPW], O[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; i++) {
+    E[i] = u4_to_f(pp[(2 * i) * IL]);
+    O[i] = u4_to_f(pp[(2 * i + 1) * IL]);
+  }
+  psum_group_finish<PPW, false, LEADER>(c, b, blk, g, lane, E, O, make128(0, 0));
 }
 
 template <bool HIST, bool LEADER>
@@ -2958,6 +3012,8 @@ static void launch_psum_part(const Cfg& c, const Bufs& b, hipStream_t s, uint32_
   if constexpr (PPW == 2) {
     const uint32_t g2 = grid / c.ngroups * ((c.ngroups + K3W - 1) / K3W);
     hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
+    if (!HIST && b.k3_split)
+      hipLaunchKernelGGL((flp_psum_finish_kernel<PPW, LEADER>), dim3(grid), dim3(64), 0, s, c, b);
   } else {
     hipLaunchKernelGGL((flp_psum_part_kernel<PPW, HIST, LEADER>), dim3(grid), dim3(64), 0, s, c, b);
   }

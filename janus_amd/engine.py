@@ -331,7 +331,8 @@ class HelperEngine:
                    batch_id: int | None = None):
         """Merge the finished output shares of a prepared batch into the engine's running batch
         aggregations and release the batch (at most once per batch). segments[i]: the
-        batch-aggregation id (any u32) of report i. batch_id defaults to the last prepared batch."""
+        batch-aggregation id (any u32) of report i. batch_id defaults to the last prepared batch,
+        which is only meaningful on an engine one thread uses: threads sharing an engine pass it."""
         m = None if accept_mask is None else np.ascontiguousarray(accept_mask, dtype=np.uint8)
         s = None if segments is None else np.ascontiguousarray(segments, dtype=np.uint32)
         bid = self.batch_id() if batch_id is None else batch_id
