@@ -283,8 +283,7 @@ int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]);
  *   option 2: accumulate report chunks, 1..4096 (frees the staging);
  *   option 3: helper K1 kernel: 0 automatic (the fused two-sponge kernel; the lane-split kernel for
  *             launches under one fused wave per SIMD; the lane-pair kernel under one lane-split wave
- *             per SIMD), 3 lane-split, 5 fused, 6 lane pairs (bits <= 32);
- *   option 4: ParallelSum K3 group finish: 0 inside the ring kernel, 1 as its own kernel.
+ *             per SIMD), 3 lane-split, 5 fused, 6 lane pairs (bits <= 32).
  * The environment variable JX_K1_SPLIT sets option 3 at create. */
 int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value);
 

@@ -126,7 +126,6 @@ struct jx_engine {
   uint64_t launches[NST] = {0, 0, 0, 0};
   uint32_t force_slow = 0;
   uint32_t k1_split = 0;  // helper K1: 0 automatic, 3 lane-split, 5 fused, 6 lane pairs (JX_K1_SPLIT, debug option 3)
-  uint32_t k3_split = 0;  // debug option 4: the K3 group finish as its own kernel
   // producer / consumer ordering (jx_engine_wait_stream / jx_engine_join_stream): reused events
   hipEvent_t ev_wait = nullptr, ev_join = nullptr;
 };
@@ -730,7 +729,6 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
   b.consts = e->d_consts;
   b.force_slow = e->force_slow;
   b.k1_split = e->k1_split;
-  b.k3_split = e->k3_split;
   // A helper launch that would give the fused two-sponge K1 less than one wave per SIMD is bound by
   // the per-report sponge latency, not by issue: the lane-split kernel runs it in twice the waves
   // (FixedPointBoundedL2VecSum 16 x 10000, 24,576 reports: 153 -> 92 ms on MI355X), and below one
@@ -1061,7 +1059,6 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
   // reports in flight: grow the budget toward one full K1 round, up to 1/3 of the device memory
   // (two engines, e.g. leader and helper, still fit on one MI355X). JX_STAGING_GB / JX_CHUNK_REPORTS override.
   const uint64_t per = per_report_bytes(e->cfg);
-  if (const char* env = getenv("JX_K3_SPLIT")) e->k3_split = atoi(env) == 1 ? 1u : 0u;
   if (const char* env = getenv("JX_K1_SPLIT")) {
     const int v = atoi(env);
     if (v == 0 || v == 3 || v == 5 || v == 6) e->k1_split = (uint32_t)v;
@@ -1783,11 +1780,6 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
     // 0: automatic (fused; lane-split below one fused wave per SIMD, lane pairs below one lane-split
     // wave per SIMD), 3: lane-split, 5: fused, 6: lane pairs (bits <= 32)
     e->k1_split = (uint32_t)value;
-    return JX_OK;
-  }
-  if (option == 4) {  // K3 group finish: 0 in the ring kernel, 1 its own kernel
-    if (value != 0 && value != 1) return JX_E_INVALID;
-    e->k3_split = (uint32_t)value;
     return JX_OK;
   }
   if (option == 2) {  // accumulate chunking (tests)

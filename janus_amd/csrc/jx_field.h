@@ -445,11 +445,28 @@ JX_HD f128 wacc_reduce(wacc26 a) {
   // flush: the top limb may hold up to 64 bits beyond position 208
   if (oi < 5) o[oi++] = buf_lo;
   if (oi < 5) o[oi++] = buf_hi;
-  // Horner from the top word: r = (r * 2^64 + o[i]) mod p
-  f128 r = make128(0, 0);
-#pragma unroll
-  for (int i = 4; i >= 0; i--) r = reduce192(o[i], r.lo, r.hi);
-  return r;
+  // Straight-line fold (value < 2^272, so o4 < 2^16). Mod p, 2^128 = 28 2^64 - 1, 2^192 = 783 2^64 - 28,
+  // 2^256 = 21896 2^64 - 783, hence
+  //   V = (o0 - S) + 2^64 H,  S = o2 + 28 o3 + 783 o4 (< 2^70),  H = o1 + 28 o2 + 783 o3 + 21896 o4 (< 2^74);
+  // T = H 2^64 + o0 - S is >= 0 (H 2^64 >= S whenever S > 0) and < 2^139; folding T's bits >= 2^128 (t2 <
+  // 2^11) once more leaves U < 2^128 + 2^80 < 2p, and one conditional subtraction makes it canonical. (The
+  // Horner form with reduce192's data-dependent loop cost ~250 VALU; this ~70.)
+  typedef unsigned __int128 u128;
+  const u128 S = (u128)o[2] + (u128)o[3] * 28u + (u128)o[4] * 783u;
+  const u128 H = (u128)o[1] + (u128)o[2] * 28u + (u128)o[3] * 783u + (u128)o[4] * 21896u;
+  const u128 Tlo = ((u128)(uint64_t)H << 64) | o[0];  // H 2^64 + o0 = t2 2^128 + Tlo
+  uint64_t t2 = (uint64_t)(H >> 64);
+  const u128 T = Tlo - S;
+  t2 -= (uint64_t)(Tlo < S);
+  const u128 add = (u128)(28u * t2) << 64;  // t2 2^128 = 28 t2 2^64 - t2
+  u128 U = T + add;
+  uint32_t top = U < add;
+  const u128 U2 = U - t2;
+  top -= (uint32_t)(U < (u128)t2);
+  const u128 P = ((u128)P128_HI << 64) | P128_LO;
+  const u128 D = U2 - P;
+  const u128 R = (top || U2 >= P) ? D : U2;
+  return make128((uint64_t)R, (uint64_t)(R >> 64));
 }
 
 // ----------------------------------------------------------------------------

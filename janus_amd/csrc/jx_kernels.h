@@ -63,14 +63,16 @@ struct Cfg {
   uint32_t coef1;       // first coefficient slot of gadget 1 (G1_* below)
   uint32_t c_omega1, c_S1;  // constant-table offsets of gadget 1's roots and S1_m
   // ParallelSum(Mul) gadget 0 (SumVec, Histogram, FixedPoint): per-report power tables K1 writes so that
-  // the FLP group finish needs no exponentiation: c_rpow + j = r^(j+1) canonical (j < chunk), c_tpow + g
+  // the FLP group finish needs no exponentiation: c_rpow + j = L r^(j+1) canonical (j < chunk), c_tpow + g
   // = t^(g * per) R, per = ceil(gpoly_len / ngroups) (the group's first gadget-polynomial coefficient)
   uint32_t c_rpow, c_tpow;
 };
 
-// coefficient slots (Montgomery form unless noted) for the ParallelSum / Sum FLP
+// coefficient slots (Montgomery form unless noted) for the ParallelSum / Sum FLP. Prio3Sum: as named;
+// ParallelSum (SumVec, Histogram, FixedPoint gadget 0) stores them scaled by L for the group finish:
+// COEF_L = L canonical, COEF_C0 = c_0 L R, COEF_HALFSUM = L (1/2) sum c_k canonical (xof_tail)
 enum : uint32_t {
-  COEF_L = 0,        // (t^P - 1)/P
+  COEF_L = 0,        // L = (t^P - 1)/P
   COEF_C0 = 1,       // c_0 = 1/(t - 1)
   COEF_HALFSUM = 2,  // (1/2) * sum_{k>=1} c_k   [canonical]
   COEF_T = 3,        // t
@@ -115,7 +117,6 @@ struct Bufs {
   uint8_t* msgs;
   const uint4* consts;
   uint32_t force_slow;  // debug: route every report through the slow XOF kernel
-  uint32_t k3_split;    // ParallelSum K3 (PPW 2, not Histogram): the group finish as its own kernel
   uint32_t k1_split;    // helper K1 kernel: 3 = lane-split (xof_lanes_kernel), 6 = lane pairs (xof_pairs_kernel,
                         // bits <= 32), otherwise the fused kernel
 };

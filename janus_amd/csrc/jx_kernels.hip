@@ -531,13 +531,22 @@ __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t
   const uint32_t stride = c.algo == ALGO_SUM ? 1u : 2u;
   const f128 rcR = mpow(rR, c.chunk);  // r^chunk (ParallelSum's d_k = c_k r^((k-1) chunk))
   const f128 sumc = bary_coeffs(coef, blk, NC, lane, tR, omega, C, COEF_C0, COEF_K, stride, c.algo != ALGO_SUM, rcR);
-  // (1/2) * sum c_k, canonical: mont(sumc*R, 1/2) = sumc/2
-  st_il(coef, blk, NC, COEF_HALFSUM, lane, mont128(sumc, u4_to_f(misc[1])));
+  if (c.algo == ALGO_SUM) {
+    // (1/2) * sum c_k, canonical: mont(sumc*R, 1/2) = sumc/2
+    st_il(coef, blk, NC, COEF_HALFSUM, lane, mont128(sumc, u4_to_f(misc[1])));
+  } else {
+    // the ParallelSum group finish (psum_group_finish) takes its constants scaled by L, so a wire at t costs
+    // two products instead of three: COEF_C0 <- c_0 L R, COEF_L <- L canonical, COEF_HALFSUM <- L (sum c_k)/2
+    // canonical; below, its power table holds L r^(j+1) (the chain starts from L r: mont(L R, r) = L r)
+    const f128 c0R = ld_il(coef, blk, NC, COEF_C0, lane);
+    st_il(coef, blk, NC, COEF_C0, lane, mont128(c0R, LR));
+    st_il(coef, blk, NC, COEF_L, lane, mont128(LR, make128(1, 0)));
+    st_il(coef, blk, NC, COEF_HALFSUM, lane, mont128(mont128(sumc, LR), u4_to_f(misc[1])));
+  }
   if (c.algo != ALGO_SUM) {
-    // power tables of the ParallelSum group finish (psum_part_finish): r^(j+1) canonical for the even
-    // wires of slot j (a chain of mont products starting from the canonical r), and t^(g * per) R for
-    // group g's share of G(t)
-    f128 rj = jr[0];
+    // power tables of the ParallelSum group finish: L r^(j+1) canonical for the even wires of slot j (a chain
+    // of mont products from L r), and t^(g * per) R for group g's share of G(t)
+    f128 rj = mont128(LR, jr[0]);
     for (uint32_t j = 0; j < c.chunk; j++) {
       st_il(coef, blk, NC, c.c_rpow + j, lane, rj);
       rj = mont128(rj, rR);
@@ -794,9 +803,6 @@ __device__ __forceinline__ uint32_t lower_to_upper(uint32_t v) {
 
 template <bool WIDE>  // WIDE (bits > 32) carries 4 more truncation words: built for 2 waves/SIMD
 __global__ __launch_bounds__(64 * K1_WAVES, WIDE ? 2 : 4) void xof_lanes_kernel(Cfg c, Bufs b) {
-#ifdef JX_HELPER_PRIO  // measurement build: the helper's sponge waves win issue arbitration on shared SIMDs
-  __builtin_amdgcn_s_setprio(JX_HELPER_PRIO);
-#endif
   const uint32_t lane = threadIdx.x & 63;
   const bool jh = lane >= 32;
   const uint64_t gw = (uint64_t)blockIdx.x * K1_WAVES + (threadIdx.x >> 6);  // 32 reports per wave
@@ -1898,9 +1904,13 @@ __device__ __forceinline__ void psum_group_finish(const Cfg& c, const Bufs& b, u
   const uint32_t NC = c.ncoef, chunk = c.chunk, A = 2 * chunk;
   const uint32_t j0 = g * PPW;
   const uint4* coefb = b.coef + il_idx(blk, NC, 0, lane);
-  // ---- wires at t for this group's slots, plus the leader's verifier share
-  const f128 LR = u4_to_f(coefb[COEF_L * IL]), c0R = u4_to_f(coefb[COEF_C0 * IL]);
-  const f128 hs = u4_to_f(coefb[COEF_HALFSUM * IL]);
+  // ---- wires at t for this group's slots, plus the leader's verifier share. K1 scaled the constants by
+  // L (xof_tail): Lc = L canonical, c0LR = c_0 L R, hsL = L (sum c_k)/2, rpowL_j = L r^(j+1), so
+  //   wire_even(t) = L (c_0 se + r^(j+1) sum_k d_k x) = mont(se, c0LR) + mont(E, rpowL_j)
+  //   wire_odd(t)  = L (c_0 so + sum_k c_k x - (sum c_k)/2) = mont(so, c0LR) + mont(O, Lc) - hsL
+  // (E, O are R-scaled: c_k, d_k are stored in Montgomery form).
+  const f128 Lc = u4_to_f(coefb[COEF_L * IL]), c0LR = u4_to_f(coefb[COEF_C0 * IL]);
+  const f128 hsL = u4_to_f(coefb[COEF_HALFSUM * IL]);
   bool dfail = false;
   f128 prod = make128(0, 0);
 #pragma unroll
@@ -1909,12 +1919,9 @@ __device__ __forceinline__ void psum_group_finish(const Cfg& c, const Bufs& b, u
     if (j < chunk) {
       f128 se = ld_il(b.proof, blk, c.proof_len, 2 * j, lane);
       f128 so = ld_il(b.proof, blk, c.proof_len, 2 * j + 1, lane);
-      // the sums are R-scaled (c_k, d_k are stored in Montgomery form): mont(sum, r^(j+1)) with the
-      // canonical table power is E r^(j+1), and O = mont(sum, 1) (canonical)
-      const f128 rpow = u4_to_f(coefb[(c.c_rpow + j) * IL]);
-      f128 Er = mont128(E[i], rpow), Oc = mont128(O[i], make128(1, 0));
-      f128 We = mont128(add128(mont128(se, c0R), Er), LR);
-      f128 Wo = mont128(sub128(add128(mont128(so, c0R), Oc), hs), LR);
+      const f128 rpowL = u4_to_f(coefb[(c.c_rpow + j) * IL]);
+      const f128 We = add128(mont128(se, c0LR), mont128(E[i], rpowL));
+      const f128 Wo = sub128(add128(mont128(so, c0LR), mont128(O[i], Lc)), hsL);
       if (LEADER) {  // the leader's verifier share: wire values at t
         if (r0 < b.n) {
           uint4* o = reinterpret_cast<uint4*>(b.lps_out + (uint64_t)c.lps_bytes * r);
@@ -2210,37 +2217,7 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
     return;
   }
 #endif
-  if (!HIST && b.k3_split) {  // the group finish runs in flp_psum_finish_kernel: store the reduced sums
-    uint4* pp = b.part + ((blk * c.ngt + g) * 4) * IL + lane;
-#pragma unroll
-    for (int i = 0; i < PPW; i++) {
-      pp[(2 * i) * IL] = f_to_u4(wacc_reduce(ae[i]));
-      pp[(2 * i + 1) * IL] = f_to_u4(wacc_reduce(ao[i]));
-    }
-    return;
-  }
   psum_part_finish<PPW, HIST, LEADER>(c, b, blk, g, lane, C, ae, ao, sx);
-}
-
-// The group finish as its own pass (Bufs::k3_split): one wave per (64-report block, slot group), the
-// XCD-aware map of the part kernels, reading the reduced wire sums the ring kernel left in the group's
-// partial slots and overwriting them with the partials.
-template <int PPW, bool LEADER>
-__global__ __launch_bounds__(64) void flp_psum_finish_kernel(Cfg c, Bufs b) {
-  const uint32_t NG = c.ngroups;
-  const uint32_t bid = blockIdx.x, xcd = bid & 7u, q = bid >> 3;
-  const uint32_t g = q % NG;
-  const uint64_t blk = (uint64_t)(q / NG) * 8 + xcd;
-  if (blk >= (b.n + 63) / 64) return;
-  const uint32_t lane = threadIdx.x;
-  const uint4* pp = b.part + ((blk * c.ngt + g) * 4) * IL + lane;
-  f128 E[PPW], O[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; i++) {
-    E[i] = u4_to_f(pp[(2 * i) * IL]);
-    O[i] = u4_to_f(pp[(2 * i + 1) * IL]);
-  }
-  psum_group_finish<PPW, false, LEADER>(c, b, blk, g, lane, E, O, make128(0, 0));
 }
 
 template <bool HIST, bool LEADER>
@@ -3012,8 +2989,6 @@ static void launch_psum_part(const Cfg& c, const Bufs& b, hipStream_t s, uint32_
   if constexpr (PPW == 2) {
     const uint32_t g2 = grid / c.ngroups * ((c.ngroups + K3W - 1) / K3W);
     hipLaunchKernelGGL((flp_psum_part_glds_kernel<PPW, HIST, LEADER, 4>), dim3(g2), dim3(64 * K3W), 0, s, c, b);
-    if (!HIST && b.k3_split)
-      hipLaunchKernelGGL((flp_psum_finish_kernel<PPW, LEADER>), dim3(grid), dim3(64), 0, s, c, b);
   } else {
     hipLaunchKernelGGL((flp_psum_part_kernel<PPW, HIST, LEADER>), dim3(grid), dim3(64), 0, s, c, b);
   }

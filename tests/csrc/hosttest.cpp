@@ -38,6 +38,12 @@ void ht_f128(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
   st(out, r);
 }
 void ht_reduce192(const uint64_t w[3], uint8_t* out) { st(out, reduce192(w[0], w[1], w[2])); }
+// wacc_reduce of nine raw column sums (each < 2^63, the wire-sum bound)
+void ht_wacc_reduce(const uint64_t cols[9], uint8_t* out) {
+  wacc26 a;
+  for (int s = 0; s < 9; s++) a.col[s] = cols[s];
+  st(out, wacc_reduce(a));
+}
 void ht_reduce192_small(const uint64_t w[3], uint8_t* out) { st(out, reduce192_small(w[0], w[1], w[2])); }
 void ht_mont_lazy(const uint8_t* a, const uint8_t* b, uint64_t out[3]) {
   uint64_t lo, hi;

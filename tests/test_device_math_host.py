@@ -32,6 +32,7 @@ def ht():
     L.ht_reduce192.argtypes = [vp, vp]
     L.ht_reduce192_small.argtypes = [vp, vp]
     L.ht_wide_dot.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp]
+    L.ht_wacc_reduce.argtypes = [vp, vp]
     L.ht_x25519.argtypes = [vp, vp, vp]
     L.ht_fe.argtypes = [ctypes.c_int, vp, vp, vp]
     L.ht_aes128.argtypes = [vp, vp, vp]
@@ -167,6 +168,20 @@ def test_xof_block_builder(ht, usage, binder):
         blk = bytearray(msg) + b"\x01" + bytes(168 - len(msg) - 1)
         blk[-1] ^= 0x80
         assert b"".join(x.to_bytes(4, "little") for x in w) == bytes(blk)
+
+
+def test_wacc_reduce_columns(ht):
+    """wacc_reduce's straight-line fold on raw column sums: every column up to 2^63 (the kernels' bound:
+    <= 5 * 512 limb products < 2^52 per column between normalisations), zeros, and random mixes."""
+    rnd = random.Random(11)
+    cases = [[0] * 9, [2**63 - 1] * 9, [2**26 - 1] * 8 + [2**63 - 1], [0] * 8 + [2**63 - 1], [1] + [0] * 8,
+             [2**63 - 1] + [0] * 8, [0, 0, 0, 0, 0, 2**63 - 1, 0, 0, 0]]
+    cases += [[rnd.randrange(2**63) for _ in range(9)] for _ in range(300)]
+    cases += [[rnd.choice([0, 2**26 - 1, 2**63 - 1, rnd.randrange(2**63)]) for _ in range(9)] for _ in range(300)]
+    for cols in cases:
+        out = ctypes.create_string_buffer(16)
+        ht.ht_wacc_reduce((ctypes.c_uint64 * 9)(*cols), out)
+        assert int.from_bytes(out.raw, "little") == sum(c << (26 * s) for s, c in enumerate(cols)) % P128, cols
 
 
 @pytest.mark.parametrize("n,norm", [(1, 0), (91, 0), (700, 0), (2000, 512), (5000, 512)])

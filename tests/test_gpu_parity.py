@@ -291,9 +291,8 @@ def test_k1_split_variants(name, split):
         np.testing.assert_array_equal(res.verdicts, want["verdicts"])
 
 
-@pytest.mark.parametrize("k3_split", [0, 1])
 @pytest.mark.parametrize("name", ["sumvec_8x1000_88", "histogram_256_16", "sumvec_64x20_9", "sumvec_small"])
-def test_k3_ring_padded_groups(name, k3_split):
+def test_k3_ring_padded_groups(name):
     """The ParallelSum FLP part kernel (the depth-4 LDS-DMA ring, 4 slot groups per workgroup) == the
     oracle, helper (verdicts, messages, output shares, aggregate) and leader (prep shares).
     sumvec_64x20_9 and sumvec_small have a padded last group and workgroup."""
@@ -304,7 +303,6 @@ def test_k3_ring_padded_groups(name, k3_split):
     nonces, ps, his, lps = _random_batch(orc, vk, n, seed=231 + sum(map(ord, name)))
     want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
     with HelperEngine(vdaf, vk) as eng:
-        eng.debug(4, k3_split)  # the group finish in the ring kernel (0) or as its own kernel (1)
         res = eng.helper_initialized_batch(nonces, ps, his, lps, want_out_shares=True)
         np.testing.assert_array_equal(res.verdicts, want["verdicts"])
         fin = want["verdicts"] == 0
@@ -320,7 +318,6 @@ def test_k3_ring_padded_groups(name, k3_split):
     shards = [orc.shard(meas[i], ln[i].tobytes(), rands[i].tobytes()) for i in range(24)]
     lps_, lis_ = (np.stack([np.frombuffer(s[k], np.uint8) for s in shards]) for k in (0, 1))
     with HelperEngine(vdaf, vk) as eng:
-        eng.debug(4, k3_split)
         init = eng.leader_initialized_batch(ln, lps_, lis_)
     for i in range(24):
         rc, share, _, _ = orc.prep_init(vk, 0, ln[i].tobytes(), lps_[i].tobytes(), lis_[i].tobytes())
