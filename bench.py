@@ -381,6 +381,9 @@ def main():
     ap.add_argument("--no-dist", dest="dist", action="store_false",
                     help="at N=1, skip the RCCL (nccl) process group and the shard-record all-gather + device merge "
                          "that every step otherwise ends with (by default the N=1 step carries the N>1 step's work)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal of the N>1 path on a 1-GPU box: every rank runs on cuda:0 and the shard records "
+                         "go over gloo (launch under torch.distributed.run; the numbers are not a scaling result)")
     args = ap.parse_args()
     ensure_world(args.gpus)
 
@@ -395,11 +398,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == args.gpus  # ensure_world
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    gpu = 0 if args.share_gpu else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     use_dist = world > 1 or args.dist
     if use_dist:
-        if world == 1:
+        if args.share_gpu:
+            dist.init_process_group("gloo")
+        elif world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", str(_free_port()))
             dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
@@ -434,7 +440,7 @@ def main():
     del d_idx
     d_verdicts = torch.empty(R, dtype=torch.uint8, device=dev)
     d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
-    eng = HelperEngine(vdaf, vk, device=local_rank)
+    eng = HelperEngine(vdaf, vk, device=gpu)
     combiner = ShardCombiner(eng) if use_dist else None
 
     def step():
@@ -459,7 +465,7 @@ def main():
     elapsed = time.perf_counter() - t
     kt = eng.timing_read()
     if use_dist:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.share_gpu else dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
