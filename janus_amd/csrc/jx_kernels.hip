@@ -311,17 +311,6 @@ __device__ __forceinline__ f128 shl32_mod(f128 h) {
   return reduce192(h.lo << 32, (h.hi << 32) | (h.lo >> 32), h.hi >> 32);
 }
 
-// K1's staging stores (measurement / proof share elements that K3 reads back much later).
-__device__ __forceinline__ void st_stage(uint4* p, uint4 v) {
-#ifdef JX_NT_STAGE
-  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-  v4u x = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(p));
-#else
-  *p = v;
-#endif
-}
-
 // one measurement element at static stream position e (fast path: no rejections)
 // WIDE (bits in (32, 64], Sum / SumVec): the word columns of bits 0..31 are folded into `lo` at
 // bit 32 and restart for the bits 32.. (weights 2^(j-32) < 2^32); out = lo + 2^32 * high.
@@ -332,7 +321,7 @@ __device__ __forceinline__ void emit_meas(const Cfg& c, uint4* mp, uint4* op, ui
   // elements past the share (last block) or not truncated (Histogram; FixedPoint's trailing norm
   // bits) add with weight 0 instead of branching around the column sums.
   const bool in = e < c.meas_len;
-  if (STORE && in) st_stage(mp + (uint64_t)e * IL, v);
+  if (STORE && in) mp[(uint64_t)e * IL] = v;
   gmax = max(gmax, in ? ge_screen(v) : 0u);
   const bool tin = !c.out_is_meas && e < c.trunc_len;
   const uint32_t sh = opaque_u32(tin ? 1u << (WIDE ? (tr.j & 31u) : tr.j) : 0u);
@@ -357,7 +346,7 @@ __device__ __forceinline__ void emit_meas(const Cfg& c, uint4* mp, uint4* op, ui
 __device__ __forceinline__ void emit_proof(const Cfg& c, uint4* pp, uint32_t e, uint4 v, uint32_t& gmax) {
   if (e >= c.proof_len) return;
   gmax = max(gmax, ge_screen(v));
-  st_stage(pp + (uint64_t)e * IL, v);
+  pp[(uint64_t)e * IL] = v;
 }
 
 // Barycentric weights of one gadget on the P-th roots of unity w^k (Montgomery form):
