@@ -470,8 +470,7 @@ static void free_staging(jx_engine* e) {
 static uint32_t stage_eb(const Cfg& c) { return c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? 8u : 16u; }
 static uint64_t coef_elems(const Cfg& c) { return c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? (uint64_t)c.np * c.nco : c.ncoef; }
 static uint64_t part_bytes(const Cfg& c) {
-  // >= 16 bytes per report: xof_pairs_kernel hands its joint_rand_parts to xof_tail_kernel through it
-  return c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? 24ull * c.np * c.ngroups : std::max<uint64_t>(16, 64ull * c.ngt);
+  return c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? 24ull * c.np * c.ngroups : 64ull * c.ngt;
 }
 // the output shares alias the measurement-share staging (Histogram: output = measurement share)
 static bool outs_alias_meas(const Cfg& c) { return c.out_is_meas && c.algo != ALGO_COUNT; }

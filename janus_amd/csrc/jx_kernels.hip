@@ -1053,12 +1053,17 @@ __global__ __launch_bounds__(64 * K1_WAVES, WIDE ? 2 : 4) void xof_lanes_kernel(
         emit_p(e0 + 11 + ci, make_uint4(st[2 + 4 * ci], st[3 + 4 * ci], st[4 + 4 * ci], st[5 + 4 * ci]));
     }
   }
-  // the S half's screen (measurement + proof elements) goes to the J half, which hands the report to the
-  // tail kernel (xof_tail_kernel, below xof_pairs_kernel: the tail sets the register peak)
+  // the S half's screen (measurement + proof elements) goes to the J half, which finishes the report
   const uint32_t smax = lower_to_upper(gmax);
-  if (jh && r0 < b.n) {
-    b.flags[r0] = smax == 0xFFFFFFFFu ? FLAG_SLOW : 0u;
-    reinterpret_cast<uint4*>(b.part)[r0] = make_uint4(own_part[0], own_part[1], own_part[2], own_part[3]);
+  if (jh) {
+    uint32_t flags = smax == 0xFFFFFFFFu ? FLAG_SLOW : 0u;
+    uint32_t nonce[4], part_l[4], lead_part[4];
+    load16(b.nonces + 16 * r, nonce);
+    load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
+    load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
+    flags = xof_tail(c, b, blk, il, r, r0 < b.n, nonce, part_l, lead_part, own_part, flags, false);
+    if (b.force_slow) flags |= FLAG_SLOW;
+    if (r0 < b.n) b.flags[r0] = flags;
   }
 }
 
@@ -1152,7 +1157,7 @@ __device__ __forceinline__ void sponge_oneblock_half(uint32_t* s, const Block& m
   keccak_p12_half(s, hi);
 }
 
-__global__ __launch_bounds__(64 * K1_WAVES, 4) void xof_pairs_kernel(Cfg c, Bufs b) {
+__global__ __launch_bounds__(64 * K1_WAVES, 2) void xof_pairs_kernel(Cfg c, Bufs b) {
   const uint32_t lane = threadIdx.x & 63;
   const bool jh = lane >= 32;     // J lanes
   const bool hi = (lane & 1u) != 0;  // high halves
@@ -1382,34 +1387,18 @@ __global__ __launch_bounds__(64 * K1_WAVES, 4) void xof_pairs_kernel(Cfg c, Bufs
       for (int ci = 0; ci < 10; ci++) emit_p(e0 + 11 + ci, h[1 + 2 * ci], h[2 + 2 * ci]);
     }
   }
-  // the high S lane's screen -> its low partner -> the low J lane, which hands the report to the tail
-  // kernel (xof_tail_kernel): the tail's ~600 Montgomery products set the register peak (178 VGPRs and two
-  // waves per SIMD with it inline, 121 and four without), and this kernel runs where waves are scarce
+  // the high S lane's screen -> its low partner -> the low J lane, which finishes the report
   const uint32_t smax = lower_to_upper(pswap(gmax));
-  if (jh && !hi && r0 < b.n) {
-    b.flags[r0] = smax == 0xFFFFFFFFu ? FLAG_SLOW : 0u;
-    reinterpret_cast<uint4*>(b.part)[r0] = make_uint4(own_part[0], own_part[1], own_part[2], own_part[3]);
+  if (jh && !hi) {
+    uint32_t flags = smax == 0xFFFFFFFFu ? FLAG_SLOW : 0u;
+    uint32_t nonce[4], part_l[4], lead_part[4];
+    load16(b.nonces + 16 * r, nonce);
+    load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
+    load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
+    flags = xof_tail(c, b, blk, il, r, r0 < b.n, nonce, part_l, lead_part, own_part, flags, false);
+    if (b.force_slow) flags |= FLAG_SLOW;
+    if (r0 < b.n) b.flags[r0] = flags;
   }
-}
-
-// The XOF tail of the reports xof_pairs_kernel squeezed and absorbed, one report per lane: its own
-// joint_rand_part and the rejection flag come through Bufs::part (the FLP partial sums' buffer, which K3
-// writes only later on the stream; >= 16 bytes per report) and Bufs::flags.
-__global__ __launch_bounds__(256) void xof_tail_kernel(Cfg c, Bufs b) {
-  const uint64_t r0 = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  const uint64_t blk = r0 >> 6;
-  const uint32_t lane = (uint32_t)(r0 & 63);
-  if (blk >= (b.n + 63) / 64) return;
-  const uint64_t r = r0 < b.n ? r0 : b.n - 1;
-  const uint4 jp = reinterpret_cast<const uint4*>(b.part)[r];
-  const uint32_t own_part[4] = {jp.x, jp.y, jp.z, jp.w};
-  uint32_t nonce[4], part_l[4], lead_part[4];
-  load16(b.nonces + 16 * r, nonce);
-  load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
-  load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
-  uint32_t flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, part_l, lead_part, own_part, b.flags[r], false);
-  if (b.force_slow) flags |= FLAG_SLOW;
-  if (r0 < b.n) b.flags[r0] = flags;
 }
 
 // ---------------------------------------------------------------------------- K1, leader role
@@ -2920,17 +2909,14 @@ hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
     hipLaunchKernelGGL((xof_leader_kernel<false, true>), grid, block, 0, s, c, b);
   else if (b.leader)
     hipLaunchKernelGGL((xof_leader_kernel<false, false>), grid, block, 0, s, c, b);
-  else if (b.k1_split == 6 && !wide) {  // lane pairs: 16 reports per wave, then the tail
+  else if (b.k1_split == 6 && !wide)  // lane pairs: 16 reports per wave
     hipLaunchKernelGGL(xof_pairs_kernel, dim3((4 * nb + K1_WAVES - 1) / K1_WAVES), block, 0, s, c, b);
-    hipLaunchKernelGGL(xof_tail_kernel, dim3((nb * 64 + 255) / 256), dim3(256), 0, s, c, b);
-  }
-  else if (b.k1_split == 3) {  // lane-split: 32 reports per wave, then the tail
+  else if (b.k1_split == 3) {  // lane-split: 32 reports per wave
     const dim3 g2((2 * nb + K1_WAVES - 1) / K1_WAVES);
     if (wide)
       hipLaunchKernelGGL((xof_lanes_kernel<true>), g2, block, 0, s, c, b);
     else
       hipLaunchKernelGGL((xof_lanes_kernel<false>), g2, block, 0, s, c, b);
-    hipLaunchKernelGGL(xof_tail_kernel, dim3((nb * 64 + 255) / 256), dim3(256), 0, s, c, b);
   } else if (wide)
     hipLaunchKernelGGL((xof_kernel<true>), grid, block, 0, s, c, b);
   else
