@@ -493,6 +493,13 @@ def main():
         all_agg, all_count = cyc.range(0, R * world, total_steps)
         verified = verified and c_agg == enc(all_agg) and c_count == all_count
 
+    rank_ok = bool(verified and verdict_ok and msgs_ok)
+    all_ok = rank_ok
+    if use_dist:  # every rank checked its own range: the line reports the AND over ranks
+        f = torch.tensor([int(rank_ok)], dtype=torch.int32, device="cpu" if args.share_gpu else dev)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        all_ok = bool(f.item())
+
     total_reports = R * world * args.steps
     value = total_reports / elapsed
     work = sumvec_work(args.bits, args.length, args.chunk)
@@ -566,11 +573,12 @@ def main():
                     "k1_hbm_GBps": round(work["hbm_k1"] * chunk_reports / (k1_ms * 1e-3) / 1e9, 1),
                     "k3_hbm_GBps": round(work["hbm_k3"] * chunk_reports / (k3_ms * 1e-3) / 1e9, 1),
                     "work_per_report": work},
-        "verified": bool(verified and verdict_ok and msgs_ok),
-        "verification": {"aggregate_and_count": bool(verified), "verdicts": verdict_ok,
+        "verified": all_ok,
+        "verification": {"all_ranks": all_ok, "aggregate_and_count": bool(verified), "verdicts": verdict_ok,
                          "prep_msgs_of_finished_reports": msgs_ok,
                          "rank_range": [start, stop], "note": "rank r holds global reports [r R, (r+1) R) of the "
-                         "cyclic pool tiling; expected aggregates from the pool's block aggregates (CyclicPool)"},
+                         "cyclic pool tiling; expected aggregates from the pool's block aggregates (CyclicPool); all_ranks = "
+                         "every rank's own check (MIN over ranks), the other fields are rank 0's"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(orc, vdaf, vk, nonces, ps, his, lps, args.cpu_seconds, cpu["threads"])

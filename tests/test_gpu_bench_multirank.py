@@ -38,4 +38,4 @@ def test_two_ranks_on_one_gpu_verify():
     assert len(lines) == 1, p.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["global_reports_per_step"] == 40000
-    assert out["verified"] is True, out.get("verification")
+    assert out["verified"] is True and out["verification"]["all_ranks"] is True, out.get("verification")
