@@ -128,6 +128,13 @@ struct jx_engine {
   uint32_t k1_split = 0;  // helper K1: 0 automatic, 3 lane-split, 5 fused, 6 lane pairs (JX_K1_SPLIT, debug option 3)
   // producer / consumer ordering (jx_engine_wait_stream / jx_engine_join_stream): reused events
   hipEvent_t ev_wait = nullptr, ev_join = nullptr;
+  // Concurrent pipelines of the fused device path (jx_helper_prep_aggregate_device, pipes_for): child
+  // engines with their own stream and staging run K1 -> K3 -> K4 of alternate launches, so launches of
+  // different phases share the device; the K4s stay in launch order through ev_pipe.
+  std::vector<jx_engine*> pipes;
+  uint32_t npipes = 0;  // 0: automatic (JX_PIPES, debug option 4)
+  bool is_pipe = false;  // a child: d_consts belongs to the parent
+  hipEvent_t ev_pipe = nullptr;
 };
 
 // The message of the last failing call, per calling thread: an engine serves several host threads,
@@ -1012,6 +1019,80 @@ static uint64_t launch_chunk(const jx_engine* e, uint64_t n) {
   return (per + 63) / 64 * 64;
 }
 
+// ---------------------------------------------------------------------------- pipelines
+// A helper launch of the fused path runs K1 (two sponges per lane, two waves per SIMD, VALU), then K3
+// (LDS-DMA ring: HBM + limb products) and K4 (HBM): one after the other, every launch's waves are in the
+// same phase at the same time (the K1 waves of a round reach their FLP-coefficient tails together, K3 runs
+// at a throttled clock beside an idle Keccak pipe). With P pipelines the launches of one call alternate
+// over P child engines, each with its own stream and staging, so different launches' phases overlap; only
+// the K4s are ordered (they add into the same aggregation). Measured on MI355X with P independent engines
+// (tools/multi_engine_probe.py): SumVec 8x1000/88, 1.25M reports, 7.28M (one) -> 7.67M (two) -> 7.79M
+// reports/s (three). Used when a call spans >= 2 launches of one segment; not for Count (one tiny kernel)
+// or the multiproof path.
+static uint32_t pipes_for(const jx_engine* e, uint64_t n, uint64_t chunk, bool many) {
+  const Cfg& c = e->cfg;
+  if (many || c.algo == ALGO_COUNT || c.algo == ALGO_SUMVEC_F64_MULTIPROOF) return 1;
+  const uint64_t launches = (n + chunk - 1) / chunk;
+  const uint64_t want = e->npipes ? e->npipes : 2;
+  return (uint32_t)(launches < want ? launches : want);
+}
+
+// Create (once) and size the first P pipelines; false when their staging does not fit (the caller then
+// runs the single-stream path, and the pipelines' staging is handed back).
+static bool ensure_pipes(jx_engine* e, uint32_t P, uint64_t chunk) {
+  while (e->pipes.size() < P) {
+    jx_engine* q = new jx_engine();
+    q->cfg = e->cfg;
+    q->device = e->device;
+    q->is_pipe = true;
+    q->d_consts = e->d_consts;
+    q->default_chunk = e->default_chunk;
+    q->round_reports = e->round_reports;
+    if (hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&q->ev_join, hipEventDisableTiming) != hipSuccess) {
+      jx_engine_destroy(q);
+      return false;
+    }
+    e->pipes.push_back(q);
+  }
+  if (!e->ev_pipe && hipEventCreateWithFlags(&e->ev_pipe, hipEventDisableTiming) != hipSuccess) return false;
+  for (uint32_t k = 0; k < P; k++) {
+    jx_engine* q = e->pipes[k];
+    q->force_slow = e->force_slow;
+    q->k1_split = e->k1_split;
+    q->timing = e->timing;
+    if (q->acc_chunks != e->acc_chunks) {  // accumulate scratch is sized by the chunking
+      (void)hipStreamSynchronize(q->stream);
+      free_staging(q);
+      q->acc_chunks = e->acc_chunks;
+    }
+    if (ensure_capacity(q, chunk) != JX_OK) {
+      for (jx_engine* r : e->pipes) {
+        (void)hipStreamSynchronize(r->stream);
+        free_staging(r);
+      }
+      t_err.clear();
+      return false;
+    }
+  }
+  return true;
+}
+
+// Move the pipelines' kernel timings into the engine's.
+static int32_t collect_pipe_timing(jx_engine* e) {
+  for (jx_engine* q : e->pipes) {
+    int32_t rc = drain_timing(q);
+    if (rc) return rc;
+    for (int i = 0; i < NST; i++) {
+      e->ms[i] += q->ms[i];
+      e->launches[i] += q->launches[i];
+      q->ms[i] = 0;
+      q->launches[i] = 0;
+    }
+  }
+  return JX_OK;
+}
+
 // ---------------------------------------------------------------------------- C ABI
 
 extern "C" {
@@ -1064,6 +1145,10 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
     if (v == 0 || v == 3 || v == 5 || v == 6) e->k1_split = (uint32_t)v;
   }
   e->round_reports = k1_round_reports(e->cfg, device, e->k1_split);
+  if (const char* env = getenv("JX_PIPES")) {
+    const int v = atoi(env);
+    if (v >= 0 && v <= 4) e->npipes = (uint32_t)v;
+  }
   uint64_t budget = 48ull << 30;
   size_t mem_free = 0, mem_total = 0;
   if (hipMemGetInfo(&mem_free, &mem_total) == hipSuccess && e->round_reports &&
@@ -1093,6 +1178,8 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
 void jx_engine_destroy(jx_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
+  for (jx_engine* p : e->pipes) jx_engine_destroy(p);
+  e->pipes.clear();
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (auto& p : e->pending) {
     (void)hipEventDestroy(p.second.first);
@@ -1107,7 +1194,8 @@ void jx_engine_destroy(jx_engine* e) {
   for (auto& kv : e->batches)
     if (kv.second.mem) (void)hipFree(kv.second.mem);
   for (auto& kv : e->batch_pool) (void)hipFree(kv.second);
-  if (e->d_consts) (void)hipFree(e->d_consts);
+  if (e->d_consts && !e->is_pipe) (void)hipFree(e->d_consts);
+  if (e->ev_pipe) (void)hipEventDestroy(e->ev_pipe);
   if (e->d_tmp) (void)hipFree(e->d_tmp);
   for (void* q : {(void*)e->d_segx, (void*)e->d_perm, (void*)e->d_items, (void*)e->d_spart, (void*)e->d_ptrs,
                   (void*)e->d_err, (void*)e->d_delta})
@@ -1557,16 +1645,44 @@ int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_
   if (c.ps_bytes && !d_ps) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
   const uint64_t chunk = launch_chunk(e, n);
-  int32_t rc = ensure_capacity(e, chunk);
-  if (rc) return rc;
   std::vector<Segment> targets;
-  rc = segment_targets(e, segment_ids, nsegments, targets);
+  int32_t rc = segment_targets(e, segment_ids, nsegments, targets);
   if (rc) return rc;
   const uint8_t *N = (const uint8_t*)d_nonces, *PS = (const uint8_t*)d_ps, *H = (const uint8_t*)d_his,
                 *L = (const uint8_t*)d_lps;
   const uint32_t* SG = (const uint32_t*)d_segment;
-  // the pointer table is uploaded once for every launch of the call (no per-launch host sync)
   const bool many = SG && targets.size() > 1;
+  const uint32_t P = pipes_for(e, n, chunk, many);
+  if (P > 1 && ensure_pipes(e, P, chunk)) {
+    // every pipeline orders after the caller's producers (jx_engine_wait_stream / _event act on the
+    // engine stream) and the engine stream after every pipeline (the join), so the call keeps the
+    // single-stream ordering contract
+    HIPCHK(e, hipEventRecord(e->ev_pipe, e->stream));
+    for (uint32_t k = 0; k < P; k++) HIPCHK(e, hipStreamWaitEvent(e->pipes[k]->stream, e->ev_pipe, 0));
+    uint64_t i = 0;
+    for (uint64_t off = 0; off < n; off += chunk, i++) {
+      jx_engine* q = e->pipes[i % P];
+      const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
+      uint8_t* vout = d_out_verdicts ? (uint8_t*)d_out_verdicts + off : q->d_verdicts;
+      uint8_t* mout = (d_out_prep_msgs && c.jr_len) ? (uint8_t*)d_out_prep_msgs + off * c.seed : q->d_msgs;
+      rc = prep_core(q, m, N + off * 16, PS ? PS + off * c.ps_bytes : nullptr, H + off * c.his_bytes,
+                     L + off * c.lps_bytes, vout, mout, staging_outs(q));
+      if (rc) return rc;
+      if (i > 0) HIPCHK(e, hipStreamWaitEvent(q->stream, e->ev_pipe, 0));  // the previous launch's K4
+      rc = accumulate_into(q, AccSrc{m, staging_outs(q), vout, N + off * 16}, nullptr, SG ? SG + off : nullptr,
+                           targets);
+      if (rc) return rc;
+      HIPCHK(e, hipEventRecord(e->ev_pipe, q->stream));
+    }
+    for (uint32_t k = 0; k < P; k++) {
+      HIPCHK(e, hipEventRecord(e->pipes[k]->ev_join, e->pipes[k]->stream));
+      HIPCHK(e, hipStreamWaitEvent(e->stream, e->pipes[k]->ev_join, 0));
+    }
+    return JX_OK;
+  }
+  rc = ensure_capacity(e, chunk);
+  if (rc) return rc;
+  // the pointer table is uploaded once for every launch of the call (no per-launch host sync)
   if (many) {
     rc = upload_targets(e, targets);
     if (rc) return rc;
@@ -1748,6 +1864,9 @@ int32_t jx_engine_timing(jx_engine* e, int32_t enable) {
   LOCK(e);
   int32_t rc = drain_timing(e);
   if (rc) return rc;
+  rc = collect_pipe_timing(e);
+  if (rc) return rc;
+  for (jx_engine* q : e->pipes) q->timing = enable != 0;
   e->timing = enable != 0;
   for (int i = 0; i < NST; i++) {
     e->ms[i] = 0;
@@ -1760,6 +1879,8 @@ int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]) {
   if (!e) return JX_E_INVALID;
   LOCK(e);
   int32_t rc = drain_timing(e);
+  if (rc) return rc;
+  rc = collect_pipe_timing(e);
   if (rc) return rc;
   for (int i = 0; i < NST; i++) {
     if (ms) ms[i] = (float)e->ms[i];
@@ -1780,6 +1901,11 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
     // 0: automatic (fused; lane-split below one fused wave per SIMD, lane pairs below one lane-split
     // wave per SIMD), 3: lane-split, 5: fused, 6: lane pairs (bits <= 32)
     e->k1_split = (uint32_t)value;
+    return JX_OK;
+  }
+  if (option == 4) {  // pipelines of the fused device path: 0 automatic, 1 single stream, 2..4
+    if (value < 0 || value > 4) return JX_E_INVALID;
+    e->npipes = (uint32_t)value;
     return JX_OK;
   }
   if (option == 2) {  // accumulate chunking (tests)
