@@ -381,6 +381,12 @@ def main():
     ap.add_argument("--no-dist", dest="dist", action="store_false",
                     help="at N=1, skip the RCCL (nccl) process group and the shard-record all-gather + device merge "
                          "that every step otherwise ends with (by default the N=1 step carries the N>1 step's work)")
+    ap.add_argument("--pipes", type=int, default=0,
+                    help="engine pipelines of the fused device path (0: the engine's choice, 2 for a multi-launch step; "
+                         "1: one stream)")
+    ap.add_argument("--alone-steps", type=int, default=2,
+                    help="with pipelines: after the timed steps, this many single-stream steps time each kernel "
+                         "alone (roofline.alone); they count in the verified aggregate")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal of the N>1 path on a 1-GPU box: every rank runs on cuda:0 and the shard records "
                          "go over gloo (launch under torch.distributed.run; the numbers are not a scaling result)")
@@ -441,6 +447,8 @@ def main():
     d_verdicts = torch.empty(R, dtype=torch.uint8, device=dev)
     d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
     eng = HelperEngine(vdaf, vk, device=gpu)
+    if args.pipes:
+        eng.debug(4, args.pipes)
     combiner = ShardCombiner(eng) if use_dist else None
 
     def step():
@@ -468,12 +476,25 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.share_gpu else dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    # pipelines (jx_engine.cpp pipes_for): the launches of a step alternate over concurrent streams, so a
+    # kernel's HIP-event duration includes the device time it shared with another launch's kernels. A few
+    # single-stream steps after the timed region time every kernel alone (roofline.alone).
+    per_step = kt["xof"]["launches"] // max(1, args.steps)
+    pipes = min(per_step, args.pipes or 2) if per_step >= 2 and args.pipes != 1 else 1
+    kt_alone = None
+    if pipes > 1 and args.alone_steps > 0:
+        eng.debug(4, 1)
+        eng.timing(True)
+        for _ in range(args.alone_steps):
+            step()
+        kt_alone = eng.timing_read()
+        eng.debug(4, args.pipes)
 
     # ---- verification against the oracle, from the pool's block aggregates (CyclicPool): this rank's
     # aggregate == (steps + warmup) x the aggregate of its global range; the merged record == the same
     # over every rank's range; every verdict and every finished report's Finish{prep_msg} == the oracle's
     agg, count, _ = eng.aggregate_share(0)
-    total_steps = args.steps + args.warmup
+    total_steps = args.steps + args.warmup + (args.alone_steps if kt_alone else 0)
 
     def partial(a, r):
         h = orc.helper_prep_batch(vk, nonces[a:r], ps[a:r], his[a:r], lps[a:r], nthreads=threads)
@@ -522,6 +543,21 @@ def main():
     k1_clock = pmc_clock("jx::xof_kernel<false>")
     k1_clock = round(k1_clock, 3) if k1_clock else None
     dom_ms = k1_ms if k1_dom else k3_ms
+    # the device over whole steps, and the kernels alone (single-stream steps after the timed region)
+    ms_all = sum(kt[k]["ms"] for k in ("xof", "flp", "accumulate", "slow"))
+    concurrency = ms_all / (elapsed * 1e3)  # kernels in flight on average (this rank's streams)
+    dev_tops = (work["ops_k1"] + work["ops_k3"]) * per_rank / elapsed / 1e12
+    alone = None
+    if kt_alone:
+        la = max(1, kt_alone["xof"]["launches"])
+        a_tops = work["ops_k1"] * R * args.alone_steps / (kt_alone["xof"]["ms"] * 1e-3) / 1e12
+        alone = {"steps": args.alone_steps, "k1_xof_ms_per_launch": round(kt_alone["xof"]["ms"] / la, 3),
+                 "k3_flp_ms_per_launch": round(kt_alone["flp"]["ms"] / max(1, kt_alone["flp"]["launches"]), 3),
+                 "k4_acc_ms_per_launch": round(kt_alone["accumulate"]["ms"] / max(1, kt_alone["accumulate"]["launches"]), 3),
+                 "kernel": "K1 xof_kernel", "achieved": round(a_tops, 3), "frac": round(a_tops / VALU_PEAK_TOPS, 4),
+                 "frac_of_mix_ceiling": round(a_tops / keccak_mix_ceiling_tops(), 4),
+                 "note": "the same step on one stream (debug option 4 = 1), untimed for `value`: each kernel's own "
+                         "issue rate"}
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -564,8 +600,19 @@ def main():
                      "traffic_source": traffic_src, "traffic_note": traffic_note,
                      "algorithmic_bytes": int(alg_bytes), "reports_per_launch": round(chunk_reports, 1),
                      "hbm_GBps": round(alg_bytes / (dom_ms * 1e-3) / 1e9, 1),
-                     "hbm_peak_GBps": HBM_PEAK_GBPS},
-        "kernels": {"k1_xof_ms_per_launch": round(k1_ms, 3), "k3_flp_ms_per_launch": round(k3_ms, 3),
+                     "hbm_peak_GBps": HBM_PEAK_GBPS,
+                     "pipelines": pipes, "kernel_concurrency": round(concurrency, 3),
+                     "device_step": {"achieved": round(dev_tops, 3), "frac": round(dev_tops / VALU_PEAK_TOPS, 4),
+                                     "note": "(K1 + K3 issue-model instructions per report) x this rank's reports / "
+                                             "the timed wall time: the whole device over whole steps"},
+                     "alone": alone,
+                     "frac_note": "achieved / frac: the dominant kernel's instructions per launch over its HIP-event "
+                                  "launch duration in the timed steps. With pipelines > 1 the launches of a step "
+                                  "alternate over concurrent streams and a launch shares the device with the other "
+                                  "pipeline's kernels for part of its duration (kernel_concurrency = summed kernel "
+                                  "durations / wall time): the kernel's own issue rate is `alone`, the device's "
+                                  "`device_step`"},
+        "kernels": {"pipelines": pipes, "k1_xof_ms_per_launch": round(k1_ms, 3), "k3_flp_ms_per_launch": round(k3_ms, 3),
                     "k4_acc_ms_per_launch": round(kt["accumulate"]["ms"] / max(1, kt["accumulate"]["launches"]), 3),
                     "slow_ms_per_launch": round(kt["slow"]["ms"] / max(1, kt["slow"]["launches"]), 3),
                     "reports_per_launch": int(chunk_reports),
