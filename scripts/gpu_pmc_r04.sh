@@ -1,7 +1,7 @@
 # Round-4 PMC passes on the final sources: SumVec over uniform 262,144-report launches (-> <name>_pmc_summary.json,
 # read by bench.py for roofline.traffic) and one serial configs[4] step of 40,960 FixedPoint 16 x 10000 reports
 # (-> <name>_fixedpoint_pmc_summary.json). Each pass is its own rocprofv3 run.
-# usage: bash scripts/gpu_pmc_r04.sh <name>
+# usage: bash scripts/gpu_pmc_r04.sh <name> [sumvec]   (sumvec: skip the configs[4] passes)
 set -o pipefail
 export TMPDIR=/tmp
 N=${1:?name}
@@ -15,6 +15,7 @@ timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -f csv -d $OUT/pmc/pmc_fetch -o r
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -f csv -d $OUT/pmc/pmc_write -o run -- python3 $ONE > $OUT/pmc_write.json 2> $OUT/pmc_write.err || { echo PMC_WRITE_FAIL; tail -5 $OUT/pmc_write.err; exit 1; }
 timeout -s KILL 150 rocprofv3 --pmc $SQ -f csv -d $OUT/pmc/pmc_sq -o run -- python3 $ONE > $OUT/pmc_sq.json 2> $OUT/pmc_sq.err || { echo PMC_SQ_FAIL; tail -5 $OUT/pmc_sq.err; exit 1; }
 python3 tools/prof_summary.py $OUT/pmc --reports-per-launch 262144 --command "python3 $ONE" > $OUT/${N}_pmc_summary.json && echo SUMMARY_OK
+[ "$2" = "sumvec" ] && exit 0
 FP="tools/bench_fixedpoint.py --skip cpu,pipelined,helper,leader --steps 1 --warmup 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/fp/pmc/trace_raw -o run -- python3 $FP > $OUT/fp/trace.json 2> $OUT/fp/trace.err || { echo FP_TRACE_FAIL; tail -20 $OUT/fp/trace.err; exit 1; }
 mkdir -p $OUT/fp/pmc/trace && cp $OUT/fp/pmc/trace_raw/run_kernel_stats.csv $OUT/fp/pmc/trace/
