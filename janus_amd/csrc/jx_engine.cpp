@@ -135,9 +135,6 @@ struct jx_engine {
   uint32_t npipes = 0;  // 0: automatic (JX_PIPES, debug option 4)
   bool is_pipe = false;  // a child: d_consts belongs to the parent
   hipEvent_t ev_pipe = nullptr;
-  // a pipeline's K1 on a low-priority stream of its own, the rest on its high-priority stream (measurement)
-  hipStream_t k1_stream = nullptr;
-  hipEvent_t ev_k1[2] = {nullptr, nullptr};
 };
 
 // The message of the last failing call, per calling thread: an engine serves several host threads,
@@ -770,15 +767,7 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
     HIPCHK(e, stage_end(e, ST_FLP, ev));
   } else {
     HIPCHK(e, stage_begin(e, &ev));
-    if (e->k1_stream) {  // a pipeline with a low-priority K1 stream (ensure_pipes, JX_PIPE_PRIO)
-      HIPCHK(e, hipEventRecord(e->ev_k1[0], e->stream));
-      HIPCHK(e, hipStreamWaitEvent(e->k1_stream, e->ev_k1[0], 0));
-      HIPCHK(e, launch_xof(c, b, e->k1_stream));
-      HIPCHK(e, hipEventRecord(e->ev_k1[1], e->k1_stream));
-      HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_k1[1], 0));
-    } else {
-      HIPCHK(e, launch_xof(c, b, e->stream));
-    }
+    HIPCHK(e, launch_xof(c, b, e->stream));
     HIPCHK(e, stage_end(e, ST_XOF, ev));
     if (!leader) {  // the leader's shares are explicit: no rejection-sampled streams to redo
       HIPCHK(e, stage_begin(e, &ev));
@@ -1059,20 +1048,8 @@ static bool ensure_pipes(jx_engine* e, uint32_t P, uint64_t chunk) {
     q->d_consts = e->d_consts;
     q->default_chunk = e->default_chunk;
     q->round_reports = e->round_reports;
-    const char* prio = getenv("JX_PIPE_PRIO");
-    if (prio && atoi(prio) != 0) {  // K3 / K4 / small kernels ahead of K1 when slots free
-      int lo = 0, hi = 0;
-      if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-          hipStreamCreateWithPriority(&q->stream, hipStreamNonBlocking, hi) != hipSuccess ||
-          hipStreamCreateWithPriority(&q->k1_stream, hipStreamNonBlocking, lo) != hipSuccess ||
-          hipEventCreateWithFlags(&q->ev_k1[0], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&q->ev_k1[1], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&q->ev_join, hipEventDisableTiming) != hipSuccess) {
-        jx_engine_destroy(q);
-        return false;
-      }
-    } else if (hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) != hipSuccess ||
-               hipEventCreateWithFlags(&q->ev_join, hipEventDisableTiming) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&q->ev_join, hipEventDisableTiming) != hipSuccess) {
       jx_engine_destroy(q);
       return false;
     }
@@ -1226,12 +1203,6 @@ void jx_engine_destroy(jx_engine* e) {
   for (int k = 0; k < 2; k++) {
     if (e->h_ptrs[k]) (void)hipHostFree(e->h_ptrs[k]);
     if (e->ev_ptrs[k]) (void)hipEventDestroy(e->ev_ptrs[k]);
-  }
-  for (hipEvent_t& v : e->ev_k1)
-    if (v) (void)hipEventDestroy(v);
-  if (e->k1_stream) {
-    (void)hipStreamSynchronize(e->k1_stream);
-    (void)hipStreamDestroy(e->k1_stream);
   }
   if (e->ev_wait) (void)hipEventDestroy(e->ev_wait);
   if (e->ev_join) (void)hipEventDestroy(e->ev_join);
