@@ -1644,7 +1644,7 @@ int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_
   const Cfg& c = e->cfg;
   if (c.ps_bytes && !d_ps) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
-  uint64_t chunk = launch_chunk(e, n);
+  const uint64_t chunk = launch_chunk(e, n);
   std::vector<Segment> targets;
   int32_t rc = segment_targets(e, segment_ids, nsegments, targets);
   if (rc) return rc;
@@ -1652,14 +1652,6 @@ int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_
                 *L = (const uint8_t*)d_lps;
   const uint32_t* SG = (const uint32_t*)d_segment;
   const bool many = SG && targets.size() > 1;
-  // With pipelines, a call of >= 4 K1 rounds runs in >= 4 whole-round launches (two per pipeline), even
-  // where the staging budget would take it in one (Histogram 256/16 at 1M reports: 130.4M -> 134.0-136.0M
-  // reports/s in four launches over two pipelines; SumVec 8x1000/88 keeps its 262,144-report launches)
-  const uint64_t rr = e->round_reports;
-  if (e->npipes != 1 && rr && n >= 4 * rr && pipes_for(e, n, rr, many) > 1) {
-    const uint64_t q = ((n + 3) / 4 + rr - 1) / rr * rr;
-    if (q < chunk) chunk = q;
-  }
   const uint32_t P = pipes_for(e, n, chunk, many);
   if (P > 1 && ensure_pipes(e, P, chunk)) {
     // every pipeline orders after the caller's producers (jx_engine_wait_stream / _event act on the
