@@ -1659,26 +1659,32 @@ int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_
     // single-stream ordering contract
     HIPCHK(e, hipEventRecord(e->ev_pipe, e->stream));
     for (uint32_t k = 0; k < P; k++) HIPCHK(e, hipStreamWaitEvent(e->pipes[k]->stream, e->ev_pipe, 0));
-    uint64_t i = 0;
-    for (uint64_t off = 0; off < n; off += chunk, i++) {
-      jx_engine* q = e->pipes[i % P];
-      const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
-      uint8_t* vout = d_out_verdicts ? (uint8_t*)d_out_verdicts + off : q->d_verdicts;
-      uint8_t* mout = (d_out_prep_msgs && c.jr_len) ? (uint8_t*)d_out_prep_msgs + off * c.seed : q->d_msgs;
-      rc = prep_core(q, m, N + off * 16, PS ? PS + off * c.ps_bytes : nullptr, H + off * c.his_bytes,
-                     L + off * c.lps_bytes, vout, mout, staging_outs(q));
-      if (rc) return rc;
-      if (i > 0) HIPCHK(e, hipStreamWaitEvent(q->stream, e->ev_pipe, 0));  // the previous launch's K4
-      rc = accumulate_into(q, AccSrc{m, staging_outs(q), vout, N + off * 16}, nullptr, SG ? SG + off : nullptr,
-                           targets);
-      if (rc) return rc;
-      HIPCHK(e, hipEventRecord(e->ev_pipe, q->stream));
-    }
+    auto run = [&]() -> int32_t {
+      uint64_t i = 0;
+      for (uint64_t off = 0; off < n; off += chunk, i++) {
+        jx_engine* q = e->pipes[i % P];
+        const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
+        uint8_t* vout = d_out_verdicts ? (uint8_t*)d_out_verdicts + off : q->d_verdicts;
+        uint8_t* mout = (d_out_prep_msgs && c.jr_len) ? (uint8_t*)d_out_prep_msgs + off * c.seed : q->d_msgs;
+        int32_t r = prep_core(q, m, N + off * 16, PS ? PS + off * c.ps_bytes : nullptr, H + off * c.his_bytes,
+                              L + off * c.lps_bytes, vout, mout, staging_outs(q));
+        if (r) return r;
+        if (i > 0) HIPCHK(e, hipStreamWaitEvent(q->stream, e->ev_pipe, 0));  // the previous launch's K4
+        r = accumulate_into(q, AccSrc{m, staging_outs(q), vout, N + off * 16}, nullptr, SG ? SG + off : nullptr,
+                            targets);
+        if (r) return r;
+        HIPCHK(e, hipEventRecord(e->ev_pipe, q->stream));
+      }
+      return JX_OK;
+    };
+    rc = run();
+    // the join, also after a failed launch: whatever was queued on a pipeline stays ordered before the
+    // engine stream's later work (and jx_engine_sync)
     for (uint32_t k = 0; k < P; k++) {
       HIPCHK(e, hipEventRecord(e->pipes[k]->ev_join, e->pipes[k]->stream));
       HIPCHK(e, hipStreamWaitEvent(e->stream, e->pipes[k]->ev_join, 0));
     }
-    return JX_OK;
+    return rc;
   }
   rc = ensure_capacity(e, chunk);
   if (rc) return rc;
