@@ -86,6 +86,8 @@ struct jx_engine {
   // accumulation scratch: partials + selection bytes
   uint64_t* d_partials = nullptr;
   uint32_t acc_chunks = 0;  // report chunks of the accumulate kernel (0: acc_nchunks picks)
+  uint8_t* d_hout = nullptr;  // the host fused path with pipelines: verdicts || prep messages of the call
+  uint64_t hout_bytes = 0;
   uint8_t* d_tmp = nullptr;  // output-share transpose / aggregate encode / records
   size_t tmp_bytes = 0;
   uint8_t* d_mask = nullptr;
@@ -596,6 +598,7 @@ static int32_t ensure_tmp(jx_engine* e, size_t bytes) {
   if (bytes <= e->tmp_bytes) return JX_OK;
   HIPCHK(e, hipStreamSynchronize(e->stream));
   if (e->d_tmp) (void)hipFree(e->d_tmp);
+  if (e->d_hout) (void)hipFree(e->d_hout);
   e->d_tmp = nullptr;
   e->tmp_bytes = 0;
   HIPCHK(e, hipMalloc((void**)&e->d_tmp, bytes));
@@ -1606,12 +1609,65 @@ int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces
   if (c.ps_bytes && !public_shares) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
   const uint64_t chunk = launch_chunk(e, n);
-  int32_t rc = ensure_capacity(e, chunk);
-  if (rc) return rc;
   Segment* seg = nullptr;
-  rc = get_segment(e, segment, &seg);
+  int32_t rc = get_segment(e, segment, &seg);
   if (rc) return rc;
   const std::vector<Segment> targets{*seg};
+  const uint32_t P = pipes_for(e, n, chunk, false);
+  if (P > 1 && ensure_pipes(e, P, chunk)) {
+    // the pipelines (see jx_helper_prep_aggregate_device): launch i's host-to-device copies (pageable: the
+    // host thread stages them) go out while the other pipeline's kernels run; the verdicts and prep
+    // messages collect in an engine buffer and come back once, after the join
+    const uint64_t ob = n + (c.jr_len ? n * c.seed : 0);
+    if (ob > e->hout_bytes) {
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+      if (e->d_hout) (void)hipFree(e->d_hout);
+      e->d_hout = nullptr;
+      e->hout_bytes = 0;
+      if (dev_alloc(e, (void**)&e->d_hout, ob) != hipSuccess) return nomem(e, "host-path outputs", ob);
+      e->hout_bytes = ob;
+    }
+    uint8_t* dv = e->d_hout;
+    uint8_t* dm = e->d_hout + n;
+    HIPCHK(e, hipEventRecord(e->ev_pipe, e->stream));
+    for (uint32_t k = 0; k < P; k++) HIPCHK(e, hipStreamWaitEvent(e->pipes[k]->stream, e->ev_pipe, 0));
+    auto run = [&]() -> int32_t {
+      uint64_t i = 0;
+      for (uint64_t off = 0; off < n; off += chunk, i++) {
+        jx_engine* q = e->pipes[i % P];
+        const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
+        HIPCHK(e, hipMemcpyAsync(q->d_nonces, nonces + off * 16, m * 16, hipMemcpyHostToDevice, q->stream));
+        if (c.ps_bytes)
+          HIPCHK(e, hipMemcpyAsync(q->d_ps, public_shares + off * c.ps_bytes, m * c.ps_bytes, hipMemcpyHostToDevice,
+                                   q->stream));
+        HIPCHK(e, hipMemcpyAsync(q->d_his, helper_input_shares + off * c.his_bytes, m * c.his_bytes,
+                                 hipMemcpyHostToDevice, q->stream));
+        HIPCHK(e, hipMemcpyAsync(q->d_lps, leader_prep_shares + off * c.lps_bytes, m * c.lps_bytes,
+                                 hipMemcpyHostToDevice, q->stream));
+        int32_t r = prep_core(q, m, q->d_nonces, q->d_ps, q->d_his, q->d_lps, dv + off, dm + off * c.seed,
+                              staging_outs(q));
+        if (r) return r;
+        if (i > 0) HIPCHK(e, hipStreamWaitEvent(q->stream, e->ev_pipe, 0));  // the previous launch's K4
+        r = accumulate_into(q, AccSrc{m, staging_outs(q), dv + off, q->d_nonces}, nullptr, nullptr, targets);
+        if (r) return r;
+        HIPCHK(e, hipEventRecord(e->ev_pipe, q->stream));
+      }
+      return JX_OK;
+    };
+    rc = run();
+    for (uint32_t k = 0; k < P; k++) {
+      HIPCHK(e, hipEventRecord(e->pipes[k]->ev_join, e->pipes[k]->stream));
+      HIPCHK(e, hipStreamWaitEvent(e->stream, e->pipes[k]->ev_join, 0));
+    }
+    if (rc) return rc;
+    if (out_verdicts) HIPCHK(e, hipMemcpyAsync(out_verdicts, dv, n, hipMemcpyDeviceToHost, e->stream));
+    if (out_prep_msgs && c.jr_len)
+      HIPCHK(e, hipMemcpyAsync(out_prep_msgs, dm, n * c.seed, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return JX_OK;
+  }
+  rc = ensure_capacity(e, chunk);
+  if (rc) return rc;
   for (uint64_t off = 0; off < n; off += chunk) {
     const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
     HIPCHK(e, hipMemcpyAsync(e->d_nonces, nonces + off * 16, m * 16, hipMemcpyHostToDevice, e->stream));

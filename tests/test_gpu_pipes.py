@@ -80,3 +80,26 @@ def test_pipes_match_oracle(name, vdaf):
     finally:
         for eng in engs:
             eng.close()
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+def test_host_path_pipes_match_oracle(P):
+    """jx_helper_prep_aggregate (host buffers) over P pipelines: verdicts and prep messages come back once
+    for the whole call; aggregate, count and checksum as the oracle's."""
+    vdaf = Prio3.sum_vec(8, 100, 10)
+    vk = bytes(range(3, 19))
+    n = 3 * 1024 + 77
+    orc, nonces, ps, his, lps = _batch(vdaf, vk, n, seed=P)
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16)
+    os.environ["JX_CHUNK_REPORTS"] = "1024"
+    try:
+        eng = HelperEngine(vdaf, vk)
+    finally:
+        del os.environ["JX_CHUNK_REPORTS"]
+    with eng:
+        eng.debug(4, P)
+        v, m = eng.prep_and_aggregate(nonces, ps, his, lps)
+        np.testing.assert_array_equal(v, want["verdicts"])
+        fin = want["verdicts"] == 0
+        np.testing.assert_array_equal(m[fin], want["prep_msgs"][fin])
+        assert eng.aggregate_share(0) == (want["agg"], want["count"], want["checksum"])
