@@ -1032,11 +1032,13 @@ static uint64_t launch_chunk(const jx_engine* e, uint64_t n) {
 // (tools/multi_engine_probe.py): SumVec 8x1000/88, 1.25M reports, 7.28M (one) -> 7.67M (two) -> 7.79M
 // reports/s (three). Used when a call spans >= 2 launches of one segment; not for Count (one tiny kernel)
 // or the multiproof path.
-static uint32_t pipes_for(const jx_engine* e, uint64_t n, uint64_t chunk, bool many) {
+// host: the host-buffer path, whose pageable copies also take turns (3 by default there: SumVec 1.25M
+// reports 5.02M -> 6.44M (two) -> 7.12M (three) reports/s including the copies, tools/bench_host_path.py).
+static uint32_t pipes_for(const jx_engine* e, uint64_t n, uint64_t chunk, bool many, bool host = false) {
   const Cfg& c = e->cfg;
   if (many || c.algo == ALGO_COUNT || c.algo == ALGO_SUMVEC_F64_MULTIPROOF) return 1;
   const uint64_t launches = (n + chunk - 1) / chunk;
-  const uint64_t want = e->npipes ? e->npipes : 2;
+  const uint64_t want = e->npipes ? e->npipes : (host ? 3 : 2);
   return (uint32_t)(launches < want ? launches : want);
 }
 
@@ -1613,7 +1615,7 @@ int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces
   int32_t rc = get_segment(e, segment, &seg);
   if (rc) return rc;
   const std::vector<Segment> targets{*seg};
-  const uint32_t P = pipes_for(e, n, chunk, false);
+  const uint32_t P = pipes_for(e, n, chunk, false, true);
   if (P > 1 && ensure_pipes(e, P, chunk)) {
     // the pipelines (see jx_helper_prep_aggregate_device): launch i's host-to-device copies (pageable: the
     // host thread stages them) go out while the other pipeline's kernels run; the verdicts and prep
