@@ -136,6 +136,7 @@ struct jx_engine {
   std::vector<jx_engine*> pipes;
   uint32_t npipes = 0;  // 0: automatic (JX_PIPES, debug option 4)
   bool is_pipe = false;  // a child: d_consts belongs to the parent
+  bool pipes_nomem = false;  // the pipelines' staging did not fit once: single stream from then on
   hipEvent_t ev_pipe = nullptr;
 };
 
@@ -1036,7 +1037,7 @@ static uint64_t launch_chunk(const jx_engine* e, uint64_t n) {
 // reports 5.02M -> 6.44M (two) -> 7.12M (three) reports/s including the copies, tools/bench_host_path.py).
 static uint32_t pipes_for(const jx_engine* e, uint64_t n, uint64_t chunk, bool many, bool host = false) {
   const Cfg& c = e->cfg;
-  if (many || c.algo == ALGO_COUNT || c.algo == ALGO_SUMVEC_F64_MULTIPROOF) return 1;
+  if (many || e->pipes_nomem || c.algo == ALGO_COUNT || c.algo == ALGO_SUMVEC_F64_MULTIPROOF) return 1;
   const uint64_t launches = (n + chunk - 1) / chunk;
   const uint64_t want = e->npipes ? e->npipes : (host ? 3 : 2);
   return (uint32_t)(launches < want ? launches : want);
@@ -1077,6 +1078,7 @@ static bool ensure_pipes(jx_engine* e, uint32_t P, uint64_t chunk) {
         free_staging(r);
       }
       t_err.clear();
+      e->pipes_nomem = true;  // not retried on every call (JX_STAGING_GB sizes one pipeline's launches)
       return false;
     }
   }
