@@ -1719,14 +1719,11 @@ int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_
     // single-stream ordering contract
     HIPCHK(e, hipEventRecord(e->ev_pipe, e->stream));
     for (uint32_t k = 0; k < P; k++) HIPCHK(e, hipStreamWaitEvent(e->pipes[k]->stream, e->ev_pipe, 0));
-    const char* stg = getenv("JX_PIPE_STAGGER");  // measurement: pipeline 1 starts with a half launch
-    const bool stagger = stg && atoi(stg) != 0;
     auto run = [&]() -> int32_t {
-      uint64_t i = 0, m = 0;
-      for (uint64_t off = 0; off < n; off += m, i++) {
+      uint64_t i = 0;
+      for (uint64_t off = 0; off < n; off += chunk, i++) {
         jx_engine* q = e->pipes[i % P];
-        const uint64_t want = (stagger && i == 1) ? (chunk / 2 + 63) / 64 * 64 : chunk;
-        m = (n - off) < want ? (n - off) : want;
+        const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
         uint8_t* vout = d_out_verdicts ? (uint8_t*)d_out_verdicts + off : q->d_verdicts;
         uint8_t* mout = (d_out_prep_msgs && c.jr_len) ? (uint8_t*)d_out_prep_msgs + off * c.seed : q->d_msgs;
         int32_t r = prep_core(q, m, N + off * 16, PS ? PS + off * c.ps_bytes : nullptr, H + off * c.his_bytes,
