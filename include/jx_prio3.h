@@ -19,10 +19,19 @@
  *  - Every function returns int32 status: 0 = OK, < 0 = engine error (JX_E_*).
  *    Per-report preparation failures are NOT errors: they are verdict bytes.
  *  - The caller owns every host buffer; it is borrowed for the duration of the call.
- *  - An engine owns its device memory and one HIP stream on one device. Every entry point takes the
- *    engine's mutex for the duration of the call, so one engine per GPU can serve concurrent
- *    aggregation jobs from several host threads; the device work of the calls is serialized on the
- *    engine stream. What a job keeps between calls (its prepared reports) is a batch handle.
+ *  - An engine is one task's handle on one device (VdafOps per task, aggregator/src/aggregator.rs:
+ *    1156-1183): its verify key, its resident batches, its running aggregations and one HIP stream.
+ *    It holds no launch staging between calls: staging is checked out of the device's arena per call
+ *    and handed back stream-ordered, and resident batches come from the same arena (jx_engine_memory),
+ *    so any number of engines (tasks) share one GPU's HBM. Every entry point takes the engine's mutex
+ *    for the duration of the call, so one engine can serve concurrent aggregation jobs from several
+ *    host threads; the device work of the calls is serialized on the engine stream. What a job keeps
+ *    between calls (its prepared reports) is a batch handle.
+ *  - Coalesced prepares (jx_engine_coalesce): with coalescing on, jx_helper_prep_batch and
+ *    jx_leader_prep_init_batch of jobs up to a quarter of a launch join the device's next shared launch
+ *    with the concurrent jobs of every coalescing engine of the same Prio3 instance on the device (each
+ *    report with its own engine's verify key), and wait for it without holding the engine mutex. Results,
+ *    batches and errors are per job, exactly as without coalescing.
  *  - Host-buffer entry points are synchronous. Device-pointer entry points (*_device) are
  *    asynchronous on the engine stream, a NON-BLOCKING stream that orders itself after nothing:
  *    PRODUCER ORDERING is the caller's. Before a *_device call whose inputs were written by work
@@ -126,6 +135,40 @@ int32_t jx_engine_set_capacity(jx_engine* e, uint64_t reports);
  * Calls naming a released or unknown batch return JX_E_STATE; a report count other than the
  * batch's returns JX_E_INVALID. */
 
+/* Device memory of the engine and of its device's arena (shared by every engine on the device), and
+ * the engine's coalescer (jx_engine_coalesce). */
+typedef struct {
+  uint64_t resident_batches;   /* this engine's resident batches */
+  uint64_t batch_bytes;        /* device bytes they hold (arena slabs) */
+  uint64_t arena_budget;       /* bytes the device arena may hold (JX_ARENA_GB, default 90% of HBM) */
+  uint64_t arena_allocated;    /* bytes it holds: checked out + idle */
+  uint64_t arena_in_use;       /* checked out now (staging of calls in progress + resident batches) */
+  uint64_t arena_peak;         /* max arena_in_use */
+  uint64_t arena_allocs;       /* device allocations it made */
+  uint64_t arena_reuses;       /* check-outs served from idle slabs */
+  uint64_t arena_waits;        /* check-outs that waited for another call's staging */
+  uint64_t arena_engines;      /* live engines on the device */
+  uint64_t last_pipelines;     /* pipelines the engine's last fused call ran */
+  uint64_t coalesced_launches; /* launches of the device coalescer this engine uses (all its engines) */
+  uint64_t coalesced_jobs;
+  uint64_t coalesced_reports;
+  uint64_t coalesce_window_us; /* its current gathering window */
+  /* phase totals over the coalescer's launches (us): gathering (first job -> closed), the callers' input
+   * copies after the close, queueing the launch, the device (queued -> done) */
+  uint64_t coalesce_gather_us;
+  uint64_t coalesce_copy_us;
+  uint64_t coalesce_enqueue_us;
+  uint64_t coalesce_device_us;
+  uint64_t arena_cross_stream_waits; /* check-outs that had to wait for another stream's work */
+} jx_memory_stats;
+int32_t jx_engine_memory(const jx_engine* e, jx_memory_stats* out);
+
+/* Coalesced prepares (Conventions). enable != 0 joins the device coalescer of this Prio3 instance;
+ * window_us: how long a launch gathers jobs after its first one arrives (0 = automatic: half the recent
+ * launch latency, 20 us .. 2 ms; a launch also closes once it holds as many jobs as the previous one, or
+ * a full launch). Calls already waiting are unaffected by a later disable. */
+int32_t jx_engine_coalesce(jx_engine* e, int32_t enable, uint32_t window_us);
+
 /* Batched helper_initialized + evaluate for n reports (host buffers).
  * out_verdicts[n] receives JX_FINISHED or a failure code; out_prep_msgs[n x PM] the outbound
  * Finish{prep_msg} payload (meaningful where verdict == JX_FINISHED); out_output_shares
@@ -189,6 +232,12 @@ int32_t jx_leader_prep_init_device(jx_engine* e, uint64_t n, const void* d_nonce
                                    uint64_t* out_batch_id);
 int32_t jx_leader_prep_finish_device(jx_engine* e, uint64_t batch_id, uint64_t n, const void* d_prep_msgs,
                                      const void* d_peer_verdicts, void* d_out_verdicts);
+/* jx_leader_prep_init_device with an explicit row stride of d_leader_input_shares (0 = LIS; otherwise
+ * >= LIS and a multiple of 16). The leader assembles these rows after HPKE open, so it can pad them for
+ * free: with a stride that is a multiple of 128 the in-place FLP kernels read whole cache lines. */
+int32_t jx_leader_prep_init_device_ex(jx_engine* e, uint64_t n, const void* d_nonces, const void* d_public_shares,
+                                      const void* d_leader_input_shares, uint64_t lis_stride, void* d_out_prep_shares,
+                                      void* d_out_verdicts, uint64_t* out_batch_id);
 
 /* Accumulate the output shares of the resident batch `batch_id` (helper, or leader after finish) into
  * the engine's running batch aggregations (the engine as one shard, §8e): report i is added iff
@@ -196,7 +245,9 @@ int32_t jx_leader_prep_finish_device(jx_engine* e, uint64_t batch_id, uint64_t n
  * `segment[i]` (any u32 batch-aggregation id; segment nullable = 0). Adds to the aggregate share, the
  * report count and the ReportIdChecksum (XOR of SHA-256(report id)). Any number of segments is handled
  * in one pass over the batch (device counting sort by segment). The batch is released: it is
- * accumulated at most once (a second call returns JX_E_STATE). */
+ * accumulated at most once (a second call returns JX_E_STATE). The call returns once the accumulation is
+ * queued on the engine stream (the host arrays are consumed before it returns); later calls on the engine
+ * see its result (jx_aggregate_read / jx_engine_sync wait for it). */
 int32_t jx_accumulate(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t* accept_mask,
                       const uint32_t* segment);
 /* Same with device arrays: d_accept_mask (nullable) and d_segment (nullable = all reports into
@@ -287,8 +338,10 @@ int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]);
  *   option 4: pipelines of jx_helper_prep_aggregate_device / jx_helper_prep_aggregate: 0 automatic
  *             (when a call of one segment spans two or more launches: 2 for the device form, 3 for the
  *             host form), 1 one stream, 2..4 that many (each with its own stream and staging; the
- *             launches alternate over them, their accumulations stay in launch order).
- * The environment variables JX_K1_SPLIT and JX_PIPES set options 3 and 4 at create. */
+ *             launches alternate over them, their accumulations stay in launch order). A call runs with
+ *             fewer when the arena cannot stage them all at once (jx_engine_memory: last_pipelines);
+ *   option 5: reports per launch of the fused paths: 0 automatic (whole K1 rounds within ~48 GiB of
+ *             staging), else >= 64 (rounded down to a multiple of 64). */
 int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value);
 
 const char* jx_status_str(int32_t status);

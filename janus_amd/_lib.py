@@ -25,6 +25,7 @@ EXPORTED_SYMBOLS = (
     "jx_shard_record_combine_device", "jx_engine_sync", "jx_engine_stream", "jx_engine_timing",
     "jx_engine_timing_read", "jx_engine_debug", "jx_status_str", "jx_last_error",
     "jx_engine_wait_stream", "jx_engine_join_stream", "jx_engine_wait_event", "jx_engine_record_event",
+    "jx_engine_memory", "jx_engine_coalesce", "jx_leader_prep_init_device_ex",
 )
 
 _lib = None
@@ -33,6 +34,14 @@ _lib = None
 class JxParams(ctypes.Structure):
     _fields_ = [("algo_id", ctypes.c_uint32), ("bits", ctypes.c_uint32), ("length", ctypes.c_uint32),
                 ("chunk_length", ctypes.c_uint32), ("num_proofs", ctypes.c_uint32)]
+
+
+class JxMemoryStats(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_uint64) for name in (
+        "resident_batches", "batch_bytes", "arena_budget", "arena_allocated", "arena_in_use", "arena_peak",
+        "arena_allocs", "arena_reuses", "arena_waits", "arena_engines", "last_pipelines", "coalesced_launches",
+        "coalesced_jobs", "coalesced_reports", "coalesce_window_us", "coalesce_gather_us", "coalesce_copy_us",
+        "coalesce_enqueue_us", "coalesce_device_us", "arena_cross_stream_waits")]
 
 
 class EngineError(RuntimeError):
@@ -74,6 +83,9 @@ def load():
         "jx_leader_prep_init_batch": (i32, [vp, u64, u8p, u8p, u8p, u8p, u8p, P(u64)]),
         "jx_leader_prep_finish_batch": (i32, [vp, u64, u64, u8p, u8p, u8p]),
         "jx_leader_prep_init_device": (i32, [vp, u64, vp, vp, vp, vp, vp, P(u64)]),
+        "jx_leader_prep_init_device_ex": (i32, [vp, u64, vp, vp, vp, u64, vp, vp, P(u64)]),
+        "jx_engine_memory": (i32, [vp, P(JxMemoryStats)]),
+        "jx_engine_coalesce": (i32, [vp, i32, u32]),
         "jx_leader_prep_finish_device": (i32, [vp, u64, u64, vp, vp, vp]),
         "jx_accumulate": (i32, [vp, u64, u64, u8p, u8p]),
         "jx_accumulate_device": (i32, [vp, u64, u64, vp, vp, P(u32), u32]),

@@ -9,9 +9,10 @@ import subprocess
 import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-SOURCES = [os.path.join(_HERE, "csrc", f) for f in ("jx_kernels.hip", "jx_engine.cpp", "jx_hpke.hip", "jx_mp64.hip")]
+SOURCES = [os.path.join(_HERE, "csrc", f) for f in ("jx_kernels.hip", "jx_engine.cpp", "jx_arena.cpp", "jx_coalesce.cpp",
+                                                  "jx_hpke.hip", "jx_mp64.hip")]
 HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("jx_field.h", "jx_keccak.h", "jx_sha256.h", "jx_kernels.h",
-                                                  "jx_hpke.h", "jx_sha_aes.h")]
+                                                  "jx_hpke.h", "jx_sha_aes.h", "jx_engine_internal.h")]
 OUT = os.path.join(_HERE, "lib", "libjanus_prio3.so")
 # jx_mp64.hip: keep the LDS for the AES table (the AMDGPU backend would otherwise move a small private
 # array of the out-of-line helpers into LDS, +16 KiB per workgroup, one workgroup less per CU)

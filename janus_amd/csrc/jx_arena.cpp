@@ -1,0 +1,175 @@
+// jx_arena.cpp — the per-device memory arena every engine on a GPU draws from.
+//
+// Janus runs one VdafOps per task (aggregator/src/aggregator.rs:1156-1183), so an aggregator with many
+// tasks of one Prio3 instance holds many engines on one GPU. Per-engine staging sized for full-device
+// launches (tens of GB for SumVec 8x1000/88) would exhaust the 288 GB of HBM after a handful of tasks.
+// Instead, staging is checked out of this arena per call and handed back stream-ordered when the call
+// has queued its last use: the slab's event is recorded on the user's stream, and the next user's stream
+// waits on that event before touching it. The host never blocks on a reuse. Resident batches (a job's
+// output shares between its prepare and its accumulation) come from the same arena, so the arena's
+// budget bounds everything the engines hold.
+//
+// Budget: JX_ARENA_GB, or 90 % of the device's memory at first use. A request that does not fit first
+// frees idle slabs, then (for per-call staging, by a caller that holds no slab) waits for another caller's
+// staging to come back; otherwise JX_E_NOMEM.
+#include <cstdlib>
+
+#include "jx_engine_internal.h"
+
+namespace jxi {
+
+static std::mutex g_mu;
+static std::map<int, Arena*> g_arenas;  // process lifetime
+
+Arena* arena_for(int device) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_arenas.find(device);
+  if (it != g_arenas.end()) return it->second;
+  Arena* A = new Arena();
+  A->device = device;
+  size_t fr = 0, tot = 0;
+  (void)hipSetDevice(device);
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) tot = 0;
+  A->budget = tot ? (uint64_t)(tot * 0.9) : (64ull << 30);
+  if (const char* env = getenv("JX_ARENA_GB")) {
+    const uint64_t gb = strtoull(env, nullptr, 10);
+    if (gb >= 1) A->budget = gb << 30;
+  }
+  g_arenas.emplace(device, A);
+  return A;
+}
+
+static void slab_destroy(Arena* A, Slab& s) {
+  if (s.ev) {
+    (void)hipEventSynchronize(s.ev);  // its last user's work
+    (void)hipEventDestroy(s.ev);
+  }
+  (void)hipFree(s.p);
+  A->allocated -= s.bytes;
+  A->frees++;
+  s = Slab{};
+}
+
+// with A->mu held: free the largest idle slab
+static bool trim_one(Arena* A) {
+  if (A->free.empty()) return false;
+  auto it = std::prev(A->free.end());
+  Slab s = it->second;
+  A->free.erase(it);
+  slab_destroy(A, s);
+  return true;
+}
+
+static void account_out(Arena* A, const Slab& s) {
+  A->in_use += s.bytes;
+  if (s.staging) A->in_use_staging += s.bytes;
+  if (A->in_use > A->peak) A->peak = A->in_use;
+}
+
+// Staging sizes round up to size classes (4 per octave, <= 19 % slack) so that launches of varying report
+// counts find idle slabs to reuse instead of allocating a new size each time.
+static size_t size_class(size_t b) {
+  if (b <= (1u << 20)) return align256(b);
+  int e = 63 - __builtin_clzll((unsigned long long)b);  // 2^e <= b < 2^(e+1)
+  const size_t step = (size_t)1 << (e - 2);
+  return (b + step - 1) / step * step;
+}
+
+hipError_t arena_get(Arena* A, size_t bytes, hipStream_t s, bool staging, bool may_wait, Slab& out) {
+  bytes = staging ? size_class(bytes ? bytes : 1) : align256(bytes ? bytes : 1);
+  std::unique_lock<std::mutex> lk(A->mu);
+  for (;;) {
+    // Idle slabs at most 2x (+1 MiB) larger (a small request does not pin a big slab). Prefer, best fit
+    // first, one whose last user is this stream or has finished: taking a slab another stream is still
+    // using would make this stream wait for that work (two concurrent launches would run one after the
+    // other). Such a slab is taken only when the budget leaves no room for a new one.
+    auto lo = A->free.lower_bound(bytes);
+    auto hi = A->free.upper_bound(2 * bytes + (1u << 20));
+    auto pick = A->free.end(), busy = A->free.end();
+    for (auto it = lo; it != hi; ++it) {
+      if (it->second.last == s || !it->second.last || hipEventQuery(it->second.ev) == hipSuccess) {
+        pick = it;
+        break;
+      }
+      if (busy == A->free.end()) busy = it;
+    }
+    (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
+    const bool room = A->allocated + bytes <= A->budget;
+    if (pick == A->free.end() && busy != A->free.end() && !room) pick = busy;
+    if (pick != A->free.end()) {
+      out = pick->second;
+      A->free.erase(pick);
+      out.staging = staging;
+      account_out(A, out);
+      A->reuses++;
+      if (out.last && out.last != s) A->cross_waits += pick == busy;
+      return hipStreamWaitEvent(s, out.ev, 0);  // after the slab's last user (a never-recorded event: no wait)
+    }
+    while (A->allocated + bytes > A->budget && trim_one(A)) {
+    }
+    if (A->allocated + bytes <= A->budget) {
+      void* p = nullptr;
+      hipError_t st = hipMalloc(&p, bytes);
+      if (st == hipErrorOutOfMemory) {  // the device (other users, torch) is fuller than the budget
+        (void)hipGetLastError();
+        while (trim_one(A)) {
+        }
+        st = hipMalloc(&p, bytes);
+      }
+      if (st == hipSuccess) {
+        hipEvent_t ev = nullptr;
+        st = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (st != hipSuccess) {
+          (void)hipFree(p);
+          return st;
+        }
+        out = Slab{p, bytes, ev, nullptr, staging};
+        A->allocated += bytes;
+        A->allocs++;
+        account_out(A, out);
+        return hipSuccess;
+      }
+      if (st != hipErrorOutOfMemory) return st;
+      (void)hipGetLastError();
+    }
+    // what is checked out holds the memory: staging comes back when its call has queued its work
+    if (!may_wait || A->in_use_staging == 0) return hipErrorOutOfMemory;
+    A->waits++;
+    A->cv.wait(lk);
+  }
+}
+
+void arena_put(Arena* A, Slab& slab, hipStream_t s) {
+  if (!slab.p) return;
+  (void)hipEventRecord(slab.ev, s);
+  slab.last = s;
+  {
+    std::lock_guard<std::mutex> lk(A->mu);
+    A->in_use -= slab.bytes;
+    if (slab.staging) A->in_use_staging -= slab.bytes;
+    A->free.emplace(slab.bytes, slab);
+  }
+  A->cv.notify_all();
+  slab = Slab{};
+}
+
+void arena_trim(Arena* A) {
+  std::lock_guard<std::mutex> lk(A->mu);
+  while (trim_one(A)) {
+  }
+}
+
+void arena_engine_add(Arena* A) {
+  std::lock_guard<std::mutex> lk(A->mu);
+  A->engines++;
+}
+
+void arena_engine_remove(Arena* A) {
+  std::lock_guard<std::mutex> lk(A->mu);
+  if (A->engines) A->engines--;
+  if (A->engines == 0)  // nothing left to reuse the idle slabs: give the memory back to the device
+    while (trim_one(A)) {
+    }
+}
+
+}  // namespace jxi

@@ -19,143 +19,26 @@
 #include <unordered_set>
 #include <vector>
 
-#include "../../include/jx_prio3.h"
+#include "jx_engine_internal.h"
 #include "jx_field.h"
-#include "jx_kernels.h"
 #include "jx_sha_aes.h"
 
 using namespace jx;
-
-namespace {
-
-// One batch aggregation's device state (aggregate share, report count, ReportIdChecksum).
-struct Segment {
-  uint4* agg = nullptr;                 // [out_len] canonical
-  uint32_t* checksum = nullptr;         // [8]
-  unsigned long long* count = nullptr;  // [1]
-};
-
-// A resident prepared batch: one aggregation job's reports after prepare_init, holding what
-// prepare_next and the accumulation need once the prepare call has returned. Staging (measurement
-// and proof shares, coefficients, FLP partials) is per-call scratch shared by every batch; the
-// output shares, verdicts, prep messages (leader: the corrected joint-rand seeds, its prepare state)
-// and report ids live here until jx_batch_release / jx_accumulate. Any number of batches can be
-// resident, so the aggregation jobs Janus steps concurrently (max_concurrent_job_workers,
-// aggregator/src/binary_utils/job_driver.rs:116-138; a leader job holds its prepare state across
-// the helper round trip, aggregation_job_driver.rs:396-416 -> :540-701) each keep their own.
-struct Batch {
-  uint64_t n = 0;
-  bool leader = false;
-  bool finished = false;      // leader: prepare_next has run (once)
-  void* mem = nullptr;        // one allocation: outs | verdicts | msgs | nonces
-  size_t bytes = 0;
-  uint4* outs = nullptr;      // interleaved [n/64][out_len][64] (Histogram: the measurement share)
-  uint8_t* verdicts = nullptr;
-  uint8_t* msgs = nullptr;
-  uint8_t* nonces = nullptr;  // report ids, for the checksums
-};
-
-// What an accumulation reads: output shares, verdicts, report ids of n reports.
-struct AccSrc {
-  uint64_t n;
-  const uint4* outs;
-  const uint8_t* verdicts;
-  const uint8_t* nonces;
-};
-
-enum { ST_XOF = 0, ST_FLP = 1, ST_ACC = 2, ST_SLOW = 3, NST = 4 };
-
-}  // namespace
-
-struct jx_engine {
-  Cfg cfg{};
-  int device = 0;
-  hipStream_t stream = nullptr;
-  std::mutex mu;  // held by every entry point for the duration of the call
-  uint64_t cap = 0;  // reports (multiple of 64)
-  uint64_t meas_cap = 0;  // reports of measurement-share staging (allocated only when needed, see leader_inplace)
-  uint64_t default_chunk = 0;
-  uint64_t round_reports = 0;  // reports that fill every K1 wave slot once (0: unknown)
-  // inputs (engine-owned copies for host entry points)
-  uint8_t *d_nonces = nullptr, *d_ps = nullptr, *d_his = nullptr, *d_lps = nullptr;
-  // staging
-  uint4 *d_meas = nullptr, *d_proof = nullptr, *d_outs = nullptr, *d_coef = nullptr, *d_consts = nullptr;
-  uint32_t* d_flags = nullptr;
-  uint4* d_part = nullptr;
-  uint8_t *d_verdicts = nullptr, *d_msgs = nullptr;  // the fused paths' per-launch results
-  // accumulation scratch: partials + selection bytes
-  uint64_t* d_partials = nullptr;
-  uint32_t acc_chunks = 0;  // report chunks of the accumulate kernel (0: acc_nchunks picks)
-  uint8_t* d_hout = nullptr;  // the host fused path with pipelines: verdicts || prep messages of the call
-  uint64_t hout_bytes = 0;
-  uint8_t* d_tmp = nullptr;  // output-share transpose / aggregate encode / records
-  size_t tmp_bytes = 0;
-  uint8_t* d_mask = nullptr;
-  uint32_t* d_seg = nullptr;
-  // leader role staging (allocated on first leader call): input shares, outbound prep shares,
-  // inbound prep messages
-  uint8_t *d_lis = nullptr, *d_lps_out = nullptr, *d_in_msgs = nullptr;
-  uint64_t leader_cap = 0;
-  std::map<uint32_t, Segment> segs;  // running batch aggregations (the engine as one shard)
-  // resident prepared batches by handle; handles are never reused
-  std::map<uint64_t, Batch> batches;
-  uint64_t batch_gen = 0, last_batch = 0;
-  std::multimap<size_t, void*> batch_pool;  // released batch allocations, reused by later batches
-  // per-call batch-aggregation deltas (jx_batch_aggregate_records): agg [ns][out_len] | count [ns] | checksum [ns][8]
-  uint8_t* d_delta = nullptr;
-  size_t delta_bytes = 0;
-  // segmented accumulation scratch (allocated on first use)
-  uint32_t* d_segx = nullptr;  // cnt, off, cursor [SEG_MAX each], ioff [SEG_MAX + 1], nitems [2]
-  uint32_t* d_perm = nullptr;
-  uint64_t perm_cap = 0;
-  uint4* d_items = nullptr;
-  uint64_t* d_spart = nullptr;
-  uint64_t spart_wmax = 0;
-  void** d_ptrs = nullptr;  // [3][nptrs]: aggs, counts, checksums of the call's segments
-  uint64_t ptrs_cap = 0;
-  // pinned host copies of the pointer table, double-buffered: buffer k is rewritten only after the
-  // upload that last read it has completed (ev_ptrs[k]), so no call waits for its own work
-  void** h_ptrs[2] = {nullptr, nullptr};
-  uint64_t h_ptrs_cap[2] = {0, 0};
-  hipEvent_t ev_ptrs[2] = {nullptr, nullptr};
-  int ptrs_k = 0;
-  std::vector<uint32_t> h_dense;
-  uint32_t* d_err = nullptr;  // combine kernels: non-canonical input seen (reported by jx_engine_sync)
-  // timing
-  bool timing = false;
-  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
-  double ms[NST] = {0, 0, 0, 0};
-  uint64_t launches[NST] = {0, 0, 0, 0};
-  uint32_t force_slow = 0;
-  uint32_t k1_split = 0;  // helper K1: 0 automatic, 3 lane-split, 5 fused, 6 lane pairs (JX_K1_SPLIT, debug option 3)
-  // producer / consumer ordering (jx_engine_wait_stream / jx_engine_join_stream): reused events
-  hipEvent_t ev_wait = nullptr, ev_join = nullptr;
-  // Concurrent pipelines of the fused device path (jx_helper_prep_aggregate_device, pipes_for): child
-  // engines with their own stream and staging run K1 -> K3 -> K4 of alternate launches, so launches of
-  // different phases share the device; the K4s stay in launch order through ev_pipe.
-  std::vector<jx_engine*> pipes;
-  uint32_t npipes = 0;  // 0: automatic (JX_PIPES, debug option 4)
-  bool is_pipe = false;  // a child: d_consts belongs to the parent
-  bool pipes_nomem = false;  // the pipelines' staging did not fit once: single stream from then on
-  hipEvent_t ev_pipe = nullptr;
-};
+using namespace jxi;
 
 // The message of the last failing call, per calling thread: an engine serves several host threads,
 // and each reads the error of its own call (jx_last_error), never another thread's.
 static thread_local std::string t_err;
 
-static int32_t fail(jx_engine* e, int32_t code, const std::string& msg) {
+namespace jxi {
+std::string& thread_error() { return t_err; }
+int32_t fail(jx_engine* e, int32_t code, const std::string& msg) {
   (void)e;
   t_err = msg;
   return code;
 }
-#define HIPCHK(e, call)                                                                                   \
-  do {                                                                                                    \
-    hipError_t _st = (call);                                                                              \
-    if (_st != hipSuccess)                                                                                \
-      return fail((e), _st == hipErrorOutOfMemory ? JX_E_NOMEM : JX_E_HIP,                                \
-                  std::string(#call) + ": " + hipGetErrorString(_st));                                    \
-  } while (0)
+}  // namespace jxi
+
 // every entry point: the engine mutex for the call, and a fresh per-thread error message
 #define LOCK(e)                                   \
   std::lock_guard<std::mutex> _lk((e)->mu);       \
@@ -451,30 +334,7 @@ static std::vector<uint4> make_consts(const Cfg& c) {
   return t;
 }
 
-// ---------------------------------------------------------------------------- buffers
-
-static void free_staging(jx_engine* e) {
-  void* ptrs[] = {e->d_nonces, e->d_ps,       e->d_his,     e->d_lps,  e->d_meas, e->d_proof, e->d_outs,
-                  e->d_coef,   e->d_flags,    e->d_verdicts, e->d_msgs, e->d_partials, e->d_mask, e->d_seg,
-                  e->d_part};
-  for (void* p : ptrs)
-    if (p) (void)hipFree(p);
-  e->d_nonces = e->d_ps = e->d_his = e->d_lps = nullptr;
-  e->d_meas = e->d_proof = e->d_outs = e->d_coef = nullptr;
-  e->d_flags = nullptr;
-  e->d_part = nullptr;
-  e->d_verdicts = e->d_msgs = nullptr;
-  e->d_partials = nullptr;
-  e->d_mask = nullptr;
-  e->d_seg = nullptr;
-  e->cap = 0;
-  e->meas_cap = 0;
-  for (uint8_t** p : {&e->d_lis, &e->d_lps_out, &e->d_in_msgs}) {
-    if (*p) (void)hipFree(*p);
-    *p = nullptr;
-  }
-  e->leader_cap = 0;
-}
+// ---------------------------------------------------------------------------- staging (per call, from the arena)
 
 // staging element bytes: the multiproof Field64 kernels use 8-byte elements (outputs stay uint4)
 static uint32_t stage_eb(const Cfg& c) { return c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? 8u : 16u; }
@@ -490,6 +350,20 @@ static bool leader_inplace(const Cfg& c) {
   return c.algo == ALGO_SUM || c.algo == ALGO_SUMVEC || c.algo == ALGO_FIXEDPOINT_L2;
 }
 
+namespace jxi {
+size_t align256(size_t v) { return (v + 255) / 256 * 256; }
+uint32_t vk_row_bytes(const Cfg& c) { return c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? 64u : 16u; }
+void vk_row(const Cfg& c, uint8_t* dst) {
+  if (c.algo == ALGO_SUMVEC_F64_MULTIPROOF) {  // the HMAC-SHA256 pads of the 32-byte key: ist[8] || ost[8]
+    memcpy(dst, c.vk_ist, 32);
+    memcpy(dst + 32, c.vk_ost, 32);
+  } else {
+    memcpy(dst, c.vk, 16);
+  }
+}
+}  // namespace jxi
+
+// Staging bytes of one report for a fused helper launch (the launch-size budget, jx_engine_create_ex).
 static uint64_t per_report_bytes(const Cfg& c, bool with_meas = true) {
   uint64_t b = (uint64_t)stage_eb(c) * ((with_meas ? c.meas_len : 0) + (uint64_t)c.np * c.proof_len + coef_elems(c));
   b += 16ull * (c.out_is_meas ? 0 : c.out_len);
@@ -506,78 +380,108 @@ static uint32_t acc_nchunks(const jx_engine* e) {
   return want < 16u ? 16u : (want > 4096u ? 4096u : want);
 }
 
-// Device allocation. On out-of-memory the released-batch pool is handed back to the device and the
-// allocation tried once more, so idle pooled batches never cause a JX_E_NOMEM.
-static void trim_batch_pool(jx_engine* e) {
-  if (e->batch_pool.empty()) return;
-  (void)hipStreamSynchronize(e->stream);  // queued work may still use a pooled allocation
-  for (auto& kv : e->batch_pool) (void)hipFree(kv.second);
-  e->batch_pool.clear();
-}
-static hipError_t dev_alloc(jx_engine* e, void** p, size_t bytes) {
-  hipError_t st = hipMalloc(p, bytes ? bytes : 16);
-  if (st == hipErrorOutOfMemory && !e->batch_pool.empty()) {
-    (void)hipGetLastError();
-    trim_batch_pool(e);
-    st = hipMalloc(p, bytes ? bytes : 16);
+// Lay the regions named by `fl` for `cap` reports out from `base` (nullptr: only size them).
+static size_t stage_layout(jx_engine* e, uint64_t cap, uint32_t fl, uint8_t* base) {
+  const Cfg& c = e->cfg;
+  const uint64_t eb = stage_eb(c);
+  size_t off = 0;
+  auto take = [&](auto*& p, size_t bytes) {
+    using T = std::remove_reference_t<decltype(p)>;
+    if (base) p = reinterpret_cast<T>(base + off);
+    off += align256(bytes ? bytes : 1);
+  };
+  if (fl & SG_IN) {
+    take(e->d_nonces, cap * 16);
+    take(e->d_ps, cap * c.ps_bytes);
   }
-  if (st != hipSuccess) *p = nullptr;
-  return st;
+  if (fl & SG_HIN) {
+    take(e->d_his, cap * c.his_bytes);
+    take(e->d_lps, cap * c.lps_bytes);
+  }
+  if (fl & SG_MEAS) take(e->d_meas, cap * c.meas_len * eb);
+  if (fl & SG_PREP) {
+    take(e->d_proof, cap * c.np * c.proof_len * eb);
+    if (!outs_alias_meas(c)) take(e->d_outs, cap * c.out_len * 16);
+    take(e->d_coef, cap * coef_elems(c) * eb);
+    take(e->d_flags, cap * 4);
+    take(e->d_part, cap * part_bytes(c));
+  }
+  if (fl & SG_RES) {
+    take(e->d_verdicts, cap);
+    take(e->d_msgs, cap * c.seed);
+  }
+  if (fl & SG_ACC) {
+    take(e->d_mask, cap);
+    take(e->d_seg, cap * 4);
+    take(e->d_partials, (size_t)acc_nchunks(e) * c.out_len * 3 * sizeof(uint64_t) + cap);
+  }
+  if (fl & SG_LEAD) {
+    take(e->d_lis, cap * e->lis_stride);
+    take(e->d_lps_out, cap * c.lps_bytes);
+  }
+  if (fl & SG_LMSG) take(e->d_in_msgs, cap * c.seed);
+  if (fl & SG_VK) take(e->d_vkeys, cap * vk_row_bytes(c));
+  if (fl & SG_JOBS) take(e->d_jobs, (size_t)MAX_JOBS_PER_LAUNCH * sizeof(JobSlice));
+  return off;
+}
+
+static void stage_clear(jx_engine* e) {
+  e->d_nonces = e->d_ps = e->d_his = e->d_lps = nullptr;
+  e->d_meas = e->d_proof = e->d_outs = e->d_coef = nullptr;
+  e->d_flags = nullptr;
+  e->d_part = nullptr;
+  e->d_verdicts = e->d_msgs = nullptr;
+  e->d_partials = nullptr;
+  e->d_mask = nullptr;
+  e->d_seg = nullptr;
+  e->d_lis = e->d_lps_out = e->d_in_msgs = nullptr;
+  e->d_vkeys = nullptr;
+  e->d_jobs = nullptr;
+  e->cap = 0;
+  e->stage_flags = 0;
+}
+
+namespace jxi {
+size_t stage_bytes(const jx_engine* e, uint64_t cap, uint32_t flags) {
+  return stage_layout(const_cast<jx_engine*>(e), (cap + 63) / 64 * 64, flags, nullptr);
 }
 
 // JX_E_NOMEM naming what holds the device memory (resident batches are the caller's to release).
 static int32_t nomem(jx_engine* e, const char* what, size_t bytes) {
   uint64_t held = 0;
-  for (auto& kv : e->batches) held += kv.second.bytes;
+  for (auto& kv : e->batches) held += kv.second.slab.bytes;
+  Arena* A = e->arena;
   return fail(e, JX_E_NOMEM,
               std::string(what) + ": out of device memory allocating " + std::to_string(bytes) + " B; " +
-                  std::to_string(e->batches.size()) + " resident batches hold " + std::to_string(held) +
-                  " B (release finished or abandoned jobs with jx_batch_release)");
+                  std::to_string(e->batches.size()) + " resident batches of this engine hold " + std::to_string(held) +
+                  " B; the device arena holds " + std::to_string(A->allocated) + " of its " + std::to_string(A->budget) +
+                  " B budget (release finished or abandoned jobs with jx_batch_release)");
 }
 
-static int32_t ensure_capacity(jx_engine* e, uint64_t n, bool need_meas = true) {
-  if (n <= e->cap) {
-    if (!need_meas || e->meas_cap >= e->cap) return JX_OK;
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    if (e->d_meas) (void)hipFree(e->d_meas);
-    e->d_meas = nullptr;
-    const size_t mb = e->cap * e->cfg.meas_len * stage_eb(e->cfg);
-    if (dev_alloc(e, (void**)&e->d_meas, mb) != hipSuccess) return nomem(e, "staging", mb);
-    e->meas_cap = e->cap;
-    return JX_OK;
-  }
-  HIPCHK(e, hipStreamSynchronize(e->stream));  // queued work may still read the old staging
-  free_staging(e);
-  const Cfg& c = e->cfg;
-  uint64_t cap = (n + 63) / 64 * 64;
-  auto A = [&](void** p, size_t bytes) -> hipError_t { return dev_alloc(e, p, bytes); };
-  HIPCHK(e, A((void**)&e->d_nonces, cap * 16));
-  HIPCHK(e, A((void**)&e->d_ps, cap * c.ps_bytes));
-  HIPCHK(e, A((void**)&e->d_his, cap * c.his_bytes));
-  HIPCHK(e, A((void**)&e->d_lps, cap * c.lps_bytes));
-  const uint64_t eb = stage_eb(c);
-  if (need_meas) {
-    HIPCHK(e, A((void**)&e->d_meas, cap * c.meas_len * eb));
-    e->meas_cap = cap;
-  }
-  HIPCHK(e, A((void**)&e->d_proof, cap * c.np * c.proof_len * eb));
-  if (!outs_alias_meas(c)) HIPCHK(e, A((void**)&e->d_outs, cap * c.out_len * 16));
-  HIPCHK(e, A((void**)&e->d_coef, cap * coef_elems(c) * eb));
-  HIPCHK(e, A((void**)&e->d_flags, cap * 4));
-  HIPCHK(e, A((void**)&e->d_part, cap * part_bytes(c)));
-  HIPCHK(e, A((void**)&e->d_verdicts, cap));
-  HIPCHK(e, A((void**)&e->d_msgs, cap * c.seed));
-  HIPCHK(e, A((void**)&e->d_mask, cap));
-  HIPCHK(e, A((void**)&e->d_seg, cap * 4));
-  size_t pbytes = (size_t)acc_nchunks(e) * c.out_len * 3 * sizeof(uint64_t) + cap;
-  HIPCHK(e, A((void**)&e->d_partials, pbytes));
-  HIPCHK(e, hipMemsetAsync(e->d_flags, 0, cap * 4, e->stream));
+int32_t stage_acquire(jx_engine* e, uint64_t n, uint32_t fl, Stage& st, bool may_wait) {
+  st.release();
+  const uint64_t cap = (n + 63) / 64 * 64;
+  const size_t bytes = stage_layout(e, cap, fl, nullptr);
+  hipError_t rc = arena_get(e->arena, bytes, e->stream, true, may_wait, st.slab);
+  if (rc == hipErrorOutOfMemory) return nomem(e, "staging", bytes);
+  HIPCHK(e, rc);
+  st.e = e;
+  stage_layout(e, cap, fl, (uint8_t*)st.slab.p);
   e->cap = cap;
+  e->stage_flags = fl;
   return JX_OK;
 }
 
+void Stage::release() {
+  if (!e) return;
+  arena_put(e->arena, slab, e->stream);
+  stage_clear(e);
+  e = nullptr;
+}
+}  // namespace jxi
+
 // the fused paths' output shares (engine staging)
-static uint4* staging_outs(jx_engine* e) { return outs_alias_meas(e->cfg) ? e->d_meas : e->d_outs; }
+uint4* jxi::staging_outs(jx_engine* e) { return outs_alias_meas(e->cfg) ? e->d_meas : e->d_outs; }
 
 static int32_t get_segment(jx_engine* e, uint32_t id, Segment** out) {
   auto it = e->segs.find(id);
@@ -599,7 +503,6 @@ static int32_t ensure_tmp(jx_engine* e, size_t bytes) {
   if (bytes <= e->tmp_bytes) return JX_OK;
   HIPCHK(e, hipStreamSynchronize(e->stream));
   if (e->d_tmp) (void)hipFree(e->d_tmp);
-  if (e->d_hout) (void)hipFree(e->d_hout);
   e->d_tmp = nullptr;
   e->tmp_bytes = 0;
   HIPCHK(e, hipMalloc((void**)&e->d_tmp, bytes));
@@ -609,11 +512,9 @@ static int32_t ensure_tmp(jx_engine* e, size_t bytes) {
 
 // ---------------------------------------------------------------------------- resident batches
 
-static size_t align256(size_t v) { return (v + 255) / 256 * 256; }
-
-// A new resident batch of n reports (handle in *id). Allocations of released batches are reused when
-// they fit (stream-ordered: every use of a batch is on the engine stream).
-static int32_t batch_new(jx_engine* e, uint64_t n, bool leader, uint64_t* id, Batch** out) {
+// A new resident batch of n reports (handle in *id), one arena allocation. Slabs handed back by released
+// batches (of any engine on the device) are reused stream-ordered.
+int32_t jxi::batch_new(jx_engine* e, uint64_t n, bool leader, uint64_t* id, Batch** out) {
   const Cfg& c = e->cfg;
   const uint64_t cap = (n + 63) / 64 * 64;
   const size_t o_outs = 0, o_ver = align256((size_t)cap * c.out_len * 16), o_msg = o_ver + align256(cap),
@@ -621,16 +522,10 @@ static int32_t batch_new(jx_engine* e, uint64_t n, bool leader, uint64_t* id, Ba
   Batch b;
   b.n = n;
   b.leader = leader;
-  auto it = e->batch_pool.lower_bound(bytes);
-  if (it != e->batch_pool.end() && it->first <= 2 * bytes + (1u << 20)) {
-    b.mem = it->second;
-    b.bytes = it->first;
-    e->batch_pool.erase(it);
-  } else {
-    if (dev_alloc(e, &b.mem, bytes ? bytes : 256) != hipSuccess) return nomem(e, "new batch", bytes);
-    b.bytes = bytes;
-  }
-  uint8_t* m = (uint8_t*)b.mem;
+  hipError_t st = arena_get(e->arena, bytes, e->stream, false, false, b.slab);
+  if (st == hipErrorOutOfMemory) return nomem(e, "new batch", bytes);
+  HIPCHK(e, st);
+  uint8_t* m = (uint8_t*)b.slab.p;
   b.outs = (uint4*)(m + o_outs);
   b.verdicts = m + o_ver;
   b.msgs = m + o_msg;
@@ -641,28 +536,15 @@ static int32_t batch_new(jx_engine* e, uint64_t n, bool leader, uint64_t* id, Ba
   return JX_OK;
 }
 
-// Keep at most this many bytes of released batch allocations for reuse.
-static constexpr size_t BATCH_POOL_MAX = 8ull << 30;
-
-static void batch_free(jx_engine* e, std::map<uint64_t, Batch>::iterator it) {
-  Batch& b = it->second;
-  size_t pooled = 0;
-  for (auto& kv : e->batch_pool) pooled += kv.first;
-  if (b.mem) {
-    if (pooled + b.bytes <= BATCH_POOL_MAX) {
-      e->batch_pool.emplace(b.bytes, b.mem);
-    } else {
-      (void)hipStreamSynchronize(e->stream);  // queued work may still read it
-      (void)hipFree(b.mem);
-    }
-  }
+void jxi::batch_free(jx_engine* e, std::map<uint64_t, Batch>::iterator it) {
+  arena_put(e->arena, it->second.slab, e->stream);  // reused after the work queued on the engine stream
   if (e->last_batch == it->first) e->last_batch = 0;
   e->batches.erase(it);
 }
 
 static int32_t find_batch(jx_engine* e, uint64_t id, uint64_t n, const char* what, Batch** out) {
   auto it = e->batches.find(id);
-  if (id == 0 || it == e->batches.end())
+  if (id == 0 || it == e->batches.end() || it->second.pending)
     return fail(e, JX_E_STATE, std::string(what) + ": batch id names no resident prepared batch (released or never made)");
   if (it->second.n != n)
     return fail(e, JX_E_INVALID, std::string(what) + ": report count differs from the batch's");
@@ -690,7 +572,7 @@ static hipError_t stage_end(jx_engine* e, int stage, hipEvent_t ev0) {
   e->pending.push_back({stage, {ev0, ev1}});
   return st;
 }
-static int32_t drain_timing(jx_engine* e) {
+int32_t jxi::drain_timing(jx_engine* e) {
   if (e->pending.empty()) return JX_OK;
   HIPCHK(e, hipStreamSynchronize(e->stream));
   for (auto& p : e->pending) {
@@ -711,9 +593,9 @@ static bool use_inplace(const jx_engine* e) { return leader_inplace(e->cfg); }
 // Prepare n <= cap reports whose inputs are at the given device pointers; the output shares go to
 // outs (a batch's buffer, or the staging of the fused paths), verdicts and prep messages / leader
 // seeds to verdicts / msgs.
-static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* his,
-                         const uint8_t* lps, uint8_t* verdicts, uint8_t* msgs, uint4* outs,
-                         const uint8_t* lis = nullptr, uint8_t* lps_out = nullptr) {
+int32_t jxi::prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* his,
+                       const uint8_t* lps, uint8_t* verdicts, uint8_t* msgs, uint4* outs, const uint8_t* lis,
+                       uint8_t* lps_out, uint64_t lis_rs, const uint8_t* vkeys) {
   const Cfg& c = e->cfg;
   const bool leader = lis != nullptr;
   Bufs b{};
@@ -723,12 +605,14 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
   b.his = his;
   b.lps = lps;
   b.lis = lis;
+  b.lis_rs = lis_rs ? lis_rs : c.lis_bytes;
+  b.vkeys = vkeys;
   b.lps_out = lps_out;
   b.leader = leader ? 1u : 0u;
   b.meas = outs_alias_meas(c) ? outs : e->d_meas;
   if (leader && use_inplace(e)) {
     b.meas_src = lis;
-    b.meas_rs = c.lis_bytes;
+    b.meas_rs = b.lis_rs;
   }
   b.proof = e->d_proof;
   b.outs = outs;
@@ -782,24 +666,6 @@ static int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const 
     HIPCHK(e, launch_flp(c, b, e->stream));
     HIPCHK(e, stage_end(e, ST_FLP, ev));
   }
-  return JX_OK;
-}
-
-static int32_t ensure_leader_capacity(jx_engine* e, uint64_t n) {
-  int32_t rc = ensure_capacity(e, n, !use_inplace(e));
-  if (rc) return rc;
-  if (n <= e->leader_cap && e->d_lis) return JX_OK;
-  HIPCHK(e, hipStreamSynchronize(e->stream));
-  for (uint8_t** p : {&e->d_lis, &e->d_lps_out, &e->d_in_msgs}) {
-    if (*p) (void)hipFree(*p);
-    *p = nullptr;
-  }
-  const Cfg& c = e->cfg;
-  const uint64_t cap = e->cap;
-  HIPCHK(e, dev_alloc(e, (void**)&e->d_lis, cap * c.lis_bytes));
-  HIPCHK(e, dev_alloc(e, (void**)&e->d_lps_out, cap * c.lps_bytes));
-  HIPCHK(e, dev_alloc(e, (void**)&e->d_in_msgs, cap * c.seed));
-  e->leader_cap = cap;
   return JX_OK;
 }
 
@@ -1028,61 +894,67 @@ static uint64_t launch_chunk(const jx_engine* e, uint64_t n) {
 // (LDS-DMA ring: HBM + limb products) and K4 (HBM): one after the other, every launch's waves are in the
 // same phase at the same time (the K1 waves of a round reach their FLP-coefficient tails together, K3 runs
 // at a throttled clock beside an idle Keccak pipe). With P pipelines the launches of one call alternate
-// over P child engines, each with its own stream and staging, so different launches' phases overlap; only
-// the K4s are ordered (they add into the same aggregation). Measured on MI355X with P independent engines
-// (tools/multi_engine_probe.py): SumVec 8x1000/88, 1.25M reports, 7.28M (one) -> 7.67M (two) -> 7.79M
-// reports/s (three). Used when a call spans >= 2 launches of one segment; not for Count (one tiny kernel)
-// or the multiproof path.
+// over P child engines, each with its own stream and per-call staging from the arena, so different
+// launches' phases overlap; only the K4s are ordered (they add into the same aggregation). Measured on
+// MI355X with P independent engines (tools/multi_engine_probe.py): SumVec 8x1000/88, 1.25M reports,
+// 7.28M (one) -> 7.67M (two) -> 7.79M reports/s (three). Used when a call spans >= 2 launches of one
+// segment; not for Count (one tiny kernel) or the multiproof path.
 // host: the host-buffer path, whose pageable copies also take turns (3 by default there: SumVec 1.25M
 // reports 5.02M -> 6.44M (two) -> 7.12M (three) reports/s including the copies, tools/bench_host_path.py).
 static uint32_t pipes_for(const jx_engine* e, uint64_t n, uint64_t chunk, bool many, bool host = false) {
   const Cfg& c = e->cfg;
-  if (many || e->pipes_nomem || c.algo == ALGO_COUNT || c.algo == ALGO_SUMVEC_F64_MULTIPROOF) return 1;
+  if (many || c.algo == ALGO_COUNT || c.algo == ALGO_SUMVEC_F64_MULTIPROOF) return 1;
   const uint64_t launches = (n + chunk - 1) / chunk;
   const uint64_t want = e->npipes ? e->npipes : (host ? 3 : 2);
   return (uint32_t)(launches < want ? launches : want);
 }
 
-// Create (once) and size the first P pipelines; false when their staging does not fit (the caller then
-// runs the single-stream path, and the pipelines' staging is handed back).
-static bool ensure_pipes(jx_engine* e, uint32_t P, uint64_t chunk) {
+jx_engine* jxi::new_child(jx_engine* parent) {
+  jx_engine* q = new jx_engine();
+  q->cfg = parent->cfg;
+  q->device = parent->device;
+  q->is_pipe = true;
+  q->arena = parent->arena;
+  q->d_consts = parent->d_consts;
+  q->default_chunk = parent->default_chunk;
+  q->auto_chunk = parent->auto_chunk;
+  q->round_reports = parent->round_reports;
+  q->lis_stride = parent->lis_stride;
+  if (hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&q->ev_join, hipEventDisableTiming) != hipSuccess) {
+    jx_engine_destroy(q);
+    return nullptr;
+  }
+  return q;
+}
+
+constexpr uint32_t MAX_PIPES = 4;
+
+// Staging for up to P pipelines: the first one may wait for the arena, the others take what is free
+// now (so two calls never wait on each other holding half their pipelines). *got = pipelines staged.
+static int32_t pipes_acquire(jx_engine* e, uint32_t P, uint64_t chunk, uint32_t flags, Stage* st, uint32_t* got) {
+  *got = 0;
   while (e->pipes.size() < P) {
-    jx_engine* q = new jx_engine();
-    q->cfg = e->cfg;
-    q->device = e->device;
-    q->is_pipe = true;
-    q->d_consts = e->d_consts;
-    q->default_chunk = e->default_chunk;
-    q->round_reports = e->round_reports;
-    if (hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&q->ev_join, hipEventDisableTiming) != hipSuccess) {
-      jx_engine_destroy(q);
-      return false;
-    }
+    jx_engine* q = new_child(e);
+    if (!q) return fail(e, JX_E_HIP, "pipelines: stream creation failed");
     e->pipes.push_back(q);
   }
-  if (!e->ev_pipe && hipEventCreateWithFlags(&e->ev_pipe, hipEventDisableTiming) != hipSuccess) return false;
+  if (!e->ev_pipe) HIPCHK(e, hipEventCreateWithFlags(&e->ev_pipe, hipEventDisableTiming));
   for (uint32_t k = 0; k < P; k++) {
     jx_engine* q = e->pipes[k];
     q->force_slow = e->force_slow;
     q->k1_split = e->k1_split;
     q->timing = e->timing;
-    if (q->acc_chunks != e->acc_chunks) {  // accumulate scratch is sized by the chunking
-      (void)hipStreamSynchronize(q->stream);
-      free_staging(q);
-      q->acc_chunks = e->acc_chunks;
+    q->acc_chunks = e->acc_chunks;
+    int32_t rc = stage_acquire(q, chunk, flags, st[k], k == 0);
+    if (rc) {
+      if (k == 0) return rc;
+      t_err.clear();  // run with the pipelines that fit (retried on the next call)
+      break;
     }
-    if (ensure_capacity(q, chunk) != JX_OK) {
-      for (jx_engine* r : e->pipes) {
-        (void)hipStreamSynchronize(r->stream);
-        free_staging(r);
-      }
-      t_err.clear();
-      e->pipes_nomem = true;  // not retried on every call (JX_STAGING_GB sizes one pipeline's launches)
-      return false;
-    }
+    *got = k + 1;
   }
-  return true;
+  return JX_OK;
 }
 
 // Move the pipelines' kernel timings into the engine's.
@@ -1099,6 +971,10 @@ static int32_t collect_pipe_timing(jx_engine* e) {
   }
   return JX_OK;
 }
+
+// measurement staging for a helper prepare whose outputs go to a batch (Histogram writes its
+// measurement share, which is its output share, straight into the batch)
+static uint32_t helper_meas_flag(const Cfg& c) { return outs_alias_meas(c) ? 0u : SG_MEAS; }
 
 // ---------------------------------------------------------------------------- C ABI
 
@@ -1120,6 +996,7 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
   std::string why;
   int32_t rc = make_cfg(params, verify_key, verify_key_len, e->cfg, why);
   if (rc) {
+    t_err = why;
     delete e;
     return rc;
   }
@@ -1128,6 +1005,9 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
     delete e;
     return JX_E_HIP;
   }
+  e->arena = arena_for(device);
+  arena_engine_add(e->arena);
+  e->lis_stride = e->cfg.lis_bytes;
   std::vector<uint4> consts = make_consts(e->cfg);
   // On the engine stream, synchronized on it alone: creating an engine orders nothing with the caller's
   // streams (that is jx_engine_wait_stream's job).
@@ -1140,44 +1020,28 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
     jx_engine_destroy(e);
     return JX_E_HIP;
   }
-  // Default chunk for the fused path: ~48 GiB of staging, enough for several K1 occupancy rounds of
+  // Reports per launch of the fused paths: ~48 GiB of staging, enough for several K1 occupancy rounds of
   // the small VDAFs. A VDAF whose reports need megabytes of staging (FixedPointBoundedL2VecSum at
   // length 10000: 2.8 MB) would fill only a few percent of the SIMDs at 48 GiB, and K1 is bound by
   // the per-report sponge latency (15k sequential permutations), so throughput scales with the
   // reports in flight: grow the budget toward one full K1 round, up to 1/3 of the device memory
-  // (two engines, e.g. leader and helper, still fit on one MI355X). JX_STAGING_GB / JX_CHUNK_REPORTS override.
+  // (two roles, e.g. leader and helper, still fit on one MI355X). Staging is checked out of the device
+  // arena per call, so this sizes launches, not what an idle engine holds. Debug option 5 overrides it.
   const uint64_t per = per_report_bytes(e->cfg);
-  if (const char* env = getenv("JX_K1_SPLIT")) {
-    const int v = atoi(env);
-    if (v == 0 || v == 3 || v == 5 || v == 6) e->k1_split = (uint32_t)v;
-  }
-  e->round_reports = k1_round_reports(e->cfg, device, e->k1_split);
-  if (const char* env = getenv("JX_PIPES")) {
-    const int v = atoi(env);
-    if (v >= 0 && v <= 4) e->npipes = (uint32_t)v;
-  }
+  e->round_reports = k1_round_reports(e->cfg, device, 0);
   uint64_t budget = 48ull << 30;
   size_t mem_free = 0, mem_total = 0;
-  if (hipMemGetInfo(&mem_free, &mem_total) == hipSuccess && e->round_reports &&
-      e->round_reports * per > budget) {
+  if (hipMemGetInfo(&mem_free, &mem_total) == hipSuccess && e->round_reports && e->round_reports * per > budget) {
     const uint64_t cap = mem_total / 3;
     budget = e->round_reports * per < cap ? e->round_reports * per : cap;
     if (budget < (48ull << 30)) budget = 48ull << 30;
-  }
-  if (const char* env = getenv("JX_STAGING_GB")) {
-    const uint64_t gb = strtoull(env, nullptr, 10);
-    if (gb >= 1) budget = gb << 30;
   }
   uint64_t chunk = budget / per;
   if (chunk > (1ull << 22)) chunk = 1ull << 22;
   chunk = chunk / 256 * 256;
   if (chunk < 256) chunk = 256;
   if (e->round_reports && chunk >= e->round_reports) chunk = chunk / e->round_reports * e->round_reports;
-  if (const char* env = getenv("JX_CHUNK_REPORTS")) {
-    uint64_t v = strtoull(env, nullptr, 10);
-    if (v >= 64) chunk = v / 64 * 64;
-  }
-  e->default_chunk = chunk;
+  e->default_chunk = e->auto_chunk = chunk;
   *out = e;
   return JX_OK;
 }
@@ -1185,6 +1049,7 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
 void jx_engine_destroy(jx_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
+  if (e->coal) coalescer_release(e);
   for (jx_engine* p : e->pipes) jx_engine_destroy(p);
   e->pipes.clear();
   if (e->stream) (void)hipStreamSynchronize(e->stream);
@@ -1192,18 +1057,18 @@ void jx_engine_destroy(jx_engine* e) {
     (void)hipEventDestroy(p.second.first);
     (void)hipEventDestroy(p.second.second);
   }
-  free_staging(e);
   for (auto& kv : e->segs) {
     (void)hipFree(kv.second.agg);
     (void)hipFree(kv.second.checksum);
     (void)hipFree(kv.second.count);
   }
-  for (auto& kv : e->batches)
-    if (kv.second.mem) (void)hipFree(kv.second.mem);
-  for (auto& kv : e->batch_pool) (void)hipFree(kv.second);
+  if (e->arena)
+    for (auto& kv : e->batches) arena_put(e->arena, kv.second.slab, e->stream);
+  e->batches.clear();
   if (e->d_consts && !e->is_pipe) (void)hipFree(e->d_consts);
   if (e->ev_pipe) (void)hipEventDestroy(e->ev_pipe);
   if (e->d_tmp) (void)hipFree(e->d_tmp);
+  if (e->d_hout) (void)hipFree(e->d_hout);
   for (void* q : {(void*)e->d_segx, (void*)e->d_perm, (void*)e->d_items, (void*)e->d_spart, (void*)e->d_ptrs,
                   (void*)e->d_err, (void*)e->d_delta})
     if (q) (void)hipFree(q);
@@ -1211,9 +1076,12 @@ void jx_engine_destroy(jx_engine* e) {
     if (e->h_ptrs[k]) (void)hipHostFree(e->h_ptrs[k]);
     if (e->ev_ptrs[k]) (void)hipEventDestroy(e->ev_ptrs[k]);
   }
+  if (e->h_acc) (void)hipHostFree(e->h_acc);
+  if (e->ev_hacc) (void)hipEventDestroy(e->ev_hacc);
   if (e->ev_wait) (void)hipEventDestroy(e->ev_wait);
   if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   if (e->stream) (void)hipStreamDestroy(e->stream);
+  if (e->arena && !e->is_pipe) arena_engine_remove(e->arena);
   delete e;
 }
 
@@ -1230,11 +1098,14 @@ int32_t jx_engine_sizes(const jx_engine* e, uint32_t* ps, uint32_t* his, uint32_
   return JX_OK;
 }
 
+// Reserve: warm the device arena with staging for `reports` reports (checked out once, then idle in the
+// arena for the next call of any engine on the device).
 int32_t jx_engine_set_capacity(jx_engine* e, uint64_t reports) {
   if (!e) return JX_E_INVALID;
   LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
-  return ensure_capacity(e, reports);
+  Stage st;
+  return stage_acquire(e, reports, SG_IN | SG_HIN | SG_MEAS | SG_PREP | SG_RES | SG_ACC, st);
 }
 
 // Release batch `id` when a prepare call fails after creating it.
@@ -1257,9 +1128,10 @@ static int32_t copy_out_shares(jx_engine* e, const uint4* outs, uint64_t n, uint
 
 static int32_t helper_prep_batch_locked(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps,
                                         const uint8_t* his, const uint8_t* lps, uint8_t* out_msgs, uint8_t* out_verdicts,
-                                        uint8_t* out_shares, uint64_t id, Batch* B) {
+                                        uint8_t* out_shares, Batch* B) {
   const Cfg& c = e->cfg;
-  int32_t rc = ensure_capacity(e, n);
+  Stage st;
+  int32_t rc = stage_acquire(e, n, SG_IN | SG_HIN | helper_meas_flag(c) | SG_PREP, st);
   if (rc) return rc;
   HIPCHK(e, hipMemcpyAsync(B->nonces, nonces, n * 16, hipMemcpyHostToDevice, e->stream));
   if (c.ps_bytes) HIPCHK(e, hipMemcpyAsync(e->d_ps, ps, n * c.ps_bytes, hipMemcpyHostToDevice, e->stream));
@@ -1275,9 +1147,11 @@ static int32_t helper_prep_batch_locked(jx_engine* e, uint64_t n, const uint8_t*
     if (rc) return rc;
   }
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  (void)id;
   return drain_timing(e);
 }
+
+// Coalesced prepares take jobs up to this size; larger ones fill the device by themselves.
+static bool coalescible(const jx_engine* e, uint64_t n) { return e->coalesce && n > 0 && n <= e->default_chunk / 4; }
 
 int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
                              const uint8_t* helper_input_shares, const uint8_t* leader_prep_shares,
@@ -1285,9 +1159,13 @@ int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, co
                              uint64_t* out_batch_id) {
   if (out_batch_id) *out_batch_id = 0;
   if (!e || (n && (!nonces || !helper_input_shares || !leader_prep_shares || !out_verdicts))) return JX_E_INVALID;
+  if (n && e->cfg.ps_bytes && !public_shares) return JX_E_INVALID;
+  if (!out_output_shares && coalescible(e, n)) {
+    t_err.clear();
+    return coalesced_helper_prep(e, n, nonces, public_shares, helper_input_shares, leader_prep_shares, out_prep_msgs,
+                                 out_verdicts, out_batch_id);
+  }
   LOCK(e);
-  const Cfg& c = e->cfg;
-  if (n && c.ps_bytes && !public_shares) return JX_E_INVALID;
   HIPCHK(e, hipSetDevice(e->device));
   uint64_t id = 0;
   Batch* B = nullptr;
@@ -1295,7 +1173,7 @@ int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, co
   if (rc) return rc;
   if (n) {
     rc = helper_prep_batch_locked(e, n, nonces, public_shares, helper_input_shares, leader_prep_shares, out_prep_msgs,
-                                  out_verdicts, out_output_shares, id, B);
+                                  out_verdicts, out_output_shares, B);
     if (rc) return drop_on_error(e, id, rc);
   }
   if (out_batch_id) *out_batch_id = id;
@@ -1305,7 +1183,8 @@ int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, co
 int32_t jx_engine_batch_id(const jx_engine* e, uint64_t* batch_id) {
   if (!e || !batch_id) return JX_E_INVALID;
   LOCK(const_cast<jx_engine*>(e));
-  *batch_id = e->batches.count(e->last_batch) ? e->last_batch : 0;
+  auto it = e->batches.find(e->last_batch);
+  *batch_id = it != e->batches.end() && !it->second.pending ? e->last_batch : 0;
   return JX_OK;
 }
 
@@ -1313,9 +1192,47 @@ int32_t jx_engine_batches(const jx_engine* e, uint64_t* resident, uint64_t* devi
   if (!e) return JX_E_INVALID;
   LOCK(const_cast<jx_engine*>(e));
   uint64_t bytes = 0;
-  for (auto& kv : e->batches) bytes += kv.second.bytes;
+  for (auto& kv : e->batches) bytes += kv.second.slab.bytes;
   if (resident) *resident = e->batches.size();
   if (device_bytes) *device_bytes = bytes;
+  return JX_OK;
+}
+
+int32_t jx_engine_memory(const jx_engine* e, jx_memory_stats* out) {
+  if (!e || !out) return JX_E_INVALID;
+  memset(out, 0, sizeof *out);
+  {
+    LOCK(const_cast<jx_engine*>(e));
+    for (auto& kv : e->batches) out->batch_bytes += kv.second.slab.bytes;
+    out->resident_batches = e->batches.size();
+    out->last_pipelines = e->last_pipes;
+  }
+  Arena* A = e->arena;
+  {
+    std::lock_guard<std::mutex> lk(A->mu);
+    out->arena_budget = A->budget;
+    out->arena_allocated = A->allocated;
+    out->arena_in_use = A->in_use;
+    out->arena_peak = A->peak;
+    out->arena_allocs = A->allocs;
+    out->arena_reuses = A->reuses;
+    out->arena_waits = A->waits;
+    out->arena_engines = A->engines;
+  }
+  uint64_t cs[12] = {0};
+  coalescer_stats(e, cs);
+  out->coalesced_launches = cs[0];
+  out->coalesced_jobs = cs[1];
+  out->coalesced_reports = cs[2];
+  out->coalesce_window_us = cs[3];
+  out->coalesce_gather_us = cs[5];
+  out->coalesce_copy_us = cs[6];
+  out->coalesce_enqueue_us = cs[7];
+  out->coalesce_device_us = cs[8];
+  {
+    std::lock_guard<std::mutex> lk(A->mu);
+    out->arena_cross_stream_waits = A->cross_waits;
+  }
   return JX_OK;
 }
 
@@ -1323,7 +1240,7 @@ int32_t jx_batch_release(jx_engine* e, uint64_t batch_id) {
   if (!e) return JX_E_INVALID;
   LOCK(e);
   auto it = e->batches.find(batch_id);
-  if (batch_id == 0 || it == e->batches.end())
+  if (batch_id == 0 || it == e->batches.end() || it->second.pending)
     return fail(e, JX_E_STATE, "release: batch id names no resident prepared batch");
   HIPCHK(e, hipSetDevice(e->device));
   batch_free(e, it);
@@ -1341,9 +1258,14 @@ int32_t jx_leader_prep_init_batch(jx_engine* e, uint64_t n, const uint8_t* nonce
                                   uint8_t* out_verdicts, uint64_t* out_batch_id) {
   if (out_batch_id) *out_batch_id = 0;
   if (!e || (n && (!nonces || !leader_input_shares || !out_prep_shares || !out_verdicts))) return JX_E_INVALID;
-  LOCK(e);
   const Cfg& c = e->cfg;
   if (n && c.ps_bytes && !public_shares) return JX_E_INVALID;
+  if (coalescible(e, n)) {
+    t_err.clear();
+    return coalesced_leader_init(e, n, nonces, public_shares, leader_input_shares, out_prep_shares, out_verdicts,
+                                 out_batch_id);
+  }
+  LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
   uint64_t id = 0;
   Batch* B = nullptr;
@@ -1351,13 +1273,19 @@ int32_t jx_leader_prep_init_batch(jx_engine* e, uint64_t n, const uint8_t* nonce
   if (rc) return rc;
   if (n) {
     auto run = [&]() -> int32_t {
-      int32_t r = ensure_leader_capacity(e, n);
+      Stage st;
+      int32_t r = stage_acquire(e, n, SG_IN | SG_LEAD | SG_PREP | (use_inplace(e) ? 0u : SG_MEAS), st);
       if (r) return r;
       HIPCHK(e, hipMemcpyAsync(B->nonces, nonces, n * 16, hipMemcpyHostToDevice, e->stream));
       if (c.ps_bytes)
         HIPCHK(e, hipMemcpyAsync(e->d_ps, public_shares, n * c.ps_bytes, hipMemcpyHostToDevice, e->stream));
-      HIPCHK(e, hipMemcpyAsync(e->d_lis, leader_input_shares, n * c.lis_bytes, hipMemcpyHostToDevice, e->stream));
-      r = prep_core(e, n, B->nonces, e->d_ps, nullptr, nullptr, B->verdicts, B->msgs, B->outs, e->d_lis, e->d_lps_out);
+      if (e->lis_stride == c.lis_bytes)
+        HIPCHK(e, hipMemcpyAsync(e->d_lis, leader_input_shares, n * c.lis_bytes, hipMemcpyHostToDevice, e->stream));
+      else  // padded rows (aligned in-place reads of the measurement share)
+        HIPCHK(e, hipMemcpy2DAsync(e->d_lis, e->lis_stride, leader_input_shares, c.lis_bytes, c.lis_bytes, n,
+                                   hipMemcpyHostToDevice, e->stream));
+      r = prep_core(e, n, B->nonces, e->d_ps, nullptr, nullptr, B->verdicts, B->msgs, B->outs, e->d_lis, e->d_lps_out,
+                    e->lis_stride);
       if (r) return r;
       HIPCHK(e, hipMemcpyAsync(out_verdicts, B->verdicts, n, hipMemcpyDeviceToHost, e->stream));
       HIPCHK(e, hipMemcpyAsync(out_prep_shares, e->d_lps_out, n * c.lps_bytes, hipMemcpyDeviceToHost, e->stream));
@@ -1371,15 +1299,18 @@ int32_t jx_leader_prep_init_batch(jx_engine* e, uint64_t n, const uint8_t* nonce
   return JX_OK;
 }
 
-int32_t jx_leader_prep_init_device(jx_engine* e, uint64_t n, const void* d_nonces, const void* d_public_shares,
-                                   const void* d_leader_input_shares, void* d_out_prep_shares, void* d_out_verdicts,
-                                   uint64_t* out_batch_id) {
+int32_t jx_leader_prep_init_device_ex(jx_engine* e, uint64_t n, const void* d_nonces, const void* d_public_shares,
+                                      const void* d_leader_input_shares, uint64_t lis_stride, void* d_out_prep_shares,
+                                      void* d_out_verdicts, uint64_t* out_batch_id) {
   if (!out_batch_id) return JX_E_INVALID;
   *out_batch_id = 0;
   if (!e || (n && (!d_nonces || !d_leader_input_shares || !d_out_prep_shares))) return JX_E_INVALID;
   LOCK(e);
   const Cfg& c = e->cfg;
   if (n && c.ps_bytes && !d_public_shares) return JX_E_INVALID;
+  if (lis_stride == 0) lis_stride = c.lis_bytes;
+  if (lis_stride < c.lis_bytes || (lis_stride & 15u))
+    return fail(e, JX_E_INVALID, "leader init: the row stride must be >= the leader input share and a multiple of 16");
   // the in-place FLP kernels read the measurement share in 16-byte vectors (header contract)
   if (n && use_inplace(e) && (reinterpret_cast<uintptr_t>(d_leader_input_shares) & 15u))
     return fail(e, JX_E_INVALID, "leader init: d_leader_input_shares must be 16-byte aligned");
@@ -1390,11 +1321,12 @@ int32_t jx_leader_prep_init_device(jx_engine* e, uint64_t n, const void* d_nonce
   if (rc) return rc;
   if (n) {
     auto run = [&]() -> int32_t {
-      int32_t r = ensure_capacity(e, n, !use_inplace(e));
+      Stage st;
+      int32_t r = stage_acquire(e, n, SG_PREP | (use_inplace(e) ? 0u : SG_MEAS), st);
       if (r) return r;
       HIPCHK(e, hipMemcpyAsync(B->nonces, d_nonces, n * 16, hipMemcpyDeviceToDevice, e->stream));
       r = prep_core(e, n, B->nonces, (const uint8_t*)d_public_shares, nullptr, nullptr, B->verdicts, B->msgs, B->outs,
-                    (const uint8_t*)d_leader_input_shares, (uint8_t*)d_out_prep_shares);
+                    (const uint8_t*)d_leader_input_shares, (uint8_t*)d_out_prep_shares, lis_stride);
       if (r) return r;
       if (d_out_verdicts) HIPCHK(e, hipMemcpyAsync(d_out_verdicts, B->verdicts, n, hipMemcpyDeviceToDevice, e->stream));
       return JX_OK;
@@ -1404,6 +1336,13 @@ int32_t jx_leader_prep_init_device(jx_engine* e, uint64_t n, const void* d_nonce
   }
   *out_batch_id = id;
   return JX_OK;
+}
+
+int32_t jx_leader_prep_init_device(jx_engine* e, uint64_t n, const void* d_nonces, const void* d_public_shares,
+                                   const void* d_leader_input_shares, void* d_out_prep_shares, void* d_out_verdicts,
+                                   uint64_t* out_batch_id) {
+  return jx_leader_prep_init_device_ex(e, n, d_nonces, d_public_shares, d_leader_input_shares, 0, d_out_prep_shares,
+                                       d_out_verdicts, out_batch_id);
 }
 
 static int32_t leader_batch(jx_engine* e, uint64_t batch_id, uint64_t n, Batch** B) {
@@ -1428,9 +1367,10 @@ int32_t jx_leader_prep_finish_batch(jx_engine* e, uint64_t batch_id, uint64_t n,
     return JX_OK;
   }
   HIPCHK(e, hipSetDevice(e->device));
-  rc = ensure_leader_capacity(e, n);
-  if (rc) return rc;
+  Stage st;
   if (c.jr_len) {
+    rc = stage_acquire(e, n, SG_LMSG, st);
+    if (rc) return rc;
     HIPCHK(e, hipMemcpyAsync(e->d_in_msgs, prep_msgs, n * c.seed, hipMemcpyHostToDevice, e->stream));
     Bufs b{};
     b.n = n;
@@ -1482,6 +1422,31 @@ static int32_t ready_batch(jx_engine* e, uint64_t batch_id, uint64_t n, const ch
   return JX_OK;
 }
 
+// Upload small host arrays through the engine's pinned buffer (no host wait for the call's own work: the
+// buffer is rewritten only after the upload that last read it has completed).
+static int32_t upload_small(jx_engine* e, const std::vector<std::pair<const void*, size_t>>& src,
+                            const std::vector<void*>& dst) {
+  size_t total = 0;
+  for (auto& s : src) total += align256(s.second);
+  if (!e->ev_hacc) HIPCHK(e, hipEventCreateWithFlags(&e->ev_hacc, hipEventDisableTiming));
+  else HIPCHK(e, hipEventSynchronize(e->ev_hacc));
+  if (e->h_acc_cap < total) {
+    if (e->h_acc) (void)hipHostFree(e->h_acc);
+    e->h_acc = nullptr;
+    e->h_acc_cap = 0;
+    HIPCHK(e, hipHostMalloc((void**)&e->h_acc, total, hipHostMallocDefault));
+    e->h_acc_cap = total;
+  }
+  size_t off = 0;
+  for (size_t i = 0; i < src.size(); i++) {
+    memcpy(e->h_acc + off, src[i].first, src[i].second);
+    HIPCHK(e, hipMemcpyAsync(dst[i], e->h_acc + off, src[i].second, hipMemcpyHostToDevice, e->stream));
+    off += align256(src[i].second);
+  }
+  HIPCHK(e, hipEventRecord(e->ev_hacc, e->stream));
+  return JX_OK;
+}
+
 int32_t jx_accumulate(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t* accept_mask,
                       const uint32_t* segment) {
   if (!e) return JX_E_INVALID;
@@ -1492,28 +1457,36 @@ int32_t jx_accumulate(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t
   HIPCHK(e, hipSetDevice(e->device));
   auto run = [&]() -> int32_t {
     if (n == 0) return JX_OK;
-    int32_t r = ensure_capacity(e, n, false);  // mask / index scratch and the accumulate partials
+    Stage st;
+    int32_t r = stage_acquire(e, n, SG_ACC, st);  // mask / index scratch and the accumulate partials
     if (r) return r;
+    std::vector<uint32_t> ids{0};
+    std::vector<std::pair<const void*, size_t>> src;
+    std::vector<void*> dst;
     const uint8_t* dm = nullptr;
+    const uint32_t* ds = nullptr;
     if (accept_mask) {
-      HIPCHK(e, hipMemcpyAsync(e->d_mask, accept_mask, n, hipMemcpyHostToDevice, e->stream));
+      src.push_back({accept_mask, n});
+      dst.push_back(e->d_mask);
       dm = e->d_mask;
     }
-    std::vector<uint32_t> ids{0};
-    const uint32_t* ds = nullptr;
     if (segment) {
       densify(segment, n, e->h_dense, ids);
       if (ids.size() > 1) {
-        HIPCHK(e, hipMemcpyAsync(e->d_seg, e->h_dense.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+        src.push_back({e->h_dense.data(), n * 4});
+        dst.push_back(e->d_seg);
         ds = e->d_seg;
       }
+    }
+    if (!src.empty()) {
+      r = upload_small(e, src, dst);
+      if (r) return r;
     }
     std::vector<Segment> targets;
     r = segment_targets(e, ids.data(), ids.size(), targets);
     if (r) return r;
     r = accumulate_into(e, batch_src(*B), dm, ds, targets);
     if (r) return r;
-    HIPCHK(e, hipStreamSynchronize(e->stream));  // the host mask / index copies are pageable
     return drain_timing(e);
   };
   rc = run();
@@ -1531,7 +1504,8 @@ int32_t jx_accumulate_device(jx_engine* e, uint64_t batch_id, uint64_t n, const 
   if (rc) return rc;
   HIPCHK(e, hipSetDevice(e->device));
   if (n) {
-    rc = ensure_capacity(e, n, false);  // mask / index scratch and the accumulate partials
+    Stage st;
+    rc = stage_acquire(e, n, SG_ACC, st);  // the accumulate partials
     if (rc) return rc;
     std::vector<Segment> targets;
     rc = segment_targets(e, segment_ids, nsegments, targets);
@@ -1565,10 +1539,9 @@ int32_t jx_batch_aggregate_records(jx_engine* e, uint64_t batch_id, uint64_t n, 
   if (rc) return rc;
   HIPCHK(e, hipSetDevice(e->device));
   const uint64_t rb = record_bytes(e->cfg);
-  if (n) {
-    rc = ensure_capacity(e, n, false);  // mask / index scratch and the accumulate partials
-    if (rc) return rc;
-  }
+  Stage st;
+  rc = stage_acquire(e, n ? n : 1, SG_ACC, st);  // mask / index scratch and the accumulate partials
+  if (rc) return rc;
   const uint8_t* dm = nullptr;
   const uint32_t* di = nullptr;
   if (n && accept_mask) {
@@ -1596,10 +1569,9 @@ int32_t jx_batch_aggregate_records_device(jx_engine* e, uint64_t batch_id, uint6
   int32_t rc = ready_batch(e, batch_id, n, "aggregate records", &B);
   if (rc) return rc;
   HIPCHK(e, hipSetDevice(e->device));
-  if (n) {
-    rc = ensure_capacity(e, n, false);  // mask / index scratch and the accumulate partials
-    if (rc) return rc;
-  }
+  Stage st;
+  rc = stage_acquire(e, n ? n : 1, SG_ACC, st);  // the accumulate partials
+  if (rc) return rc;
   return batch_records(e, B, (const uint8_t*)d_accept_mask, (const uint32_t*)d_segment_index, nsegments,
                        (uint8_t*)d_out_records);
 }
@@ -1617,8 +1589,15 @@ int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces
   int32_t rc = get_segment(e, segment, &seg);
   if (rc) return rc;
   const std::vector<Segment> targets{*seg};
-  const uint32_t P = pipes_for(e, n, chunk, false, true);
-  if (P > 1 && ensure_pipes(e, P, chunk)) {
+  const uint32_t want = pipes_for(e, n, chunk, false, true);
+  Stage pst[MAX_PIPES];
+  uint32_t P = 0;
+  if (want > 1) {
+    rc = pipes_acquire(e, want, chunk, SG_IN | SG_HIN | SG_MEAS | SG_PREP | SG_ACC, pst, &P);
+    if (rc) return rc;
+  }
+  e->last_pipes = P > 1 ? P : 1;
+  if (P > 1) {
     // the pipelines (see jx_helper_prep_aggregate_device): launch i's host-to-device copies (pageable: the
     // host thread stages them) go out while the other pipeline's kernels run; the verdicts and prep
     // messages collect in an engine buffer and come back once, after the join
@@ -1628,7 +1607,7 @@ int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces
       if (e->d_hout) (void)hipFree(e->d_hout);
       e->d_hout = nullptr;
       e->hout_bytes = 0;
-      if (dev_alloc(e, (void**)&e->d_hout, ob) != hipSuccess) return nomem(e, "host-path outputs", ob);
+      HIPCHK(e, hipMalloc((void**)&e->d_hout, ob));
       e->hout_bytes = ob;
     }
     uint8_t* dv = e->d_hout;
@@ -1670,7 +1649,9 @@ int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return JX_OK;
   }
-  rc = ensure_capacity(e, chunk);
+  if (P == 1) pst[0].release();  // one pipeline's staging only: run on the engine stream
+  Stage st;
+  rc = stage_acquire(e, chunk, SG_IN | SG_HIN | SG_MEAS | SG_PREP | SG_RES | SG_ACC, st);
   if (rc) return rc;
   for (uint64_t off = 0; off < n; off += chunk) {
     const uint64_t m = (n - off) < chunk ? (n - off) : chunk;
@@ -1712,8 +1693,15 @@ int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_
                 *L = (const uint8_t*)d_lps;
   const uint32_t* SG = (const uint32_t*)d_segment;
   const bool many = SG && targets.size() > 1;
-  const uint32_t P = pipes_for(e, n, chunk, many);
-  if (P > 1 && ensure_pipes(e, P, chunk)) {
+  const uint32_t want = pipes_for(e, n, chunk, many);
+  Stage pst[MAX_PIPES];
+  uint32_t P = 0;
+  if (want > 1) {
+    rc = pipes_acquire(e, want, chunk, SG_MEAS | SG_PREP | SG_RES | SG_ACC, pst, &P);
+    if (rc) return rc;
+  }
+  e->last_pipes = P > 1 ? P : 1;
+  if (P > 1) {
     // every pipeline orders after the caller's producers (jx_engine_wait_stream / _event act on the
     // engine stream) and the engine stream after every pipeline (the join), so the call keeps the
     // single-stream ordering contract
@@ -1746,7 +1734,9 @@ int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_
     }
     return rc;
   }
-  rc = ensure_capacity(e, chunk);
+  if (P == 1) pst[0].release();
+  Stage st;
+  rc = stage_acquire(e, chunk, SG_MEAS | SG_PREP | SG_RES | SG_ACC, st);
   if (rc) return rc;
   // the pointer table is uploaded once for every launch of the call (no per-launch host sync)
   if (many) {
@@ -1955,6 +1945,23 @@ int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]) {
   return JX_OK;
 }
 
+int32_t jx_engine_coalesce(jx_engine* e, int32_t enable, uint32_t window_us) {
+  if (!e || e->is_pipe) return JX_E_INVALID;
+  if (window_us > 1000000) return JX_E_INVALID;
+  {
+    LOCK(e);
+    HIPCHK(e, hipSetDevice(e->device));
+  }
+  if (enable) {
+    if (!e->coal) e->coal = coalescer_for(e);
+    if (!e->coal) return fail(e, JX_E_HIP, "coalesce: could not start the device coalescer");
+  }
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->coalesce = enable != 0;
+  if (e->coal) coalescer_set_window(e, window_us);
+  return JX_OK;
+}
+
 int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
   if (!e) return JX_E_INVALID;
   LOCK(e);
@@ -1974,11 +1981,15 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
     e->npipes = (uint32_t)value;
     return JX_OK;
   }
-  if (option == 2) {  // accumulate chunking (tests)
+  if (option == 2) {  // accumulate chunking (tests); staging is sized per call
     if (value < 1 || value > 4096) return JX_E_INVALID;
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    free_staging(e);
     e->acc_chunks = (uint32_t)value;
+    return JX_OK;
+  }
+  if (option == 5) {  // reports per launch of the fused paths: 0 automatic, else >= 64 (rounded down to 64)
+    if (value != 0 && value < 64) return JX_E_INVALID;
+    e->default_chunk = value ? (uint64_t)value / 64 * 64 : e->auto_chunk;
+    for (jx_engine* q : e->pipes) q->default_chunk = e->default_chunk;
     return JX_OK;
   }
   return JX_E_INVALID;

@@ -1,0 +1,251 @@
+// jx_engine_internal.h — engine internals shared by jx_engine.cpp (the C ABI and launch sequencing),
+// jx_arena.cpp (the per-device memory arena) and jx_coalesce.cpp (the per-device job coalescer).
+// Not part of the ABI: include/jx_prio3.h is.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/jx_prio3.h"
+#include "jx_kernels.h"
+
+namespace jxi {
+
+using jx::Cfg;
+
+// ---------------------------------------------------------------------------- device arena (jx_arena.cpp)
+// One per HIP device, shared by every engine (every task) on it: launch staging is checked out per call and
+// handed back stream-ordered, and resident batches are carved from the same pool. A slab handed back is
+// reused by another stream only after that stream waits on the slab's event (recorded where its last user
+// finished), so reuse never blocks the host.
+struct Slab {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipEvent_t ev = nullptr;  // recorded on the stream of the slab's last user when it was handed back
+  hipStream_t last = nullptr;  // that stream
+  bool staging = false;     // per-call staging (comes back soon) vs. a resident batch (comes back on release)
+};
+
+struct Arena {
+  int device = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  uint64_t budget = 0;           // bytes the arena may hold (free + checked out)
+  uint64_t allocated = 0;        // bytes held (free + checked out)
+  uint64_t in_use = 0;           // checked out
+  uint64_t in_use_staging = 0;   // checked out as per-call staging
+  uint64_t peak = 0;             // max in_use
+  uint64_t allocs = 0, reuses = 0, waits = 0, frees = 0, cross_waits = 0;
+  uint32_t engines = 0;          // live engines on this device (the last one out trims the free slabs)
+  std::multimap<size_t, Slab> free;
+};
+
+Arena* arena_for(int device);
+// Check out `bytes` for work on stream `s` (the stream waits on the slab's last user). may_wait: when the
+// budget is held by other callers' staging, wait for a hand-back (a caller that holds no slab may wait;
+// one that already holds one must not). hipErrorOutOfMemory when it cannot be satisfied.
+hipError_t arena_get(Arena* A, size_t bytes, hipStream_t s, bool staging, bool may_wait, Slab& out);
+// Hand a slab back after queueing its last use on stream `s`.
+void arena_put(Arena* A, Slab& slab, hipStream_t s);
+// Free every slab on the free list (waits for their last users).
+void arena_trim(Arena* A);
+void arena_engine_add(Arena* A);
+void arena_engine_remove(Arena* A);
+
+// ---------------------------------------------------------------------------- engine state
+
+// One batch aggregation's device state (aggregate share, report count, ReportIdChecksum).
+struct Segment {
+  uint4* agg = nullptr;                 // [out_len] canonical
+  uint32_t* checksum = nullptr;         // [8]
+  unsigned long long* count = nullptr;  // [1]
+};
+
+// A resident prepared batch: one aggregation job's reports after prepare_init, holding what
+// prepare_next and the accumulation need once the prepare call has returned. Staging (measurement
+// and proof shares, coefficients, FLP partials) is per-call scratch from the arena; the output
+// shares, verdicts, prep messages (leader: the corrected joint-rand seeds, its prepare state) and
+// report ids live here until jx_batch_release / jx_accumulate. Any number of batches can be
+// resident, so the aggregation jobs Janus steps concurrently (max_concurrent_job_workers,
+// aggregator/src/binary_utils/job_driver.rs:116-138; a leader job holds its prepare state across
+// the helper round trip, aggregation_job_driver.rs:396-416 -> :540-701) each keep their own.
+struct Batch {
+  uint64_t n = 0;
+  bool leader = false;
+  bool finished = false;      // leader: prepare_next has run (once)
+  bool pending = false;       // a coalesced launch is still writing it (not visible to other calls yet)
+  Slab slab;                  // one arena allocation: outs | verdicts | msgs | nonces
+  uint4* outs = nullptr;      // interleaved [n/64][out_len][64] (Histogram: the measurement share)
+  uint8_t* verdicts = nullptr;
+  uint8_t* msgs = nullptr;
+  uint8_t* nonces = nullptr;  // report ids, for the checksums
+};
+
+// What an accumulation reads: output shares, verdicts, report ids of n reports.
+struct AccSrc {
+  uint64_t n;
+  const uint4* outs;
+  const uint8_t* verdicts;
+  const uint8_t* nonces;
+};
+
+enum { ST_XOF = 0, ST_FLP = 1, ST_ACC = 2, ST_SLOW = 3, NST = 4 };
+
+// Per-call staging regions (stage_acquire flags)
+enum : uint32_t {
+  SG_IN = 1,     // host-path inputs: nonces, public shares
+  SG_HIN = 256,  // host-path helper inputs: helper input shares, leader prep shares
+  SG_MEAS = 2,   // measurement-share staging
+  SG_PREP = 4,   // proof shares, output shares, FLP coefficients, flags, FLP partials
+  SG_RES = 8,    // per-launch verdicts and prep messages of the fused paths
+  SG_ACC = 16,   // accumulation: mask, dense segment index, partials
+  SG_LEAD = 32,  // host-path leader: input shares (rows of lis_stride) and outbound prep shares
+  SG_LMSG = 64,  // host-path leader finish: inbound prep messages
+  SG_VK = 128,   // coalesced launches: one verify key per report (16 B; multiproof: HMAC pads, 64 B)
+  SG_JOBS = 512, // coalesced launches: the job table (MAX_JOBS_PER_LAUNCH slices)
+};
+
+struct Coalescer;  // jx_coalesce.cpp
+
+}  // namespace jxi
+
+struct jx_engine {
+  jxi::Cfg cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;  // held by every entry point for the duration of the call (coalesced prepares: not while waiting)
+  jxi::Arena* arena = nullptr;
+  // per-call staging, carved from an arena slab by stage_acquire and cleared by its release
+  uint64_t cap = 0;       // reports the current staging holds (0: none checked out)
+  uint32_t stage_flags = 0;
+  uint64_t default_chunk = 0;  // reports per launch of the fused paths (debug option 5 overrides auto_chunk)
+  uint64_t auto_chunk = 0;
+  uint64_t round_reports = 0;  // reports that fill every K1 wave slot once (0: unknown)
+  uint64_t lis_stride = 0;     // row stride of the staged leader input shares (host leader path)
+  uint8_t *d_nonces = nullptr, *d_ps = nullptr, *d_his = nullptr, *d_lps = nullptr;
+  uint4 *d_meas = nullptr, *d_proof = nullptr, *d_outs = nullptr, *d_coef = nullptr, *d_consts = nullptr;
+  uint32_t* d_flags = nullptr;
+  uint4* d_part = nullptr;
+  uint8_t *d_verdicts = nullptr, *d_msgs = nullptr;  // the fused paths' per-launch results
+  uint64_t* d_partials = nullptr;
+  uint8_t* d_mask = nullptr;
+  uint32_t* d_seg = nullptr;
+  uint8_t *d_lis = nullptr, *d_lps_out = nullptr, *d_in_msgs = nullptr;
+  uint8_t* d_vkeys = nullptr;
+  jx::JobSlice* d_jobs = nullptr;
+  uint32_t acc_chunks = 0;  // report chunks of the accumulate kernel (0: acc_nchunks picks)
+  // persistent per-engine scratch (small, or only for host output shares)
+  uint8_t* d_hout = nullptr;  // the host fused path with pipelines: verdicts || prep messages of the call
+  uint64_t hout_bytes = 0;
+  uint8_t* d_tmp = nullptr;  // output-share transpose / aggregate encode / records
+  size_t tmp_bytes = 0;
+  std::map<uint32_t, jxi::Segment> segs;  // running batch aggregations (the engine as one shard)
+  // resident prepared batches by handle; handles are never reused
+  std::map<uint64_t, jxi::Batch> batches;
+  uint64_t batch_gen = 0, last_batch = 0;
+  // per-call batch-aggregation deltas (jx_batch_aggregate_records): agg [ns][out_len] | count [ns] | checksum [ns][8]
+  uint8_t* d_delta = nullptr;
+  size_t delta_bytes = 0;
+  // segmented accumulation scratch (allocated on first use)
+  uint32_t* d_segx = nullptr;  // cnt, off, cursor [SEG_MAX each], ioff [SEG_MAX + 1], nitems [2]
+  uint32_t* d_perm = nullptr;
+  uint64_t perm_cap = 0;
+  uint4* d_items = nullptr;
+  uint64_t* d_spart = nullptr;
+  uint64_t spart_wmax = 0;
+  void** d_ptrs = nullptr;  // [3][nptrs]: aggs, counts, checksums of the call's segments
+  uint64_t ptrs_cap = 0;
+  // pinned host copies of the pointer table, double-buffered: buffer k is rewritten only after the
+  // upload that last read it has completed (ev_ptrs[k]), so no call waits for its own work
+  void** h_ptrs[2] = {nullptr, nullptr};
+  uint64_t h_ptrs_cap[2] = {0, 0};
+  hipEvent_t ev_ptrs[2] = {nullptr, nullptr};
+  int ptrs_k = 0;
+  // pinned host staging for the small host arrays of jx_accumulate (mask, dense segment index), so the
+  // call returns once queued: reused after ev_hacc (the last upload that read it) has completed
+  uint8_t* h_acc = nullptr;
+  uint64_t h_acc_cap = 0;
+  hipEvent_t ev_hacc = nullptr;
+  std::vector<uint32_t> h_dense;
+  uint32_t* d_err = nullptr;  // combine kernels: non-canonical input seen (reported by jx_engine_sync)
+  // timing
+  bool timing = false;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  double ms[jxi::NST] = {0, 0, 0, 0};
+  uint64_t launches[jxi::NST] = {0, 0, 0, 0};
+  uint32_t force_slow = 0;
+  uint32_t k1_split = 0;  // helper K1: 0 automatic, 3 lane-split, 5 fused, 6 lane pairs (debug option 3)
+  // producer / consumer ordering (jx_engine_wait_stream / jx_engine_join_stream): reused events
+  hipEvent_t ev_wait = nullptr, ev_join = nullptr;
+  // Concurrent pipelines of the fused paths (pipes_for): child engines with their own stream run
+  // K1 -> K3 -> K4 of alternate launches, so launches of different phases share the device; the K4s stay
+  // in launch order through ev_pipe. Their staging comes from the arena per call.
+  std::vector<jx_engine*> pipes;
+  uint32_t npipes = 0;  // 0: automatic (debug option 4)
+  uint32_t last_pipes = 0;  // pipelines the last fused call ran (fewer than asked when staging was short)
+  bool is_pipe = false;  // a child: d_consts belongs to the parent
+  hipEvent_t ev_pipe = nullptr;
+  // coalesced prepares (jx_engine_coalesce): the device's coalescer for this engine's Prio3 instance
+  jxi::Coalescer* coal = nullptr;
+  bool coalesce = false;
+};
+
+namespace jxi {
+
+// errors: per calling thread (jx_last_error)
+int32_t fail(jx_engine* e, int32_t code, const std::string& msg);
+std::string& thread_error();
+
+#define HIPCHK(e, call)                                                                                   \
+  do {                                                                                                    \
+    hipError_t _st = (call);                                                                              \
+    if (_st != hipSuccess)                                                                                \
+      return ::jxi::fail((e), _st == hipErrorOutOfMemory ? JX_E_NOMEM : JX_E_HIP,                         \
+                         std::string(#call) + ": " + hipGetErrorString(_st));                             \
+  } while (0)
+
+// Per-call staging: an arena slab carved into the engine's d_* regions named by the flags; released
+// (handed back stream-ordered on the engine's stream) when the Stage goes out of scope.
+struct Stage {
+  jx_engine* e = nullptr;
+  Slab slab;
+  Stage() = default;
+  Stage(const Stage&) = delete;
+  Stage& operator=(const Stage&) = delete;
+  ~Stage() { release(); }
+  void release();
+};
+int32_t stage_acquire(jx_engine* e, uint64_t n, uint32_t flags, Stage& st, bool may_wait = true);
+size_t stage_bytes(const jx_engine* e, uint64_t cap, uint32_t flags);
+
+int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* his,
+                  const uint8_t* lps, uint8_t* verdicts, uint8_t* msgs, uint4* outs, const uint8_t* lis = nullptr,
+                  uint8_t* lps_out = nullptr, uint64_t lis_rs = 0, const uint8_t* vkeys = nullptr);
+uint4* staging_outs(jx_engine* e);
+int32_t batch_new(jx_engine* e, uint64_t n, bool leader, uint64_t* id, Batch** out);
+void batch_free(jx_engine* e, std::map<uint64_t, Batch>::iterator it);
+int32_t drain_timing(jx_engine* e);
+size_t align256(size_t v);
+uint32_t vk_row_bytes(const Cfg& c);
+void vk_row(const Cfg& c, uint8_t* dst);  // this engine's verify key as one SG_VK row
+jx_engine* new_child(jx_engine* parent);  // a pipeline / coalescer lane: own stream, shared consts
+
+// ---------------------------------------------------------------------------- coalescer (jx_coalesce.cpp)
+Coalescer* coalescer_for(jx_engine* e);
+// A coalesced helper prepare / leader prepare_init of a job of n reports: joins the device's next launch
+// with other engines' (tasks') jobs of the same Prio3 instance. Blocks the calling thread until its results
+// are in the caller's buffers; the engine mutex is not held while waiting.
+int32_t coalesced_helper_prep(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* his,
+                              const uint8_t* lps, uint8_t* out_msgs, uint8_t* out_verdicts, uint64_t* out_batch_id);
+int32_t coalesced_leader_init(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* lis,
+                              uint8_t* out_prep_shares, uint8_t* out_verdicts, uint64_t* out_batch_id);
+void coalescer_stats(const jx_engine* e, uint64_t out[12]);
+void coalescer_set_window(jx_engine* e, uint32_t window_us);  // 0: automatic
+void coalescer_release(jx_engine* e);
+
+}  // namespace jxi

@@ -99,7 +99,12 @@ struct Bufs {
   const uint8_t* ps;
   const uint8_t* his;
   const uint8_t* lps;
-  const uint8_t* lis;   // leader role: explicit leader input shares (n x lis_bytes)
+  const uint8_t* lis;   // leader role: explicit leader input shares (n rows of lis_rs bytes)
+  uint64_t lis_rs;      // leader role: row stride of lis (>= lis_bytes, a multiple of 16)
+  // per-report verify keys (nullable: every report uses Cfg::vk / vk_ist, vk_ost): a coalesced launch
+  // prepares the jobs of several tasks (engines) of one Prio3 instance. Row r: the 16-byte key
+  // (TurboSHAKE instances) or the HMAC-SHA256 pads ist[8] || ost[8] of the 32-byte key (multiproof).
+  const uint8_t* vkeys;
   uint8_t* lps_out;     // leader role: outbound prep shares (n x lps_bytes)
   uint32_t leader;      // 1: run prepare_init for agg_id 0 (leader_initialized)
   uint4* meas;
@@ -188,6 +193,18 @@ hipError_t launch_record_combine(const Cfg& c, const uint8_t* parts, uint32_t np
                                  hipStream_t s);
 hipError_t launch_transpose_out(const Cfg& c, const uint4* outs, uint64_t n, uint8_t* dst, hipStream_t s);
 hipError_t launch_agg_encode(const Cfg& c, const uint4* agg, uint8_t* dst, hipStream_t s);
+// one job of a coalesced launch: reports [first, first + n) go to the job's batch buffers
+struct JobSlice {
+  uint64_t first, n;
+  uint4* outs;
+  uint8_t* verdicts;
+  uint8_t* msgs;
+  uint8_t* nonces;
+};
+constexpr uint32_t MAX_JOBS_PER_LAUNCH = 4096;
+hipError_t launch_scatter_jobs(const Cfg& c, const JobSlice* d_jobs, uint32_t njobs, uint64_t max_job_reports,
+                               const uint4* outs, const uint8_t* verdicts, const uint8_t* msgs, const uint8_t* nonces,
+                               hipStream_t s);
 // multiproof Field64 SumVec (jx_mp64.hip)
 uint64_t k1_round_reports(const Cfg& c, int device, uint32_t k1_split = 0);
 uint64_t mp_k1_round_reports(int device);

@@ -78,6 +78,16 @@ __device__ __forceinline__ void load16(const uint8_t* p, uint32_t w[4]) {
   w[3] = v.w;
 }
 
+// the verify key of report r: its row of the per-report keys of a coalesced launch, or the engine's
+__device__ __forceinline__ void load_vk(const Cfg& c, const Bufs& b, uint64_t r, uint32_t vk[4]) {
+  if (b.vkeys) {
+    load16(b.vkeys + 16 * r, vk);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; i++) vk[i] = c.vk[i];
+  }
+}
+
 // Montgomery exponentiation, uniform exponent
 __device__ f128 mpow(f128 aR, uint32_t e) {
   f128 r = make128(R1_128_LO, R1_128_HI);
@@ -162,7 +172,7 @@ __global__ __launch_bounds__(256) void count_kernel(Cfg c, Bufs b) {
   uint64_t x[1], proof[5], t[1];
   bool bad = false;
   if (LEADER) {
-    const uint2* ls = reinterpret_cast<const uint2*>(b.lis + (uint64_t)c.lis_bytes * r);
+    const uint2* ls = reinterpret_cast<const uint2*>(b.lis + b.lis_rs * r);
     uint2 q = ls[0];
     x[0] = (uint64_t)q.x | ((uint64_t)q.y << 32);
     bad |= x[0] >= P64;
@@ -198,7 +208,9 @@ __global__ __launch_bounds__(256) void count_kernel(Cfg c, Bufs b) {
   {  // query_rands: XOF(verify_key, DST(usage 5), [PROOFS=1] || nonce)
     Block m;
     blk_zero(m);
-    int pos = blk_xof_prefix(m, ALGO_COUNT, 5, c.vk);
+    uint32_t vk[4];
+    load_vk(c, b, r, vk);
+    int pos = blk_xof_prefix(m, ALGO_COUNT, 5, vk);
     blk_put_byte(m, pos, 1);
 #pragma unroll
     for (int i = 0; i < 4; i++) blk_put_word(m, pos + 1 + 4 * i, nonce[i]);
@@ -500,7 +512,9 @@ __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t
   {
     Block m;
     blk_zero(m);
-    int pos = blk_xof_prefix(m, c.dst_id, 5, c.vk);
+    uint32_t vk[4];
+    load_vk(c, b, r, vk);
+    int pos = blk_xof_prefix(m, c.dst_id, 5, vk);
     blk_put_byte(m, pos, 1);
 #pragma unroll
     for (int i = 0; i < 4; i++) blk_put_word(m, pos + 1 + 4 * i, nonce[i]);
@@ -1419,7 +1433,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_leader_kernel(Cfg c, Bufs b
   if (blk >= nblk) return;
   const uint64_t r0 = blk * 64 + lane;
   const uint64_t r = r0 < b.n ? r0 : b.n - 1;
-  const uint8_t* ls = b.lis + (uint64_t)c.lis_bytes * r;
+  const uint8_t* ls = b.lis + b.lis_rs * r;
   const uint32_t MB = c.meas_len * 16;
   const uint32_t ML = 42 + MB;
   const uint32_t NM = (MB + 167) / 168;
@@ -2875,6 +2889,39 @@ __global__ void transpose_out_kernel(Cfg c, const uint4* outs, uint64_t n, uint8
   }
 }
 
+// Coalesced launches (jx_coalesce.cpp): copy job j's slice [first, first + n) of the launch's staging into
+// the job's own resident batch, so every job keeps an independent batch (interleaved output shares
+// re-based to lane 0, verdicts, prep messages / leader seeds, report ids). blockIdx.y = job; the threads of
+// a job stride over its destination elements (coalesced writes, reads shifted by first % 64).
+__global__ __launch_bounds__(256) void scatter_jobs_kernel(Cfg c, const JobSlice* jobs, const uint4* outs,
+                                                           const uint8_t* verdicts, const uint8_t* msgs,
+                                                           const uint8_t* nonces) {
+  const JobSlice j = jobs[blockIdx.y];
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nblk = (j.n + 63) / 64;
+  const uint64_t total = nblk * c.out_len * 64;
+  for (uint64_t t = t0; t < total; t += stride) {
+    const uint64_t blk = t / ((uint64_t)c.out_len * 64);
+    const uint32_t rem = (uint32_t)(t % ((uint64_t)c.out_len * 64));
+    const uint32_t e = rem / 64, l = rem % 64;
+    const uint64_t i = blk * 64 + l;
+    if (i >= j.n) continue;
+    const uint64_t r = j.first + i;
+    j.outs[t] = outs[il_idx(r / 64, c.out_len, e, r % 64)];
+  }
+  const uint32_t mb = c.seed;  // prep message / seed bytes: 16 or 32
+  for (uint64_t i = t0; i < j.n; i += stride) {
+    const uint64_t r = j.first + i;
+    j.verdicts[i] = verdicts[r];
+    const uint4* sm = reinterpret_cast<const uint4*>(msgs + r * mb);
+    uint4* dm = reinterpret_cast<uint4*>(j.msgs + i * mb);
+    dm[0] = sm[0];
+    if (mb == 32) dm[1] = sm[1];
+    reinterpret_cast<uint4*>(j.nonces)[i] = reinterpret_cast<const uint4*>(nonces)[r];
+  }
+}
+
 __global__ void agg_encode_kernel(Cfg c, const uint4* agg, uint8_t* dst) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= c.out_len) return;
@@ -3105,6 +3152,17 @@ hipError_t launch_record_combine(const Cfg& c, const uint8_t* parts, uint32_t np
 hipError_t launch_transpose_out(const Cfg& c, const uint4* outs, uint64_t n, uint8_t* dst, hipStream_t s) {
   uint64_t t = n * c.out_len;
   hipLaunchKernelGGL(transpose_out_kernel, dim3((uint32_t)((t + 255) / 256)), dim3(256), 0, s, c, outs, n, dst);
+  return hipGetLastError();
+}
+hipError_t launch_scatter_jobs(const Cfg& c, const JobSlice* d_jobs, uint32_t njobs, uint64_t max_job_reports,
+                               const uint4* outs, const uint8_t* verdicts, const uint8_t* msgs, const uint8_t* nonces,
+                               hipStream_t s) {
+  if (njobs == 0) return hipSuccess;
+  const uint64_t elems = (max_job_reports + 63) / 64 * 64 * c.out_len;
+  uint64_t gx = (elems + 255) / 256;
+  if (gx > 1024) gx = 1024;
+  hipLaunchKernelGGL(scatter_jobs_kernel, dim3((uint32_t)gx, njobs), dim3(256), 0, s, c, d_jobs, outs, verdicts, msgs,
+                     nonces);
   return hipGetLastError();
 }
 hipError_t launch_agg_encode(const Cfg& c, const uint4* agg, uint8_t* dst, hipStream_t s) {

@@ -482,7 +482,20 @@ __device__ uint32_t mp_tail(const Cfg& c, const Bufs& b, const TTab& T, uint64_t
     m_byte(m, pos, c.np);
 #pragma unroll
     for (int i = 0; i < 16; i++) m_byte(m, pos + 1 + i, nonce[i >> 2] >> (8 * (i & 3)));
-    hmac_tag(tag, c.vk_ist, c.vk_ost, m, pos + 17);
+    // the verify key's pads: this report's row of a coalesced launch's keys, or the engine's
+    uint32_t vist[8], vost[8];
+    if (b.vkeys) {
+      const uint4* kp = reinterpret_cast<const uint4*>(b.vkeys + 64 * r);
+      const uint4 k0 = kp[0], k1 = kp[1], k2 = kp[2], k3 = kp[3];
+      vist[0] = k0.x, vist[1] = k0.y, vist[2] = k0.z, vist[3] = k0.w;
+      vist[4] = k1.x, vist[5] = k1.y, vist[6] = k1.z, vist[7] = k1.w;
+      vost[0] = k2.x, vost[1] = k2.y, vost[2] = k2.z, vost[3] = k2.w;
+      vost[4] = k3.x, vost[5] = k3.y, vost[6] = k3.z, vost[7] = k3.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; i++) vist[i] = c.vk_ist[i], vost[i] = c.vk_ost[i];
+    }
+    hmac_tag(tag, vist, vost, m, pos + 17);
     ctr_sample<MP_MAX_PROOFS>(T, tag, c.np, qr);
   }
   // ---- per-proof barycentric coefficients (canonical Field64):
@@ -552,7 +565,7 @@ __global__ __launch_bounds__(64 * MP_XOF_WAVES) void mp_xof_kernel(Cfg c, Bufs b
   const TTab T = ttab(tt, lane);
   const uint32_t M = c.meas_len, MB = 8 * M, NPL = c.np * c.proof_len;
   const uint8_t* hs = LEADER ? nullptr : b.his + (uint64_t)c.his_bytes * r;
-  const uint8_t* ls = LEADER ? b.lis + (uint64_t)c.lis_bytes * r : nullptr;
+  const uint8_t* ls = LEADER ? b.lis + b.lis_rs * r : nullptr;
   uint2* const mp = reinterpret_cast<uint2*>(b.meas) + (blk * M) * IL + lane;
   uint4* const op = b.outs + (blk * c.out_len) * IL + lane;
   uint32_t nonce[4];

@@ -164,8 +164,10 @@ class HelperEngine:
         if stream is False:
             return None
         if stream is None:
-            import torch
-
+            try:
+                import torch
+            except ImportError:  # raw device pointers without torch: the caller orders by hand
+                return None
             stream = torch.cuda.current_stream(self.device)
         return int(getattr(stream, "cuda_stream", stream))
 
@@ -194,15 +196,18 @@ class HelperEngine:
 
     @contextlib.contextmanager
     def _ordered(self, stream):
-        if stream is False:
+        h = self._stream_handle(stream)
+        if h is None:  # stream=False (ordered by hand), or no torch to order against
             yield
             return
-        h = self._stream_handle(stream)
         check(self._L.jx_engine_wait_stream(self._h, h or None), self._h, "jx_engine_wait_stream")
         try:
             yield
-        finally:
-            check(self._L.jx_engine_join_stream(self._h, h or None), self._h, "jx_engine_join_stream")
+        except BaseException:
+            # the join still orders whatever the failed call queued; its own error must not hide the call's
+            self._L.jx_engine_join_stream(self._h, h or None)
+            raise
+        check(self._L.jx_engine_join_stream(self._h, h or None), self._h, "jx_engine_join_stream")
 
     # ------------------------------------------------------------------ prepare
     def helper_initialized_batch(self, nonces, public_shares, helper_input_shares, leader_prep_shares,
@@ -340,14 +345,17 @@ class HelperEngine:
 
     # ------------------------------------------------------------------ device-pointer paths (inputs in HBM)
     def leader_init_device(self, n: int, d_nonces: int, d_public_shares: int | None, d_leader_input_shares: int,
-                           d_out_prep_shares: int, d_out_verdicts: int | None = None, stream=None) -> int:
+                           d_out_prep_shares: int, d_out_verdicts: int | None = None, stream=None,
+                           lis_stride: int = 0) -> int:
         """leader_initialized for n reports resident in HBM; returns the batch id. Asynchronous,
-        ordered against `stream` (module docstring)."""
+        ordered against `stream` (module docstring). lis_stride: the row stride of the leader input
+        shares (0: packed rows of leader_input_share_len; a multiple of 128 lets the in-place FLP
+        kernels read whole cache lines)."""
         bid = ctypes.c_uint64()
         with self._ordered(stream):
-            st = self._L.jx_leader_prep_init_device(self._h, n, d_nonces, d_public_shares, d_leader_input_shares,
-                                                    d_out_prep_shares, d_out_verdicts, ctypes.byref(bid))
-            check(st, self._h, "jx_leader_prep_init_device")
+            st = self._L.jx_leader_prep_init_device_ex(self._h, n, d_nonces, d_public_shares, d_leader_input_shares,
+                                                       lis_stride, d_out_prep_shares, d_out_verdicts, ctypes.byref(bid))
+            check(st, self._h, "jx_leader_prep_init_device_ex")
         return bid.value
 
     def leader_finish_device(self, batch_id: int, n: int, d_prep_msgs: int | None, d_peer_verdicts: int | None = None,
@@ -450,6 +458,19 @@ class HelperEngine:
         s = ctypes.c_void_p()
         check(self._L.jx_engine_stream(self._h, ctypes.byref(s)), self._h, "jx_engine_stream")
         return s.value or 0
+
+    # ------------------------------------------------------------------ coalescing and memory
+    def coalesce(self, enable: bool = True, window_us: int = 0):
+        """Coalesced prepares: helper_initialized_batch / leader_initialized_batch of small jobs join the
+        device's next shared launch with the concurrent jobs of every coalescing engine of this Prio3
+        instance on the device (each report keeps its own engine's verify key). window_us = 0: automatic."""
+        check(self._L.jx_engine_coalesce(self._h, int(bool(enable)), int(window_us)), self._h, "jx_engine_coalesce")
+
+    def memory(self) -> dict:
+        """This engine's resident batches and the device arena / coalescer counters (jx_engine_memory)."""
+        m = _lib.JxMemoryStats()
+        check(self._L.jx_engine_memory(self._h, ctypes.byref(m)), self._h, "jx_engine_memory")
+        return {name: int(getattr(m, name)) for name, _ in m._fields_}
 
     # ------------------------------------------------------------------ instrumentation
     def timing(self, enable: bool):

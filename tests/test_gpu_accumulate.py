@@ -124,11 +124,8 @@ def test_fused_device_segments_match_oracle():
     T = lambda a: torch.from_numpy(np.array(a, copy=True)).to(dev)  # noqa: E731  (writable copy)
     d_seg = T(dense.astype(np.int32))
     import os
-    os.environ["JX_CHUNK_REPORTS"] = "512"  # several launches: the segment array is offset per launch
-    try:
-        eng = HelperEngine(vdaf, vk)
-    finally:
-        del os.environ["JX_CHUNK_REPORTS"]
+    eng = HelperEngine(vdaf, vk)
+    eng.debug(5, 512)  # 512 reports per launch
     with eng:
         d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
         keep = [T(nonces), T(ps), T(his), T(lps)]  # hold the tensors: a freed block is reused at once
@@ -156,11 +153,8 @@ def test_fused_device_multi_launch(name, vdaf):
     want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
     dev = torch.device("cuda", 0)
     T = lambda a: torch.from_numpy(np.array(a, copy=True)).to(dev)  # noqa: E731  (writable copy)
-    os.environ["JX_CHUNK_REPORTS"] = "512"
-    try:
-        eng = HelperEngine(vdaf, vk)
-    finally:
-        del os.environ["JX_CHUNK_REPORTS"]
+    eng = HelperEngine(vdaf, vk)
+    eng.debug(5, 512)  # 512 reports per launch
     with eng:
         d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
         d_m = torch.zeros((n, 16), dtype=torch.uint8, device=dev)

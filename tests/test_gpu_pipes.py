@@ -36,16 +36,14 @@ def test_pipes_match_oracle(name, vdaf):
     import torch
 
     vk = bytes(range(7, 23))
-    n = 4 * 1024 + 333  # 5 launches of 1,024 (the last one ragged) at JX_CHUNK_REPORTS=1024
+    n = 4 * 1024 + 333  # 5 launches of 1,024 (the last one ragged) at 1,024 reports per launch
     orc, nonces, ps, his, lps = _batch(vdaf, vk, n, seed=sum(map(ord, name)))
     want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16)
     dev = torch.device("cuda", 0)
     pinned = [torch.from_numpy(np.array(a, copy=True)).pin_memory() for a in (nonces, ps, his, lps)]
-    os.environ["JX_CHUNK_REPORTS"] = "1024"
-    try:
-        engs = [HelperEngine(vdaf, vk) for _ in range(4)]
-    finally:
-        del os.environ["JX_CHUNK_REPORTS"]
+    engs = [HelperEngine(vdaf, vk) for _ in range(4)]
+    for _e in engs:
+        _e.debug(5, 1024)  # 1024 reports per launch
     try:
         for P, eng in zip((1, 2, 3, 4), engs):
             eng.debug(4, P)
@@ -91,11 +89,8 @@ def test_host_path_pipes_match_oracle(P):
     n = 3 * 1024 + 77
     orc, nonces, ps, his, lps = _batch(vdaf, vk, n, seed=P)
     want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16)
-    os.environ["JX_CHUNK_REPORTS"] = "1024"
-    try:
-        eng = HelperEngine(vdaf, vk)
-    finally:
-        del os.environ["JX_CHUNK_REPORTS"]
+    eng = HelperEngine(vdaf, vk)
+    eng.debug(5, 1024)  # 1024 reports per launch
     with eng:
         eng.debug(4, P)
         v, m = eng.prep_and_aggregate(nonces, ps, his, lps)
@@ -103,3 +98,20 @@ def test_host_path_pipes_match_oracle(P):
         fin = want["verdicts"] == 0
         np.testing.assert_array_equal(m[fin], want["prep_msgs"][fin])
         assert eng.aggregate_share(0) == (want["agg"], want["count"], want["checksum"])
+        # aggregate_share's scratch must not free the host path's output buffer.
+        # Call again, after the read, with a larger batch: verdicts, prep messages and the running
+        # aggregate (now both calls) still equal the oracle's.
+        n2 = n + 1500
+        orc2, nonces2, ps2, his2, lps2 = _batch(vdaf, vk, n2, seed=100 + P)
+        want2 = orc2.helper_prep_batch(vk, nonces2, ps2, his2, lps2, nthreads=16)
+        v2, m2 = eng.prep_and_aggregate(nonces2, ps2, his2, lps2)
+        np.testing.assert_array_equal(v2, want2["verdicts"])
+        fin2 = want2["verdicts"] == 0
+        np.testing.assert_array_equal(m2[fin2], want2["prep_msgs"][fin2])
+        agg, cnt, cs = eng.aggregate_share(0)
+        both = [(int.from_bytes(want["agg"][i:i + 16], "little") + int.from_bytes(want2["agg"][i:i + 16], "little"))
+                % P128 for i in range(0, len(want["agg"]), 16)]
+        assert agg == b"".join(x.to_bytes(16, "little") for x in both)
+        assert cnt == want["count"] + want2["count"]
+        assert cs == bytes(a ^ b for a, b in zip(want["checksum"], want2["checksum"]))
+        assert eng.memory()["last_pipelines"] == P

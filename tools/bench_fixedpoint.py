@@ -111,13 +111,10 @@ def run(bits=16, length=10000, reports=40960, role_reports=65536, pool=48, steps
         helper_staging_gb = -(-int(reports * vdaf.meas_len * 16 * 1.15) // (1 << 30)) + 2
 
     def helper_engine():
-        if not helper_staging_gb:
-            return HelperEngine(vdaf, vk)
-        os.environ["JX_STAGING_GB"] = str(helper_staging_gb)
-        try:
-            return HelperEngine(vdaf, vk)
-        finally:
-            del os.environ["JX_STAGING_GB"]
+        h = HelperEngine(vdaf, vk)
+        if helper_staging_gb:  # one launch per job (staging comes from the device arena per launch)
+            h.debug(5, reports)
+        return h
 
     def timed_steps(step, engines):
         for _ in range(warmup):
@@ -268,12 +265,8 @@ def run(bits=16, length=10000, reports=40960, role_reports=65536, pool=48, steps
         d_n, d_ps, d_his, d_lps = tile(nonces, R), tile(ps, R), tile(his, R), tile(lps, R)
         d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
         d_hv = torch.empty(R, dtype=torch.uint8, device=dev)
-        free, _ = torch.cuda.mem_get_info()
-        os.environ["JX_STAGING_GB"] = str(max(1, int(free * 0.85) >> 30))  # this engine owns the GPU
-        try:
-            helper = HelperEngine(vdaf, vk)
-        finally:
-            del os.environ["JX_STAGING_GB"]
+        helper = HelperEngine(vdaf, vk)
+        helper.debug(5, R)  # this engine owns the GPU: the whole step in one launch
 
         def hstep(timed):
             helper.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(), d_lps.data_ptr(), R,
