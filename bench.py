@@ -56,7 +56,8 @@ OPS_PER_MONT = 56
 OPS_PER_FMUL = 16
 ALG_OPS_PER_PERM = 3720
 ALG_OPS_PER_FMUL = 160
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_summary.json")
+K1_KERNEL = "jx::xof_kernel<false>"
 KERNEL_SOURCES = ["janus_amd/csrc/jx_kernels.hip", "janus_amd/csrc/jx_engine.cpp", "janus_amd/csrc/jx_kernels.h",
                   "janus_amd/csrc/jx_field.h", "janus_amd/csrc/jx_keccak.h", "janus_amd/csrc/jx_sha256.h"]
 
@@ -121,6 +122,19 @@ def pmc_clock(kernel: str):
     if d.get("workload", {}).get("sources_digest") != sources_digest():
         return None
     return d.get("kernels", {}).get(kernel, {}).get("clock_GHz")
+
+
+def pmc_kernel(kernel: str):
+    """(entry, reports per launch) of `kernel` in the committed PMC summary when it was taken on these
+    kernel sources, else (None, None)."""
+    try:
+        d = json.load(open(PMC_SUMMARY))
+    except (OSError, ValueError):
+        return None, None
+    wl = d.get("workload", {})
+    if wl.get("sources_digest") != sources_digest() or not wl.get("reports_per_launch"):
+        return None, None
+    return d.get("kernels", {}).get(kernel), wl["reports_per_launch"]
 
 
 def pmc_traffic(kernel: str, reports_per_launch: float):
@@ -417,6 +431,11 @@ def main():
             dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
         else:
             dist.init_process_group("nccl", device_id=dev)
+    # the world the collective actually formed: a launcher world that RCCL silently shrank would
+    # otherwise report one GPU's work as N GPUs'
+    rccl_world = dist.get_world_size() if use_dist else 1
+    if rccl_world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the process group has {rccl_world} ranks")
 
     vdaf = Prio3.sum_vec(args.bits, args.length, args.chunk)
     vk = bytes(range(16))
@@ -472,15 +491,17 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t
     kt = eng.timing_read()
+    elapsed_min = elapsed
     if use_dist:
         e = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.share_gpu else dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+        e2 = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.share_gpu else dev)
+        dist.all_reduce(e2, op=dist.ReduceOp.MIN)
+        elapsed, elapsed_min = float(e.item()), float(e2.item())
     # pipelines (jx_engine.cpp pipes_for): the launches of a step alternate over concurrent streams, so a
     # kernel's HIP-event duration includes the device time it shared with another launch's kernels. A few
     # single-stream steps after the timed region time every kernel alone (roofline.alone).
-    per_step = kt["xof"]["launches"] // max(1, args.steps)
-    pipes = min(per_step, args.pipes or 2) if per_step >= 2 and args.pipes != 1 else 1
+    pipes = eng.memory()["last_pipelines"]  # what the engine ran (fewer than asked if the arena was short)
     kt_alone = None
     if pipes > 1 and args.alone_steps > 0:
         eng.debug(4, 1)
@@ -516,10 +537,12 @@ def main():
 
     rank_ok = bool(verified and verdict_ok and msgs_ok)
     all_ok = rank_ok
+    ranks_verified = int(rank_ok)
     if use_dist:  # every rank checked its own range: the line reports the AND over ranks
         f = torch.tensor([int(rank_ok)], dtype=torch.int32, device="cpu" if args.share_gpu else dev)
-        dist.all_reduce(f, op=dist.ReduceOp.MIN)
-        all_ok = bool(f.item())
+        dist.all_reduce(f, op=dist.ReduceOp.SUM)
+        ranks_verified = int(f.item())
+        all_ok = ranks_verified == world
 
     total_reports = R * world * args.steps
     value = total_reports / elapsed
@@ -532,32 +555,47 @@ def main():
     # achieved rates from total kernel time over total reports (exact for unequal launches)
     k1_tops = work["ops_k1"] * per_rank / (kt["xof"]["ms"] * 1e-3) / 1e12
     k3_tops = work["ops_k3"] * per_rank / (kt["flp"]["ms"] * 1e-3) / 1e12
-    k1_alg = work["alg_ops_k1"] * per_rank / (kt["xof"]["ms"] * 1e-3) / 1e12
-    k3_alg = work["alg_ops_k3"] * per_rank / (kt["flp"]["ms"] * 1e-3) / 1e12
-    k1_dom = kt["xof"]["ms"] >= kt["flp"]["ms"]
-    dominant = "K1 xof_kernel" if k1_dom else "K3 flp_psum_part_kernel"
-    ach, alg = (k1_tops, k1_alg) if k1_dom else (k3_tops, k3_alg)
-    traffic, traffic_src, traffic_note = pmc_traffic("jx::xof_kernel<false>" if k1_dom else
-                                                     "jx::flp_psum_part_glds_kernel<2, false, false, 4, 4>", chunk_reports)
-    alg_bytes = (work["hbm_k1"] if k1_dom else work["hbm_k3"]) * chunk_reports
-    k1_clock = pmc_clock("jx::xof_kernel<false>")
+    # K1 (the XOF stage) is the dominant kernel: 4.7x K3's time per report
+    ach = k1_tops
+    k1_clock = pmc_clock(K1_KERNEL)
     k1_clock = round(k1_clock, 3) if k1_clock else None
-    dom_ms = k1_ms if k1_dom else k3_ms
     # the device over whole steps, and the kernels alone (single-stream steps after the timed region)
     ms_all = sum(kt[k]["ms"] for k in ("xof", "flp", "accumulate", "slow"))
     concurrency = ms_all / (elapsed * 1e3)  # kernels in flight on average (this rank's streams)
     dev_tops = (work["ops_k1"] + work["ops_k3"]) * per_rank / elapsed / 1e12
     alone = None
+    # K1's own rate: its launches on one stream (the alone steps after the timed region when pipelines
+    # overlap the timed launches, else the timed launches themselves)
+    ka, steps_a = (kt_alone, args.alone_steps) if kt_alone else (kt, args.steps)
+    la = max(1, ka["xof"]["launches"])
+    a_tops = work["ops_k1"] * R * steps_a / (ka["xof"]["ms"] * 1e-3) / 1e12
     if kt_alone:
-        la = max(1, kt_alone["xof"]["launches"])
-        a_tops = work["ops_k1"] * R * args.alone_steps / (kt_alone["xof"]["ms"] * 1e-3) / 1e12
         alone = {"steps": args.alone_steps, "k1_xof_ms_per_launch": round(kt_alone["xof"]["ms"] / la, 3),
                  "k3_flp_ms_per_launch": round(kt_alone["flp"]["ms"] / max(1, kt_alone["flp"]["launches"]), 3),
                  "k4_acc_ms_per_launch": round(kt_alone["accumulate"]["ms"] / max(1, kt_alone["accumulate"]["launches"]), 3),
-                 "kernel": "K1 xof_kernel", "achieved": round(a_tops, 3), "frac": round(a_tops / VALU_PEAK_TOPS, 4),
-                 "frac_of_mix_ceiling": round(a_tops / keccak_mix_ceiling_tops(), 4),
+                 "kernel": "K1 xof_kernel", "achieved_model": round(a_tops, 3),
+                 "frac_model": round(a_tops / VALU_PEAK_TOPS, 4),
                  "note": "the same step on one stream (debug option 4 = 1), untimed for `value`: each kernel's own "
-                         "issue rate"}
+                         "rate"}
+    # instructions per report: counted by the PMC pass (SQ_INSTS_VALU x 64 lanes, committed summary on these
+    # sources) when there is one, else the issue model (work_per_report)
+    pmc_k1, pmc_rpl = pmc_kernel(K1_KERNEL)
+    if pmc_k1 and "SQ_INSTS_VALU" in pmc_k1.get("pmc", {}):
+        lane_ops = pmc_k1["pmc"]["SQ_INSTS_VALU"] * 64 / pmc_rpl
+        frac_src = "PMC SQ_INSTS_VALU x 64 per report (" + os.path.relpath(PMC_SUMMARY, ROOT) + ") / K1 HIP-event " \
+                   "duration of its single-stream launches"
+        frac_pmc = pmc_k1["pmc"]["SQ_INSTS_VALU"] * 64 / (pmc_k1["avg_ns"] * 1e-9) / 1e12 / VALU_PEAK_TOPS
+    else:
+        lane_ops = work["ops_k1"]
+        frac_src = "issue model (2280 per Keccak-p[1600,12], bench.py sumvec_work) / K1 HIP-event duration of its " \
+                   "single-stream launches (no PMC summary on these sources)"
+        frac_pmc = None
+    own_tops = lane_ops * R * steps_a / (ka["xof"]["ms"] * 1e-3) / 1e12
+    alg_alone = work["alg_ops_k1"] * R * steps_a / (ka["xof"]["ms"] * 1e-3) / 1e12
+    rpl_alone = R * steps_a / la
+    k1_ms_alone = ka["xof"]["ms"] / la
+    traffic, traffic_src, traffic_note = pmc_traffic(K1_KERNEL, rpl_alone)
+    alg_bytes = work["hbm_k1"] * rpl_alone
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -580,38 +618,48 @@ def main():
                    "combine_note": "every step ends with the shard-record RCCL all-gather + device merge"
                    if combiner is not None else "N=1 with --no-dist: no combine in the step"},
         "startup": {"pool": how, "seconds": round(startup_s, 1)},
-        "roofline": {"bound": "valu", "kernel": dominant, "achieved": round(ach, 3), "peak": round(VALU_PEAK_TOPS, 2),
-                     "unit": "TOP/s int32 instruction issue (2280 per Keccak-p[1600,12]; DESIGN.md §5)",
-                     "frac": round(ach / VALU_PEAK_TOPS, 4),
+        "roofline": {"bound": "valu", "kernel": "K1 xof_kernel (helper XOF stage)", "achieved": round(own_tops, 3),
+                     "peak": round(VALU_PEAK_TOPS, 2),
+                     "unit": "TOP/s int32 lane-op issue (256 CU x 4 SIMD32 x 32 lanes x 2.4 GHz)",
+                     "frac": round(own_tops / VALU_PEAK_TOPS, 4),
+                     "frac_source": frac_src,
+                     "frac_pmc_run": round(frac_pmc, 4) if frac_pmc else None,
+                     "k1_ms_per_launch_alone": round(ka["xof"]["ms"] / la, 3),
+                     "reports_per_launch_alone": round(R * steps_a / la, 1),
+                     "frac_in_pipeline": round(ach / VALU_PEAK_TOPS, 4),
+                     "frac_device_step": round(dev_tops / VALU_PEAK_TOPS, 4),
+                     "kernel_concurrency": round(concurrency, 3),
+                     "frac_model_alone": round(a_tops / VALU_PEAK_TOPS, 4),
                      "mix_ceiling": round(keccak_mix_ceiling_tops(), 2),
-                     "frac_of_mix_ceiling": round(ach / keccak_mix_ceiling_tops(), 4) if k1_dom else None,
+                     "frac_of_mix_ceiling": round(a_tops / keccak_mix_ceiling_tops(), 4),
                      "clock_GHz_pmc": k1_clock,
-                     "frac_of_mix_ceiling_at_clock": round(ach / (keccak_mix_ceiling_tops() * k1_clock / 2.4), 4)
-                     if (k1_dom and k1_clock) else None,
+                     "frac_of_mix_ceiling_at_clock": round(a_tops / (keccak_mix_ceiling_tops() * k1_clock / 2.4), 4)
+                     if k1_clock else None,
                      "mix_note": "mix_ceiling = the Keccak round's issue ceiling at the measured per-instruction "
                                  "rates (bench.py KECCAK_ROUND_MIX, DESIGN.md §5), nominal 2.4 GHz; "
-                                 "_at_clock scales it to the PMC shader clock under K1",
-                     "achieved_algorithmic": round(alg, 3),
-                     "frac_algorithmic": round(alg / VALU_PEAK_TOPS, 4),
+                                 "_at_clock scales it to the PMC shader clock under K1; both over K1 alone (model count)",
+                     "achieved_algorithmic": round(alg_alone, 3),
+                     "frac_algorithmic": round(alg_alone / VALU_PEAK_TOPS, 4),
                      "algorithmic_unit": "TOP/s of the spec's 32-bit ops (3720 per Keccak-p[1600,12], 160 per "
-                                         "Field128 product), kernel-independent",
+                                         "Field128 product), kernel-independent, K1 alone",
                      "traffic": traffic, "traffic_unit": "HBM bytes per average launch (rocprofv3 2*FETCH_SIZE + "
                                                          "WRITE_SIZE)",
                      "traffic_source": traffic_src, "traffic_note": traffic_note,
-                     "algorithmic_bytes": int(alg_bytes), "reports_per_launch": round(chunk_reports, 1),
-                     "hbm_GBps": round(alg_bytes / (dom_ms * 1e-3) / 1e9, 1),
+                     "algorithmic_bytes": int(alg_bytes), "reports_per_launch": round(rpl_alone, 1),
+                     "hbm_GBps": round(alg_bytes / (k1_ms_alone * 1e-3) / 1e9, 1),
                      "hbm_peak_GBps": HBM_PEAK_GBPS,
                      "pipelines": pipes, "kernel_concurrency": round(concurrency, 3),
                      "device_step": {"achieved": round(dev_tops, 3), "frac": round(dev_tops / VALU_PEAK_TOPS, 4),
                                      "note": "(K1 + K3 issue-model instructions per report) x this rank's reports / "
                                              "the timed wall time: the whole device over whole steps"},
                      "alone": alone,
-                     "frac_note": "achieved / frac: the dominant kernel's instructions per launch over its HIP-event "
-                                  "launch duration in the timed steps. With pipelines > 1 the launches of a step "
-                                  "alternate over concurrent streams and a launch shares the device with the other "
-                                  "pipeline's kernels for part of its duration (kernel_concurrency = summed kernel "
-                                  "durations / wall time): the kernel's own issue rate is `alone`, the device's "
-                                  "`device_step`"},
+                     "frac_note": "frac: K1's own issue rate, its instructions per report (PMC-counted when the "
+                                  "committed summary matches these sources) x reports / its HIP-event duration on one "
+                                  "stream; frac_pmc_run: the same from the PMC run alone (rocprof duration). "
+                                  "frac_in_pipeline: K1's issue-model work over its HIP-event duration inside the "
+                                  "timed pipelined steps, where a launch shares the device with the other pipeline "
+                                  "(kernel_concurrency = summed kernel durations / wall time); frac_device_step: "
+                                  "(K1 + K3 issue-model instructions) x reports / timed wall time"},
         "kernels": {"pipelines": pipes, "k1_xof_ms_per_launch": round(k1_ms, 3), "k3_flp_ms_per_launch": round(k3_ms, 3),
                     "k4_acc_ms_per_launch": round(kt["accumulate"]["ms"] / max(1, kt["accumulate"]["launches"]), 3),
                     "slow_ms_per_launch": round(kt["slow"]["ms"] / max(1, kt["slow"]["launches"]), 3),
@@ -621,11 +669,15 @@ def main():
                     "k3_hbm_GBps": round(work["hbm_k3"] * chunk_reports / (k3_ms * 1e-3) / 1e9, 1),
                     "work_per_report": work},
         "verified": all_ok,
+        "rccl_world": rccl_world, "ranks_verified": ranks_verified,
+        "collective": ("gloo (--share-gpu rehearsal)" if args.share_gpu else "nccl (RCCL)") if use_dist else None,
+        "elapsed_spread": round(elapsed / elapsed_min, 4) if elapsed_min > 0 else None,
         "verification": {"all_ranks": all_ok, "aggregate_and_count": bool(verified), "verdicts": verdict_ok,
                          "prep_msgs_of_finished_reports": msgs_ok,
                          "rank_range": [start, stop], "note": "rank r holds global reports [r R, (r+1) R) of the "
                          "cyclic pool tiling; expected aggregates from the pool's block aggregates (CyclicPool); all_ranks = "
-                         "every rank's own check (MIN over ranks), the other fields are rank 0's"},
+                         "every rank's own check (ranks_verified of rccl_world ranks), the other fields are rank 0's; "
+                         "elapsed_spread = max / min per-rank timed seconds"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(orc, vdaf, vk, nonces, ps, his, lps, args.cpu_seconds, cpu["threads"])
@@ -661,16 +713,17 @@ def secondary_configs(cpu: dict, threads: int) -> dict:
     t0 = time.perf_counter()
     sec = {}
     specs = [
+        # timed steps: Count's 100k-report call takes ~0.13 ms, so 200 of them (~30 ms) get above timer noise
         ("configs[0]", "Prio3Count (configs[0]: 100k reports)", Prio3.count(),
-         lambda rng, K: rng.integers(0, 2, size=(K, 1), dtype=np.uint64), 100_000),
+         lambda rng, K: rng.integers(0, 2, size=(K, 1), dtype=np.uint64), 100_000, 200),
         ("configs[1]", "Prio3Sum bits=32 (configs[1])", Prio3.sum(32),
-         lambda rng, K: rng.integers(0, 1 << 32, size=(K, 1), dtype=np.uint64), 1_000_000),
+         lambda rng, K: rng.integers(0, 1 << 32, size=(K, 1), dtype=np.uint64), 1_000_000, 10),
         ("configs[2]", "Prio3Histogram length=256 chunk_length=16 (configs[2])", Prio3.histogram(256, 16),
-         lambda rng, K: rng.integers(0, 256, size=(K, 1), dtype=np.uint64), 1_000_000),
+         lambda rng, K: rng.integers(0, 256, size=(K, 1), dtype=np.uint64), 1_000_000, 10),
     ]
-    for key, name, v, fn, R in specs:
+    for key, name, v, fn, R, nsteps in specs:
         t = time.perf_counter()
-        r = BC.run(name, v, fn, R, 4096, 3, 1, 3.0, threads, cpu)
+        r = BC.run(name, v, fn, R, 4096, nsteps, 1, 3.0, threads, cpu)
         r["roofline"] = issue_roofline(v, "helper", R, r["kernels"])
         r["driver_seconds"] = round(time.perf_counter() - t, 1)
         sec[key] = r

@@ -341,7 +341,9 @@ int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]);
  *             launches alternate over them, their accumulations stay in launch order). A call runs with
  *             fewer when the arena cannot stage them all at once (jx_engine_memory: last_pipelines);
  *   option 5: reports per launch of the fused paths: 0 automatic (whole K1 rounds within ~48 GiB of
- *             staging), else >= 64 (rounded down to a multiple of 64). */
+ *             staging), else >= 64 (rounded down to a multiple of 64);
+ *   option 6: lane-split K1 workgroups per CU (its placement for chain-latency-bound launches): 2 default
+ *             (at most two waves per SIMD), 0 no cap, 1..8. */
 int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value);
 
 const char* jx_status_str(int32_t status);

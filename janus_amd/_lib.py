@@ -10,8 +10,6 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libjanus_prio3.so")
-if os.environ.get("JX_LIB_VARIANT"):  # measurement builds (e.g. tools/k3_probe.sh): lib/libjanus_prio3_<variant>.so
-    LIB_PATH = os.path.join(_HERE, "lib", f"libjanus_prio3_{os.environ['JX_LIB_VARIANT']}.so")
 
 # Every symbol include/jx_prio3.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (

@@ -28,11 +28,10 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, variant: str = "", defines: tuple = ()) -> str:
-    """Build the library; `variant` + `defines` make a measurement build lib/libjanus_prio3_<variant>.so
-    (loaded only when JX_LIB_VARIANT names it)."""
-    out = OUT if not variant else os.path.join(os.path.dirname(OUT), f"libjanus_prio3_{variant}.so")
-    if not variant and not force and not _stale():
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Build the library (measurement variants live in tools/kernel_probe.hip, not here)."""
+    out = OUT
+    if not force and not _stale():
         return OUT
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -40,9 +39,8 @@ def build(force: bool = False, verbose: bool = False, variant: str = "", defines
     # compile the translation units in parallel
     procs = []
     for src in SOURCES:
-        obj = os.path.join(os.path.dirname(out), os.path.basename(src) + (f".{variant}" if variant else "") + ".o")
+        obj = os.path.join(os.path.dirname(out), os.path.basename(src) + ".o")
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-x", "hip", "-c", src, "-o", obj]
-        cmd += [f"-D{d}" for d in defines]
         cmd += EXTRA_FLAGS.get(os.path.basename(src), [])
         procs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), cmd))
         objs.append(obj)

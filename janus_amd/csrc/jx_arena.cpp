@@ -108,29 +108,33 @@ hipError_t arena_get(Arena* A, size_t bytes, hipStream_t s, bool staging, bool m
     while (A->allocated + bytes > A->budget && trim_one(A)) {
     }
     if (A->allocated + bytes <= A->budget) {
+      // the budget is reserved under the lock and the device allocation made outside it: a large hipMalloc
+      // takes milliseconds, and every other engine's check-outs (batches, staging) must not wait for it
+      A->allocated += bytes;
+      lk.unlock();
       void* p = nullptr;
       hipError_t st = hipMalloc(&p, bytes);
-      if (st == hipErrorOutOfMemory) {  // the device (other users, torch) is fuller than the budget
-        (void)hipGetLastError();
-        while (trim_one(A)) {
-        }
-        st = hipMalloc(&p, bytes);
-      }
+      hipEvent_t ev = nullptr;
       if (st == hipSuccess) {
-        hipEvent_t ev = nullptr;
         st = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-        if (st != hipSuccess) {
-          (void)hipFree(p);
-          return st;
-        }
+        if (st != hipSuccess) (void)hipFree(p);
+      }
+      lk.lock();
+      if (st == hipSuccess) {
         out = Slab{p, bytes, ev, nullptr, staging};
-        A->allocated += bytes;
         A->allocs++;
         account_out(A, out);
         return hipSuccess;
       }
+      A->allocated -= bytes;
       if (st != hipErrorOutOfMemory) return st;
       (void)hipGetLastError();
+      // the device (other users, torch) is fuller than the budget: give back the idle slabs and retry once
+      if (!A->free.empty()) {
+        while (trim_one(A)) {
+        }
+        continue;
+      }
     }
     // what is checked out holds the memory: staging comes back when its call has queued its work
     if (!may_wait || A->in_use_staging == 0) return hipErrorOutOfMemory;

@@ -68,7 +68,7 @@ struct Lane {
   uint64_t reports = 0, cap_reports = 0;
   uint32_t copying = 0, unconsumed = 0;
   std::vector<CReq*> reqs;
-  clk::time_point opened, launched;
+  clk::time_point opened, launched, last_arrival;
   // region offsets in h_in (rows of cap_reports)
   size_t o_non = 0, o_ps = 0, o_his = 0, o_lps = 0, o_lis = 0, o_vk = 0, o_jobs = 0;
   // region offsets in h_out
@@ -107,6 +107,10 @@ static std::string coal_key(const jx_engine* e) {
   return std::to_string(e->device) + "/" + std::to_string(c.algo) + "/" + std::to_string(c.bits) + "/" +
          std::to_string(c.length) + "/" + std::to_string(c.chunk) + "/" + std::to_string(c.np);
 }
+
+// A gathering lane also closes once no job has joined it for this long: the callers a finished launch
+// wakes come back in a burst, and the launch should not wait out the whole window for a straggler.
+constexpr uint32_t kQuietUs = 100;
 
 static uint32_t cur_window_us(const Coalescer* C) {
   if (C->window_us) return C->window_us;
@@ -186,8 +190,11 @@ static int32_t launch_lane(Coalescer* C, Lane& L, std::string& err) {
   uint32_t fl = SG_IN | SG_PREP | SG_RES | SG_VK | SG_JOBS;
   fl |= leader ? SG_LEAD : SG_HIN;
   if (!inpl) fl |= SG_MEAS;
+  // staging for a power of two of reports (>= 1,024): launches of varying size reuse the lane's slab
+  uint64_t cap = 1024;
+  while (cap < m) cap <<= 1;
   Stage st;
-  int32_t rc = stage_acquire(q, m, fl, st);
+  int32_t rc = stage_acquire(q, cap, fl, st);
   if (rc) {
     err = thread_error();
     return rc;
@@ -259,10 +266,17 @@ static void dispatcher_main(Coalescer* C) {
     if (C->stop) return;
     Lane& L = C->lanes[C->open];
     const auto deadline = L.opened + std::chrono::microseconds(cur_window_us(C));
-    C->cv.wait_until(lk, deadline, [&] {
+    auto ready = [&] {
       return C->stop || L.full || L.reports >= L.cap_reports || L.reqs.size() >= MAX_JOBS_PER_LAUNCH ||
              (C->last_jobs && L.reqs.size() >= C->last_jobs);
-    });
+    };
+    for (;;) {  // until ready, the window has passed, or the arrivals have gone quiet
+      const auto quiet = L.last_arrival + std::chrono::microseconds(kQuietUs);
+      const auto until = quiet < deadline ? quiet : deadline;
+      if (C->cv.wait_until(lk, until, ready)) break;
+      const auto now = clk::now();
+      if (now >= deadline || now >= L.last_arrival + std::chrono::microseconds(kQuietUs)) break;
+    }
     if (C->stop) return;
     L.state = SEALED;  // no more reservations; new callers open the next lane
     C->open = -1;
@@ -323,25 +337,25 @@ Coalescer* coalescer_for(jx_engine* e) {
   Coalescer* C = new Coalescer();
   C->key = key;
   C->device = e->device;
-  // the base: a child of e that owns a copy of the constant tables (e may go away before the coalescer)
-  jx_engine* base = new_child(e);
-  if (!base) {
-    delete C;
-    return nullptr;
-  }
-  size_t cbytes = 0;
-  {
-    // the constant table size: the same tables the creating engine holds
-    const Cfg& c = e->cfg;
-    cbytes = (size_t)(c.P + c.gpoly_len + jx::NMISC + c.P1 + c.gpoly1_len) * sizeof(uint4);
-  }
+  // the base: the engine state the lanes copy, with its own copy of the constant tables (e may go away
+  // before the coalescer) and no stream of its own (the device has few hardware queues: the lanes get them)
+  jx_engine* base = new jx_engine();
+  base->cfg = e->cfg;
+  base->device = e->device;
+  base->is_pipe = true;
+  base->arena = e->arena;
+  base->default_chunk = e->default_chunk;
+  base->auto_chunk = e->auto_chunk;
+  base->round_reports = e->round_reports;
+  base->lis_stride = e->lis_stride;
+  const Cfg& cc = e->cfg;
+  const size_t cbytes = (size_t)(cc.P + cc.gpoly_len + jx::NMISC + cc.P1 + cc.gpoly1_len) * sizeof(uint4);
   uint4* consts = nullptr;
   if (hipMalloc((void**)&consts, cbytes) != hipSuccess ||
-      hipMemcpyAsync(consts, e->d_consts, cbytes, hipMemcpyDeviceToDevice, base->stream) != hipSuccess ||
-      hipStreamSynchronize(base->stream) != hipSuccess) {
+      hipMemcpyAsync(consts, e->d_consts, cbytes, hipMemcpyDeviceToDevice, e->stream) != hipSuccess ||
+      hipStreamSynchronize(e->stream) != hipSuccess) {
     if (consts) (void)hipFree(consts);
-    base->d_consts = nullptr;
-    jx_engine_destroy(base);
+    delete base;
     delete C;
     return nullptr;
   }
@@ -353,7 +367,8 @@ Coalescer* coalescer_for(jx_engine* e) {
   for (uint32_t k = 0; k < kLanes; k++) {
     Lane& L = C->lanes[k];
     L.q = new_child(base);
-    if (!L.q || hipEventCreateWithFlags(&L.ev_done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess) {
+    // the completer spin-waits on this event (a blocking-sync event's interrupt wake-up measured ms late)
+    if (!L.q || hipEventCreateWithFlags(&L.ev_done, hipEventDisableTiming) != hipSuccess) {
       for (uint32_t j = 0; j <= k; j++) {
         if (C->lanes[j].q) jx_engine_destroy(C->lanes[j].q);
         if (C->lanes[j].ev_done) (void)hipEventDestroy(C->lanes[j].ev_done);
@@ -434,6 +449,7 @@ static Lane* reserve(Coalescer* C, std::unique_lock<std::mutex>& lk, CReq* r, in
       if (L.leader == r->leader && L.reports + r->n <= L.cap_reports && L.reqs.size() < MAX_JOBS_PER_LAUNCH) {
         r->first = L.reports;
         L.reports += r->n;
+        L.last_arrival = clk::now();
         L.reqs.push_back(r);
         L.copying++;
         C->cv.notify_all();
@@ -459,7 +475,7 @@ static Lane* reserve(Coalescer* C, std::unique_lock<std::mutex>& lk, CReq* r, in
         L.reports = 0;
         L.reqs.clear();
         L.copying = 0;
-        L.opened = clk::now();
+        L.opened = L.last_arrival = clk::now();
         C->open = (int)k;
         break;
       }
@@ -483,7 +499,7 @@ static int32_t coalesced(jx_engine* e, bool leader, uint64_t n, const uint8_t* n
   r.out_verdicts = out_verdicts;
   r.out_prep_shares = out_prep_shares;
   {
-    std::lock_guard<std::mutex> el(e->mu);
+    std::lock_guard<FairMutex> el(e->mu);
     HIPCHK(e, hipSetDevice(e->device));
     Batch* B = nullptr;
     int32_t rc = batch_new(e, n, leader, &r.id, &B);
@@ -493,7 +509,7 @@ static int32_t coalesced(jx_engine* e, bool leader, uint64_t n, const uint8_t* n
     r.batch_ev = B->slab.ev;
   }
   auto drop = [&](int32_t rc) {
-    std::lock_guard<std::mutex> el(e->mu);
+    std::lock_guard<FairMutex> el(e->mu);
     auto it = e->batches.find(r.id);
     if (it != e->batches.end()) batch_free(e, it);
     return rc;
@@ -546,7 +562,7 @@ static int32_t coalesced(jx_engine* e, bool leader, uint64_t n, const uint8_t* n
     return drop(r.rc);
   }
   {
-    std::lock_guard<std::mutex> el(e->mu);
+    std::lock_guard<FairMutex> el(e->mu);
     auto it = e->batches.find(r.id);
     if (it != e->batches.end()) it->second.pending = false;
     e->last_batch = r.id;

@@ -41,7 +41,7 @@ int32_t fail(jx_engine* e, int32_t code, const std::string& msg) {
 
 // every entry point: the engine mutex for the call, and a fresh per-thread error message
 #define LOCK(e)                                   \
-  std::lock_guard<std::mutex> _lk((e)->mu);       \
+  std::lock_guard<jxi::FairMutex> _lk((e)->mu);   \
   t_err.clear()
 
 
@@ -624,6 +624,7 @@ int32_t jxi::prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const ui
   b.consts = e->d_consts;
   b.force_slow = e->force_slow;
   b.k1_split = e->k1_split;
+  b.k1_lds = lanes_lds_bytes(e->lanes_wg_cap);
   // A helper launch that would give the fused two-sponge K1 less than one wave per SIMD is bound by
   // the per-report sponge latency, not by issue: the lane-split kernel runs it in twice the waves
   // (FixedPointBoundedL2VecSum 16 x 10000, 24,576 reports: 153 -> 92 ms on MI355X), and below one
@@ -944,6 +945,7 @@ static int32_t pipes_acquire(jx_engine* e, uint32_t P, uint64_t chunk, uint32_t 
     jx_engine* q = e->pipes[k];
     q->force_slow = e->force_slow;
     q->k1_split = e->k1_split;
+    q->lanes_wg_cap = e->lanes_wg_cap;
     q->timing = e->timing;
     q->acc_chunks = e->acc_chunks;
     int32_t rc = stage_acquire(q, chunk, flags, st[k], k == 0);
@@ -1007,7 +1009,9 @@ int32_t jx_engine_create_ex(const jx_prio3_params* params, const uint8_t* verify
   }
   e->arena = arena_for(device);
   arena_engine_add(e->arena);
-  e->lis_stride = e->cfg.lis_bytes;
+  // staged leader input shares (host-buffer leader path, coalesced leader launches): rows padded to 128 B for
+  // the instances whose FLP kernels read the measurement share in place, so those reads take whole lines
+  e->lis_stride = leader_inplace(e->cfg) ? (e->cfg.lis_bytes + 127u) / 128u * 128u : e->cfg.lis_bytes;
   std::vector<uint4> consts = make_consts(e->cfg);
   // On the engine stream, synchronized on it alone: creating an engine orders nothing with the caller's
   // streams (that is jx_engine_wait_stream's job).
@@ -1956,7 +1960,7 @@ int32_t jx_engine_coalesce(jx_engine* e, int32_t enable, uint32_t window_us) {
     if (!e->coal) e->coal = coalescer_for(e);
     if (!e->coal) return fail(e, JX_E_HIP, "coalesce: could not start the device coalescer");
   }
-  std::lock_guard<std::mutex> lk(e->mu);
+  std::lock_guard<FairMutex> lk(e->mu);
   e->coalesce = enable != 0;
   if (e->coal) coalescer_set_window(e, window_us);
   return JX_OK;
@@ -1984,6 +1988,12 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
   if (option == 2) {  // accumulate chunking (tests); staging is sized per call
     if (value < 1 || value > 4096) return JX_E_INVALID;
     e->acc_chunks = (uint32_t)value;
+    return JX_OK;
+  }
+  if (option == 6) {  // lane-split K1 workgroups per CU: 0 no cap, 1..8
+    if (value < 0 || value > 8) return JX_E_INVALID;
+    e->lanes_wg_cap = (uint32_t)value;
+    for (jx_engine* q : e->pipes) q->lanes_wg_cap = e->lanes_wg_cap;
     return JX_OK;
   }
   if (option == 5) {  // reports per launch of the fused paths: 0 automatic, else >= 64 (rounded down to 64)

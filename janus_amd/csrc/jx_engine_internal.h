@@ -6,6 +6,7 @@
 
 #include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <string>
@@ -112,13 +113,42 @@ enum : uint32_t {
 
 struct Coalescer;  // jx_coalesce.cpp
 
+// The engine mutex, handed over in arrival order: an engine serves many host threads (one per job in
+// flight), and with std::mutex a thread could wait behind a stream of others (measured: 2 s tail latency at
+// 64 threads). Each waiter sleeps on its own condition variable; unlock wakes only the next one.
+class FairMutex {
+ public:
+  void lock() {
+    std::unique_lock<std::mutex> l(m_);
+    if (!locked_ && q_.empty()) {
+      locked_ = true;
+      return;
+    }
+    std::condition_variable cv;
+    q_.push_back(&cv);
+    cv.wait(l, [&] { return !locked_ && q_.front() == &cv; });
+    q_.pop_front();
+    locked_ = true;
+  }
+  void unlock() {
+    std::lock_guard<std::mutex> l(m_);
+    locked_ = false;
+    if (!q_.empty()) q_.front()->notify_one();
+  }
+
+ private:
+  std::mutex m_;
+  bool locked_ = false;
+  std::deque<std::condition_variable*> q_;
+};
+
 }  // namespace jxi
 
 struct jx_engine {
   jxi::Cfg cfg{};
   int device = 0;
   hipStream_t stream = nullptr;
-  std::mutex mu;  // held by every entry point for the duration of the call (coalesced prepares: not while waiting)
+  jxi::FairMutex mu;  // held by every entry point for the duration of the call (coalesced prepares: not while waiting)
   jxi::Arena* arena = nullptr;
   // per-call staging, carved from an arena slab by stage_acquire and cleared by its release
   uint64_t cap = 0;       // reports the current staging holds (0: none checked out)
@@ -180,6 +210,7 @@ struct jx_engine {
   uint64_t launches[jxi::NST] = {0, 0, 0, 0};
   uint32_t force_slow = 0;
   uint32_t k1_split = 0;  // helper K1: 0 automatic, 3 lane-split, 5 fused, 6 lane pairs (debug option 3)
+  uint32_t lanes_wg_cap = 2;  // lane-split K1 workgroups per CU (debug option 6; 0: no cap)
   // producer / consumer ordering (jx_engine_wait_stream / jx_engine_join_stream): reused events
   hipEvent_t ev_wait = nullptr, ev_join = nullptr;
   // Concurrent pipelines of the fused paths (pipes_for): child engines with their own stream run

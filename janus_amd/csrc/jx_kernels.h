@@ -124,6 +124,7 @@ struct Bufs {
   uint32_t force_slow;  // debug: route every report through the slow XOF kernel
   uint32_t k1_split;    // helper K1 kernel: 3 = lane-split (xof_lanes_kernel), 6 = lane pairs (xof_pairs_kernel,
                         // bits <= 32), otherwise the fused kernel
+  uint32_t k1_lds;      // dynamic LDS of the lane-split kernel: caps its workgroups per CU (lanes_lds_bytes)
 };
 
 struct AccArgs {
@@ -207,6 +208,7 @@ hipError_t launch_scatter_jobs(const Cfg& c, const JobSlice* d_jobs, uint32_t nj
                                hipStream_t s);
 // multiproof Field64 SumVec (jx_mp64.hip)
 uint64_t k1_round_reports(const Cfg& c, int device, uint32_t k1_split = 0);
+uint32_t lanes_lds_bytes(uint32_t wgs_per_cu);
 uint64_t mp_k1_round_reports(int device);
 hipError_t launch_mp_xof(const Cfg& c, const Bufs& b, hipStream_t s);
 hipError_t launch_mp_slow(const Cfg& c, const Bufs& b, hipStream_t s);

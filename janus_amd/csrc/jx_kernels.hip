@@ -456,6 +456,9 @@ __device__ __forceinline__ void sample2_f128(uint32_t* S, f128 out[2], uint32_t 
 // prepare-message seed, query randomness, FLP coefficients.
 // part_h: the helper's joint_rand_part. Writes msgs / flags / coef.
 // Returns flags (with FLAG_SLOW set if a rejected sample was hit and slow == false).
+// INL: the barycentric coefficient chains are inlined instead of called (the lane-split kernel, whose
+// registers have room for them: a call's frame and the registers saved around it cost it 80 B of scratch)
+template <bool INL = false>
 __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t lane, uint64_t r, bool write_msg,
                              const uint32_t nonce[4], const uint32_t part_l[4], const uint32_t lead_part[4],
                              const uint32_t part_h[4], uint32_t flags, bool slow) {
@@ -544,7 +547,13 @@ __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t
   const uint32_t C = c.calls;
   const uint32_t stride = c.algo == ALGO_SUM ? 1u : 2u;
   const f128 rcR = mpow(rR, c.chunk);  // r^chunk (ParallelSum's d_k = c_k r^((k-1) chunk))
-  const f128 sumc = bary_coeffs(coef, blk, NC, lane, tR, omega, C, COEF_C0, COEF_K, stride, c.algo != ALGO_SUM, rcR);
+  f128 sumc;
+  if constexpr (INL) {
+    [[clang::always_inline]] sumc =
+        bary_coeffs(coef, blk, NC, lane, tR, omega, C, COEF_C0, COEF_K, stride, c.algo != ALGO_SUM, rcR);
+  } else {
+    sumc = bary_coeffs(coef, blk, NC, lane, tR, omega, C, COEF_C0, COEF_K, stride, c.algo != ALGO_SUM, rcR);
+  }
   if (c.algo == ALGO_SUM) {
     // (1/2) * sum c_k, canonical: mont(sumc*R, 1/2) = sumc/2
     st_il(coef, blk, NC, COEF_HALFSUM, lane, mont128(sumc, u4_to_f(misc[1])));
@@ -582,7 +591,12 @@ __device__ uint32_t xof_tail(const Cfg& c, const Bufs& b, uint64_t blk, uint32_t
     const uint32_t B = c.coef1;
     st_il(coef, blk, NC, B + G1_L, lane, mont128(sub128(tp1, R1), u4_to_f(misc[7])));
     st_il(coef, blk, NC, B + G1_T, lane, t1R);
-    (void)bary_coeffs(coef, blk, NC, lane, t1R, b.consts + c.c_omega1, c.calls1, B + G1_C0, B + G1_K, 1);
+    if constexpr (INL) {
+      [[clang::always_inline]] (void)bary_coeffs(coef, blk, NC, lane, t1R, b.consts + c.c_omega1, c.calls1, B + G1_C0,
+                                                  B + G1_K, 1);
+    } else {
+      (void)bary_coeffs(coef, blk, NC, lane, t1R, b.consts + c.c_omega1, c.calls1, B + G1_C0, B + G1_K, 1);
+    }
   }
   return flags;
 }
@@ -599,7 +613,11 @@ __device__ __forceinline__ bool ge_exact(uint4 v) {
 // kernel (xof_lanes_kernel). Variants measured slower and removed: squeeze-only +
 // absorb-only launches, sequential S/J permutations at 3 waves/SIMD.
 constexpr uint32_t K1_WAVES = 4;  // waves (64-report blocks) per K1 workgroup
-template <bool WIDE = false>
+// PROBE (measurement variants, instantiated only by tools/kernel_probe.hip, never by the library):
+// 1 = the measurement-share staging stores skipped at run time by a uniform branch the compiler cannot
+// resolve (everything else as built), 2 = no per-block emission at all (stores, truncation, >= p screen),
+// 3 = the stores without the truncation and the screen. The variants write a sink to flags so nothing is dead.
+template <bool WIDE = false, int PROBE = 0>
 __global__ __launch_bounds__(64 * K1_WAVES, 1) void xof_kernel(Cfg c, Bufs b) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t blk = (uint64_t)blockIdx.x * K1_WAVES + (threadIdx.x >> 6);
@@ -657,9 +675,23 @@ __global__ __launch_bounds__(64 * K1_WAVES, 1) void xof_kernel(Cfg c, Bufs b) {
   f128 trunc_lo = make128(0, 0);
   uint4* const mp = b.meas + il_idx(blk, c.meas_len, 0, lane);
   uint4* const op = b.outs + il_idx(blk, c.out_len, 0, lane);
-  auto emit = [&](uint32_t e, uint4 v) { emit_meas<WIDE>(c, mp, op, e, v, gmax, tr, trunc_lo); };
+  uint32_t sink = 0;
+  auto emit = [&](uint32_t e, uint4 v) {
+    if constexpr (PROBE == 1) {
+      if (b.force_slow == 0x5EED5EEDu && e < c.meas_len) mp[(uint64_t)e * IL] = v;  // never true at run time
+      emit_meas<WIDE, false>(c, mp, op, e, v, gmax, tr, trunc_lo);
+    } else if constexpr (PROBE == 3) {
+      if (e < c.meas_len) mp[(uint64_t)e * IL] = v;
+    } else {
+      emit_meas<WIDE>(c, mp, op, e, v, gmax, tr, trunc_lo);
+    }
+  };
   // emit the measurement elements of block m (10 or 11, by parity)
   auto emit_block = [&](uint32_t m) {
+    if constexpr (PROBE == 2) {
+      sink ^= S[0] ^ S[41];
+      return;
+    }
     const uint32_t e0 = 21 * (m >> 1);
     if ((m & 1) == 0) {
 #pragma unroll
@@ -794,6 +826,7 @@ __global__ __launch_bounds__(64 * K1_WAVES, 1) void xof_kernel(Cfg c, Bufs b) {
   load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
   load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
   flags = xof_tail(c, b, blk, lane, r, r0 < b.n, nonce, part_l, lead_part, own_part, flags, false);
+  if constexpr (PROBE != 0) flags = (sink ^ gmax ^ (uint32_t)tr.T[0]) & ~FLAG_SLOW;
   if (b.force_slow) flags |= FLAG_SLOW;
   if (r0 < b.n) b.flags[r0] = flags;
 }
@@ -815,8 +848,12 @@ __device__ __forceinline__ uint32_t lower_to_upper(uint32_t v) {
   return r[0];
 }
 
-template <bool WIDE>  // WIDE (bits > 32) carries 4 more truncation words: built for 2 waves/SIMD
-__global__ __launch_bounds__(64 * K1_WAVES, WIDE ? 2 : 4) void xof_lanes_kernel(Cfg c, Bufs b) {
+// Registers: the XOF tail is inlined (xof_tail<true>) and the kernel is built for two waves per SIMD, so
+// nothing spills (no scratch); how many of its workgroups share a CU is capped at launch by dynamic LDS
+// it does not use (Bufs::k1_lds, jx_engine_debug option 6), the placement the two-jobs shape wants
+// (chain-latency-bound waves, at most two per SIMD).
+template <bool WIDE>  // WIDE (bits > 32) carries 4 more truncation words
+__global__ __launch_bounds__(64 * K1_WAVES, 2) void xof_lanes_kernel(Cfg c, Bufs b) {
   const uint32_t lane = threadIdx.x & 63;
   const bool jh = lane >= 32;
   const uint64_t gw = (uint64_t)blockIdx.x * K1_WAVES + (threadIdx.x >> 6);  // 32 reports per wave
@@ -1075,7 +1112,8 @@ __global__ __launch_bounds__(64 * K1_WAVES, WIDE ? 2 : 4) void xof_lanes_kernel(
     load16(b.nonces + 16 * r, nonce);
     load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
     load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
-    flags = xof_tail(c, b, blk, il, r, r0 < b.n, nonce, part_l, lead_part, own_part, flags, false);
+    [[clang::always_inline]] flags =
+        xof_tail<true>(c, b, blk, il, r, r0 < b.n, nonce, part_l, lead_part, own_part, flags, false);
     if (b.force_slow) flags |= FLAG_SLOW;
     if (r0 < b.n) b.flags[r0] = flags;
   }
@@ -2107,7 +2145,9 @@ __device__ __forceinline__ void lds_read4(uint32_t a0, uint32_t a1, uint32_t a2,
       : "memory");
 }
 // W: waves (slot groups) per workgroup
-template <int PPW, bool HIST, bool LEADER, int D, int W = K3W>
+// RING_ONLY (a measurement variant, instantiated only by tools/kernel_probe.hip): the ring, then a hash of
+// the column sums instead of the group finish (results wrong by design), to time the finish by difference.
+template <int PPW, bool HIST, bool LEADER, int D, int W = K3W, bool RING_ONLY = false>
 __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bufs b) {
   static_assert(PPW == 2, "lds_read4 reads c, d and two measurement rows");
   constexpr int ROWS = 2 + W * PPW;  // c_k, d_k, then x[wave][i]
@@ -2220,8 +2260,7 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
     }
   }
   if (g >= NG) return;
-#ifdef JX_K3_PROBE  // measurement build only (tools/k3_probe.sh): the ring without the group finish
-  {
+  if constexpr (RING_ONLY) {
     uint64_t h = 0;
 #pragma unroll
     for (int i = 0; i < PPW; i++)
@@ -2230,7 +2269,6 @@ __global__ __launch_bounds__(64 * W, 4) void flp_psum_part_glds_kernel(Cfg c, Bu
     b.part[((blk * c.ngt + g) * 4) * IL + lane] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), 0, 0);
     return;
   }
-#endif
   psum_part_finish<PPW, HIST, LEADER>(c, b, blk, g, lane, C, ae, ao, sx);
 }
 
@@ -2961,15 +2999,22 @@ hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
   else if (b.k1_split == 3) {  // lane-split: 32 reports per wave
     const dim3 g2((2 * nb + K1_WAVES - 1) / K1_WAVES);
     if (wide)
-      hipLaunchKernelGGL((xof_lanes_kernel<true>), g2, block, 0, s, c, b);
+      hipLaunchKernelGGL((xof_lanes_kernel<true>), g2, block, b.k1_lds, s, c, b);
     else
-      hipLaunchKernelGGL((xof_lanes_kernel<false>), g2, block, 0, s, c, b);
+      hipLaunchKernelGGL((xof_lanes_kernel<false>), g2, block, b.k1_lds, s, c, b);
   } else if (wide)
     hipLaunchKernelGGL((xof_kernel<true>), grid, block, 0, s, c, b);
   else
     hipLaunchKernelGGL((xof_kernel<false>), grid, block, 0, s, c, b);
   return hipGetLastError();
 }
+// Dynamic LDS that caps the lane-split kernel at `wgs_per_cu` workgroups per CU (0: no cap).
+uint32_t lanes_lds_bytes(uint32_t wgs_per_cu) {
+  if (wgs_per_cu == 0) return 0;
+  constexpr uint32_t LDS_PER_CU = 160u << 10;
+  return (LDS_PER_CU / (wgs_per_cu + 1) + 1024u) / 1024u * 1024u;
+}
+
 // Reports that occupy every K1 wave slot of the device exactly once: CUs x resident
 // workgroups per CU (from the kernel's register/LDS footprint) x 64 reports per wave. K1 waves
 // all run the same length, so a launch runs in ceil(reports / this) equal "rounds"; the
@@ -2984,7 +3029,7 @@ uint64_t k1_round_reports(const Cfg& c, int device, uint32_t k1_split) {
   if (c.algo == ALGO_COUNT) {
     st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, count_kernel<false>, threads, 0);
   } else if (k1_split == 3) {
-    st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_lanes_kernel<false>, threads, 0);
+    st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_lanes_kernel<false>, threads, lanes_lds_bytes(2));
     per_wg = threads / 2;
   } else if (k1_split == 6) {
     st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_pairs_kernel, threads, 0);

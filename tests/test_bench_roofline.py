@@ -48,3 +48,22 @@ def test_prio3_work_matches_sumvec_model_and_roofline_picks_dominant():
     r = bench.issue_roofline(Prio3.count(), "helper", 1000, {"k1_ms_per_launch": 1.0, "k3_ms_per_launch": 0.0})
     assert r["kernel"] == "K1 (XOF)"
     json.dumps(r)  # the bench line is JSON
+
+
+def test_pmc_kernel_instruction_count_only_on_these_sources(tmp_path, monkeypatch):
+    """roofline.frac takes K1's instructions per report from the committed PMC summary only when that
+    summary was taken on these kernel sources (bench.pmc_kernel)."""
+    k = bench.K1_KERNEL
+    summary = {"workload": {"reports_per_launch": 262144, "sources_digest": "other"},
+               "kernels": {k: {"avg_ns": 26.0e6, "pmc": {"SQ_INSTS_VALU": 16.0e9}}}}
+    p = tmp_path / "s.json"
+    p.write_text(json.dumps(summary))
+    monkeypatch.setattr(bench, "PMC_SUMMARY", str(p))
+    assert bench.pmc_kernel(k) == (None, None)
+    summary["workload"]["sources_digest"] = bench.sources_digest()
+    p.write_text(json.dumps(summary))
+    ent, rpl = bench.pmc_kernel(k)
+    assert rpl == 262144 and ent["pmc"]["SQ_INSTS_VALU"] == 16.0e9
+    # the PMC run's own issue fraction: instructions x 64 lanes / duration / 78.6 T
+    frac = ent["pmc"]["SQ_INSTS_VALU"] * 64 / (ent["avg_ns"] * 1e-9) / 1e12 / bench.VALU_PEAK_TOPS
+    assert 0.4 < frac < 0.6

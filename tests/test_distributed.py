@@ -169,7 +169,7 @@ def _bench_shard_rank(rank, world, port, name, R, q):
         q.put((rank, False, False, False, repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 @pytest.mark.parametrize("name,R", [("sumvec_small.json", 23), ("count.json", 17)])
 def test_bench_distinct_shard_expectations(world, name, R):
     """bench.py's N > 1 verification: ranks hold distinct global report ranges, and the expected rank

@@ -39,3 +39,6 @@ def test_two_ranks_on_one_gpu_verify():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["global_reports_per_step"] == 40000
     assert out["verified"] is True and out["verification"]["all_ranks"] is True, out.get("verification")
+    # the self-checking fields the 8-GPU run carries: the collective's world, ranks verified, timing spread
+    assert out["rccl_world"] == 2 and out["ranks_verified"] == 2
+    assert out["elapsed_spread"] >= 1.0

@@ -171,8 +171,9 @@ def test_reference_e2e_result(bits):
     assert vdaf.decode_fixedpoint_result(total, 4) == [0.5, 0.5, 0.6875]
 
 
-@pytest.mark.parametrize("split", [0, 3, 6, 5], ids=["auto", "lanes", "pairs", "fused"])
-def test_two_jobs_in_flight(split):
+@pytest.mark.parametrize("split,padded", [(0, False), (3, False), (6, False), (5, False), (0, True)],
+                         ids=["auto", "lanes", "pairs", "fused", "auto-padded-rows"])
+def test_two_jobs_in_flight(split, padded):
     """configs[4]'s bench shape (tools/bench_fixedpoint.py, two jobs in flight): while the helper engine
     prepares job i-1 on its stream, the leader engine initializes job i on its own; then the leader
     finishes job i-1. Inputs live in HBM (a 24-report pool tiled to 4,096 reports per job), the helper's
@@ -201,7 +202,16 @@ def test_two_jobs_in_flight(split):
     def tile(x):
         return torch.from_numpy(np.array(x).reshape(K, -1)).to(dev).repeat(-(-R // K), 1)[:R].contiguous()
 
-    d_n, d_ps, d_lis, d_his = tile(nonces), tile(ps), tile(lis), tile(his)
+    # padded: the leader's input-share rows at a 128-byte multiple stride (jx_leader_prep_init_device_ex),
+    # with garbage in the padding (it must never be read)
+    stride = -(-lis.shape[1] // 128) * 128 if padded else 0
+    if padded:
+        rows = np.full((K, stride), 0xA5, np.uint8)
+        rows[:, :lis.shape[1]] = lis
+        d_lis = tile(rows)
+    else:
+        d_lis = tile(lis)
+    d_n, d_ps, d_his = tile(nonces), tile(ps), tile(his)
     d_lps = [torch.empty((R, vdaf.prep_share_len), dtype=torch.uint8, device=dev) for _ in range(2)]
     d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
     d_hv = torch.empty(R, dtype=torch.uint8, device=dev)
@@ -212,7 +222,7 @@ def test_two_jobs_in_flight(split):
         prev = None
         for i in range(jobs + 1):
             bid = leader.leader_init_device(R, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(),
-                                            d_lps[i % 2].data_ptr()) if i < jobs else None
+                                            d_lps[i % 2].data_ptr(), lis_stride=stride) if i < jobs else None
             if prev is not None:
                 helper.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(),
                                                  d_lps[(i - 1) % 2].data_ptr(), R, 0, d_msgs.data_ptr(),

@@ -61,7 +61,7 @@ def make_pool(bits, length, K, vk, threads):
 
 
 def run(bits=16, length=10000, reports=40960, role_reports=65536, pool=48, steps=3, warmup=1, cpu_seconds=10.0,
-        skip=(), helper_staging_gb=-1):
+        skip=(), helper_staging_gb=-1, pad_lis=True, lanes_cap=None, helper_k1=None):
     """The configs[4] legs (ping-pong one job at a time, two jobs in flight, each role alone, CPU
     baseline); returns one JSON-able dict. Every leg is verified against the oracle."""
     import torch
@@ -89,6 +89,18 @@ def run(bits=16, length=10000, reports=40960, role_reports=65536, pool=48, steps
         reps = -(-R // K)
         return torch.from_numpy(x2).to(dev).repeat(reps, 1)[:R].contiguous()
 
+    # the leader's input-share rows padded to a multiple of 128 bytes (jx_leader_prep_init_device_ex): the
+    # in-place FLP ring then reads whole cache lines (the leader assembles these rows after HPKE open, so the
+    # padding is free at that copy)
+    lis_stride = -(-lis.shape[1] // 128) * 128 if pad_lis else 0
+
+    def tile_lis(R):
+        if not lis_stride:
+            return tile(lis, R)
+        rows = np.zeros((K, lis_stride), np.uint8)
+        rows[:, :lis.shape[1]] = lis
+        return tile(rows, R)
+
     def tiled(x, R):  # host copy of tile(x, R): report g is pool report g % K
         return np.asarray(x)[np.arange(R) % K]
 
@@ -114,6 +126,10 @@ def run(bits=16, length=10000, reports=40960, role_reports=65536, pool=48, steps
         h = HelperEngine(vdaf, vk)
         if helper_staging_gb:  # one launch per job (staging comes from the device arena per launch)
             h.debug(5, reports)
+        if lanes_cap is not None:  # lane-split K1 workgroups per CU (jx_engine_debug option 6)
+            h.debug(6, lanes_cap)
+        if helper_k1 is not None:  # helper K1 kernel (option 3)
+            h.debug(3, helper_k1)
         return h
 
     def timed_steps(step, engines):
@@ -134,13 +150,14 @@ def run(bits=16, length=10000, reports=40960, role_reports=65536, pool=48, steps
         "unit": "reports/s", "n_gpus": 1, "steps": steps, "warmup": warmup, "higher_is_better": True,
         "data": f"synthetic: {K} distinct C-oracle client reports (1 in 6 with a false norm claim) tiled on device",
         "pool_seconds": round(pool_s, 1),
+        "leader_input_row_stride": lis_stride or int(lis.shape[1]),
     }
     verified = True
 
     # ---------------------------------------------------------------- ping-pong, both roles on one GPU
     if "pingpong" not in skip:
         R = reports
-        d_n, d_ps, d_lis, d_his = tile(nonces, R), tile(ps, R), tile(lis, R), tile(his, R)
+        d_n, d_ps, d_lis, d_his = tile(nonces, R), tile(ps, R), tile_lis(R), tile(his, R)
         d_lps = torch.empty((R, vdaf.prep_share_len), dtype=torch.uint8, device=dev)
         d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
         d_hv = torch.empty(R, dtype=torch.uint8, device=dev)
@@ -150,7 +167,8 @@ def run(bits=16, length=10000, reports=40960, role_reports=65536, pool=48, steps
 
         def step(timed):
             t = time.perf_counter()
-            bid = leader.leader_init_device(R, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(), d_lps.data_ptr())
+            bid = leader.leader_init_device(R, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(), d_lps.data_ptr(),
+                                            lis_stride=lis_stride)
             leader.sync()
             t1 = time.perf_counter()
             helper.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(), d_lps.data_ptr(), R,
@@ -201,7 +219,7 @@ def run(bits=16, length=10000, reports=40960, role_reports=65536, pool=48, steps
     # before the first step; job i-1's leader prep shares are complete (leader.sync) before its helper step.
     if "pipelined" not in skip:
         R = reports
-        d_n, d_ps, d_lis, d_his = tile(nonces, R), tile(ps, R), tile(lis, R), tile(his, R)
+        d_n, d_ps, d_lis, d_his = tile(nonces, R), tile(ps, R), tile_lis(R), tile(his, R)
         d_lps = [torch.empty((R, vdaf.prep_share_len), dtype=torch.uint8, device=dev) for _ in range(2)]
         d_msgs = torch.empty((R, 16), dtype=torch.uint8, device=dev)
         d_hv = torch.empty(R, dtype=torch.uint8, device=dev)
@@ -214,7 +232,7 @@ def run(bits=16, length=10000, reports=40960, role_reports=65536, pool=48, steps
         def pstep(timed):
             i = state["i"]
             bid = leader.leader_init_device(R, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(),
-                                            d_lps[i % 2].data_ptr(), stream=nf)
+                                            d_lps[i % 2].data_ptr(), stream=nf, lis_stride=lis_stride)
             if state["prev"] is not None:
                 helper.prep_and_aggregate_device(d_n.data_ptr(), d_ps.data_ptr(), d_his.data_ptr(),
                                                  d_lps[(i - 1) % 2].data_ptr(), R, 0, d_msgs.data_ptr(),
@@ -290,7 +308,7 @@ def run(bits=16, length=10000, reports=40960, role_reports=65536, pool=48, steps
         torch.cuda.empty_cache()
         log(f"helper alone: {roles['helper']}")
     if "leader" not in skip:
-        d_n, d_ps, d_lis = tile(nonces, R), tile(ps, R), tile(lis, R)
+        d_n, d_ps, d_lis = tile(nonces, R), tile(ps, R), tile_lis(R)
         d_lps = torch.empty((R, vdaf.prep_share_len), dtype=torch.uint8, device=dev)
         d_msgs = tile(want["prep_msgs"], R)  # the helper's Finish messages (rejected reports: peer verdicts)
         d_hv = tile(want["verdicts"], R).reshape(R).contiguous()
@@ -298,7 +316,8 @@ def run(bits=16, length=10000, reports=40960, role_reports=65536, pool=48, steps
         leader = HelperEngine(vdaf, vk)
 
         def lstep(timed):
-            bid = leader.leader_init_device(R, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(), d_lps.data_ptr())
+            bid = leader.leader_init_device(R, d_n.data_ptr(), d_ps.data_ptr(), d_lis.data_ptr(), d_lps.data_ptr(),
+                                            lis_stride=lis_stride)
             leader.leader_finish_device(bid, R, d_msgs.data_ptr(), d_hv.data_ptr(), d_lv.data_ptr())
             leader.accumulate_device(bid, R)
             leader.sync()
@@ -388,9 +407,15 @@ def main():
     ap.add_argument("--helper-staging-gb", type=int, default=-1,
                     help="staging budget of the helper engine in the two-role legs (default: sized so one launch "
                          "holds --reports; 0: the engine's own, 1/3 of HBM)")
+    ap.add_argument("--packed-lis", action="store_true",
+                    help="leader input shares in packed rows (no 128-byte padding of the row stride)")
+    ap.add_argument("--lanes-cap", type=int, default=None, help="lane-split K1 workgroups per CU (debug option 6)")
+    ap.add_argument("--helper-k1", type=int, default=None, help="helper K1 kernel (debug option 3: 3, 5, 6)")
     a = ap.parse_args()
     out = run(a.bits, a.length, a.reports, a.role_reports, a.pool, a.steps, a.warmup, a.cpu_seconds,
-              set(filter(None, a.skip.split(","))), a.helper_staging_gb)
+              set(filter(None, a.skip.split(","))), a.helper_staging_gb, pad_lis=not a.packed_lis,
+              lanes_cap=a.lanes_cap, helper_k1=a.helper_k1)
+    out["variant"] = {"packed_lis": a.packed_lis, "lanes_cap": a.lanes_cap, "helper_k1": a.helper_k1}
     print(json.dumps(out), flush=True)
 
 

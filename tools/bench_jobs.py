@@ -252,6 +252,9 @@ def main():
     ap.add_argument("--mode", default="direct", choices=("direct", "coalesce"))
     ap.add_argument("--window-us", type=int, default=0, help="coalesce mode: the gathering window (0: engine default)")
     ap.add_argument("--out", default=None, help="also append the JSON lines to this file")
+    ap.add_argument("--keep-pool", default=None,
+                    help="cpp driver: write the pool file(s) into this directory and keep them (for running "
+                         "tools/bin/jobs_driver directly, e.g. under rocprofv3)")
     ap.add_argument("--driver", default="cpp", choices=("cpp", "python"),
                     help="cpp: native threads (tools/jobs_driver.cpp) call the C ABI; python: Python threads "
                          "through janus_amd.engine (the interpreter's lock serialises their host work)")
@@ -275,7 +278,10 @@ def main():
 
             build_driver()
             with tempfile.TemporaryDirectory() as tmp:
-                for n in [int(x) for x in a.sizes.split(",")]:
+                if a.keep_pool:
+                    os.makedirs(a.keep_pool, exist_ok=True)
+                    tmp = a.keep_pool
+                for n in [int(x) for x in a.sizes.split(",") if int(x) > 0]:
                     for T in [int(x) for x in a.threads.split(",")]:
                         line = json.dumps(run_case_cpp(vdaf, vk, pool, n, T, a.seconds, a.mode, a.window_us, tmp))
                         print(line, flush=True)

@@ -188,7 +188,7 @@ int main(int argc, char** argv) {
   printf("{\"jobs\": %llu, \"reports\": %llu, \"wall_s\": %.4f, \"reports_per_s\": %.1f, \"prep_ms_p50\": %.3f, "
          "\"prep_ms_p99\": %.3f, \"job_ms_p50\": %.3f, \"job_ms_p99\": %.3f, \"bad_jobs\": %llu, \"launches\": %llu, "
          "\"jobs_per_launch\": %.2f, \"gather_ms\": %.3f, \"copy_ms\": %.3f, \"enqueue_ms\": %.3f, \"device_ms\": %.3f, "
-         "\"window_us\": %llu, \"arena_cross_stream_waits\": %llu}\n",
+         "\"window_us\": %llu, \"arena_cross_stream_waits\": %llu, \"arena_allocs\": %llu, \"arena_peak_gb\": %.2f}\n",
          (unsigned long long)njobs, (unsigned long long)(njobs * n), wall, njobs * n / wall, pct(lat_prep, 0.5),
          pct(lat_prep, 0.99), pct(lat_job, 0.5), pct(lat_job, 0.99), (unsigned long long)nbad, (unsigned long long)la,
          la ? (double)(m1.coalesced_jobs - m0.coalesced_jobs) / la : 0.0,
@@ -196,6 +196,7 @@ int main(int argc, char** argv) {
          la ? (m1.coalesce_copy_us - m0.coalesce_copy_us) / 1e3 / la : 0.0,
          la ? (m1.coalesce_enqueue_us - m0.coalesce_enqueue_us) / 1e3 / la : 0.0,
          la ? (m1.coalesce_device_us - m0.coalesce_device_us) / 1e3 / la : 0.0, (unsigned long long)m1.coalesce_window_us,
-         (unsigned long long)(m1.arena_cross_stream_waits - m0.arena_cross_stream_waits));
+         (unsigned long long)(m1.arena_cross_stream_waits - m0.arena_cross_stream_waits),
+         (unsigned long long)(m1.arena_allocs - m0.arena_allocs), m1.arena_peak / 1e9);
   return 0;
 }

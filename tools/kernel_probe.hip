@@ -1,0 +1,115 @@
+// kernel_probe.hip — measurement harness, never part of the library: the helper's K1 (XOF stage) and K3
+// (FLP ring) of SumVec 8x1000/88 launched directly on n reports of random bytes, in their product form and
+// in their measurement variants (template parameters the library never instantiates):
+//   K1 xof_kernel<false, 1>: the measurement-share staging stores skipped (a uniform run-time branch);
+//   K1 xof_kernel<false, 2>: no per-block emission at all (stores, truncation, >= p screen);
+//   K1 xof_kernel<false, 3>: the stores without the truncation and the >= p screen;
+//   K3 flp_psum_part_glds_kernel<..., RING_ONLY = true>: the ring without the group finish.
+// Timed by HIP events (ms per launch); run under rocprofv3 --pmc for each variant's clock and VALU
+// utilisation ("K1's clock"). Results of the variants are wrong by design.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/kernel_probe.hip -Iinclude -Ljanus_amd/lib -ljanus_prio3 \
+//         -Wl,-rpath,'$ORIGIN/../../janus_amd/lib' -o tools/bin/kernel_probe
+//   tools/bin/kernel_probe [reports=262144] [launches=5]
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../janus_amd/csrc/jx_engine_internal.h"
+#include "../janus_amd/csrc/jx_kernels.hip"
+
+#define CK(x)                                                                 \
+  do {                                                                        \
+    hipError_t _s = (x);                                                      \
+    if (_s != hipSuccess) {                                                   \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(_s));                 \
+      exit(1);                                                                \
+    }                                                                         \
+  } while (0)
+
+__global__ void fill_kernel(uint32_t* p, uint64_t words, uint32_t seed) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t x = (uint32_t)i * 0x9E3779B9u ^ seed;
+    x ^= x >> 16;
+    x *= 0x85EBCA6Bu;
+    x ^= x >> 13;
+    p[i] = x;
+  }
+}
+
+static void* dalloc(size_t bytes, uint32_t seed) {
+  void* p = nullptr;
+  CK(hipMalloc(&p, bytes ? bytes : 16));
+  hipLaunchKernelGGL(fill_kernel, dim3(1024), dim3(256), 0, 0, (uint32_t*)p, (uint64_t)(bytes / 4), seed);
+  return p;
+}
+
+template <typename F>
+static double time_ms(F launch, int n, hipStream_t s) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  launch();  // warm-up
+  CK(hipEventRecord(a, s));
+  for (int i = 0; i < n; i++) launch();
+  CK(hipEventRecord(b, s));
+  CK(hipEventSynchronize(b));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, a, b));
+  return ms / n;
+}
+
+int main(int argc, char** argv) {
+  const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 262144;
+  const int iters = argc > 2 ? atoi(argv[2]) : 5;
+  jx_prio3_params p{2, 8, 1000, 88, 1};
+  uint8_t vk[16] = {0};
+  jx_engine* e = nullptr;
+  if (jx_engine_create(&p, vk, 0, &e)) return 2;
+  const jx::Cfg c = e->cfg;
+  jx::Bufs b{};
+  b.n = n;
+  b.nonces = (const uint8_t*)dalloc(n * 16, 1);
+  b.ps = (const uint8_t*)dalloc(n * c.ps_bytes, 2);
+  b.his = (const uint8_t*)dalloc(n * c.his_bytes, 3);
+  b.lps = (const uint8_t*)dalloc(n * c.lps_bytes, 4);
+  b.meas = (uint4*)dalloc(n * c.meas_len * 16, 5);
+  b.proof = (uint4*)dalloc(n * c.proof_len * 16, 6);
+  b.outs = (uint4*)dalloc(n * c.out_len * 16, 7);
+  b.coef = (uint4*)dalloc(n * c.ncoef * 16, 8);
+  b.flags = (uint32_t*)dalloc(n * 4, 9);
+  b.part = (uint4*)dalloc(n * 64 * c.ngt, 10);
+  b.verdicts = (uint8_t*)dalloc(n, 11);
+  b.msgs = (uint8_t*)dalloc(n * 16, 12);
+  b.consts = e->d_consts;
+  b.lis_rs = c.lis_bytes;
+  b.k1_split = 5;
+  CK(hipDeviceSynchronize());
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  const uint32_t nb = (uint32_t)((n + 63) / 64);
+  const dim3 g1((nb + jx::K1_WAVES - 1) / jx::K1_WAVES), b1(64 * jx::K1_WAVES);
+  const double k1 = time_ms([&] { hipLaunchKernelGGL((jx::xof_kernel<false, 0>), g1, b1, 0, s, c, b); }, iters, s);
+  const double k1_sink = time_ms([&] { hipLaunchKernelGGL((jx::xof_kernel<false, 1>), g1, b1, 0, s, c, b); }, iters, s);
+  const double k1_noemit = time_ms([&] { hipLaunchKernelGGL((jx::xof_kernel<false, 2>), g1, b1, 0, s, c, b); }, iters, s);
+  const double k1_stores = time_ms([&] { hipLaunchKernelGGL((jx::xof_kernel<false, 3>), g1, b1, 0, s, c, b); }, iters, s);
+  const uint32_t grid = ((nb + 7) / 8) * 8 * c.ngroups;
+  const uint32_t g3 = grid / c.ngroups * ((c.ngroups + jx::K3W - 1) / jx::K3W);
+  const double k3 = time_ms(
+      [&] {
+        hipLaunchKernelGGL((jx::flp_psum_part_glds_kernel<2, false, false, 4, jx::K3W, false>), dim3(g3),
+                           dim3(64 * jx::K3W), 0, s, c, b);
+      },
+      iters, s);
+  const double k3_ring = time_ms(
+      [&] {
+        hipLaunchKernelGGL((jx::flp_psum_part_glds_kernel<2, false, false, 4, jx::K3W, true>), dim3(g3),
+                           dim3(64 * jx::K3W), 0, s, c, b);
+      },
+      iters, s);
+  printf("{\"reports\": %llu, \"launches\": %d, \"k1_ms\": %.3f, \"k1_no_stores_ms\": %.3f, \"k1_no_emission_ms\": %.3f, "
+         "\"k1_stores_only_ms\": %.3f, \"k3_ms\": %.3f, \"k3_ring_only_ms\": %.3f}\n",
+         (unsigned long long)n, iters, k1, k1_sink, k1_noemit, k1_stores, k3, k3_ring);
+  jx_engine_destroy(e);
+  return 0;
+}
