@@ -164,9 +164,10 @@ typedef struct {
 int32_t jx_engine_memory(const jx_engine* e, jx_memory_stats* out);
 
 /* Coalesced prepares (Conventions). enable != 0 joins the device coalescer of this Prio3 instance;
- * window_us: how long a launch gathers jobs after its first one arrives (0 = automatic: half the recent
- * launch latency, 20 us .. 2 ms; a launch also closes once it holds as many jobs as the previous one, or
- * a full launch). Calls already waiting are unaffected by a later disable. */
+ * window_us: the longest a launch gathers jobs after its first one arrives (0 = automatic: 1.5x the recent
+ * launch latency, 0.1 .. 20 ms). A launch closes earlier when it is full, or once no job has joined for
+ * 100 us while no other launch of the coalescer is running (or it already holds a quarter of a full
+ * launch). Calls already waiting are unaffected by a later disable. */
 int32_t jx_engine_coalesce(jx_engine* e, int32_t enable, uint32_t window_us);
 
 /* Batched helper_initialized + evaluate for n reports (host buffers).

@@ -15,9 +15,10 @@
 //        lane's pinned host rows itself (callers copy in parallel);
 //     3. waits (without its engine's mutex) until the launch is done, then copies its verdicts / prep
 //        messages / prep shares out of the lane's pinned result rows and returns its batch handle.
-//   dispatcher thread: closes the gathering lane when it holds a full launch, when as many jobs have
-//     come back as the previous launch held (closed-loop callers have all resubmitted), or when the
-//     gathering window has passed; then, on the lane's stream: one upload per input region, K1 -> K1' -> K3
+//   dispatcher thread: closes the gathering lane when it holds a full launch, once no job has joined for
+//     a quiet period while no other launch runs (a running launch's callers join this one when it
+//     returns), or when the gathering window has passed; then, on the lane's stream: one upload per input
+//     region, K1 -> K1' -> K3
 //     over all jobs (each report with its own task's verify key, Bufs::vkeys), one scatter kernel that
 //     copies every job's slice into its batch, one download of the results, an event.
 //   completer thread: waits for launches in order and wakes their callers.
@@ -51,6 +52,7 @@ struct CReq {
   int32_t rc = 0;
   std::string err;
   bool done = false;
+  std::condition_variable cv;  // this job's caller waits here for its launch (no herd of wake-ups)
 };
 
 enum LaneState { FREE, GATHER, SEALED, RUNNING, DONE };
@@ -82,7 +84,9 @@ struct Coalescer {
   int device = 0;
   jx_engine* base = nullptr;  // owns the constant tables the lanes share
   std::mutex mu;
-  std::condition_variable cv;
+  // one condition variable per kind of waiter: the dispatcher (a job joined, copies done), the completer (a
+  // launch queued), callers waiting for a lane to gather in; callers waiting for their launch use their own
+  std::condition_variable cv_disp, cv_comp, cv_lane;
   Lane lanes[kLanes];
   int open = -1;
   std::deque<int> running;
@@ -91,7 +95,7 @@ struct Coalescer {
   uint32_t refs = 0;
   uint32_t window_us = 0;         // 0: automatic
   double ewma_us = 0;             // launch latency
-  uint32_t last_jobs = 0;         // jobs of the last launch
+  uint32_t nrunning = 0;          // launches queued on the device and not yet done
   uint64_t max_reports = 0;       // reports per launch
   uint64_t launches = 0, jobs = 0, reports = 0;
   // per-phase totals (microseconds, summed over launches): gathering (first job -> closed), the callers'
@@ -112,11 +116,14 @@ static std::string coal_key(const jx_engine* e) {
 // wakes come back in a burst, and the launch should not wait out the whole window for a straggler.
 constexpr uint32_t kQuietUs = 100;
 
+// The longest a gathering lane waits for more jobs (automatic: 1.5x the recent launch latency, 0.1-20 ms). It
+// matters while another launch runs: the jobs that launch returns join this one instead of starting a
+// fragment of their own (closed-loop callers then share one launch per round trip).
 static uint32_t cur_window_us(const Coalescer* C) {
   if (C->window_us) return C->window_us;
-  if (C->ewma_us <= 0) return 500;
-  double w = 0.5 * C->ewma_us;
-  return (uint32_t)(w < 20 ? 20 : (w > 2000 ? 2000 : w));
+  if (C->ewma_us <= 0) return 2000;
+  double w = 1.5 * C->ewma_us;
+  return (uint32_t)(w < 100 ? 100 : (w > 20000 ? 20000 : w));
 }
 
 // bytes of one report's pinned input row / result row
@@ -251,38 +258,40 @@ static void finish_lane(Coalescer* C, Lane& L, int32_t rc, const std::string& er
     r->rc = rc;
     if (rc) r->err = err;
     r->done = true;
+    r->cv.notify_one();
   }
   L.unconsumed = (uint32_t)L.reqs.size();
   L.state = DONE;
-  if (L.unconsumed == 0) L.state = FREE;
-  C->cv.notify_all();
+  if (L.unconsumed == 0) {
+    L.state = FREE;
+    C->cv_lane.notify_all();
+  }
 }
 
 static void dispatcher_main(Coalescer* C) {
   (void)hipSetDevice(C->device);
   std::unique_lock<std::mutex> lk(C->mu);
   for (;;) {
-    C->cv.wait(lk, [&] { return C->stop || (C->open >= 0 && C->lanes[C->open].reports > 0); });
+    C->cv_disp.wait(lk, [&] { return C->stop || (C->open >= 0 && C->lanes[C->open].reports > 0); });
     if (C->stop) return;
     Lane& L = C->lanes[C->open];
     const auto deadline = L.opened + std::chrono::microseconds(cur_window_us(C));
-    auto ready = [&] {
-      return C->stop || L.full || L.reports >= L.cap_reports || L.reqs.size() >= MAX_JOBS_PER_LAUNCH ||
-             (C->last_jobs && L.reqs.size() >= C->last_jobs);
-    };
-    for (;;) {  // until ready, the window has passed, or the arrivals have gone quiet
-      const auto quiet = L.last_arrival + std::chrono::microseconds(kQuietUs);
-      const auto until = quiet < deadline ? quiet : deadline;
-      if (C->cv.wait_until(lk, until, ready)) break;
+    // Close when full; otherwise once the arrivals have gone quiet AND no other launch is running (or this one
+    // is already big enough to fill the device with its own phases); at the latest at the window's end.
+    for (;;) {
+      if (C->stop || L.full || L.reports >= L.cap_reports || L.reqs.size() >= MAX_JOBS_PER_LAUNCH) break;
       const auto now = clk::now();
-      if (now >= deadline || now >= L.last_arrival + std::chrono::microseconds(kQuietUs)) break;
+      if (now >= deadline) break;
+      const auto quiet_at = L.last_arrival + std::chrono::microseconds(kQuietUs);
+      if (now >= quiet_at && (C->nrunning == 0 || L.reports >= C->max_reports / 4)) break;
+      C->cv_disp.wait_until(lk, now < quiet_at && quiet_at < deadline ? quiet_at : deadline);
     }
     if (C->stop) return;
     L.state = SEALED;  // no more reservations; new callers open the next lane
     C->open = -1;
-    C->cv.notify_all();
+    C->cv_lane.notify_all();
     const auto t_sealed = clk::now();
-    C->cv.wait(lk, [&] { return L.copying == 0; });
+    C->cv_disp.wait(lk, [&] { return L.copying == 0; });
     lk.unlock();
     std::string err;
     L.launched = clk::now();
@@ -296,13 +305,13 @@ static void dispatcher_main(Coalescer* C) {
     C->launches++;
     C->jobs += L.reqs.size();
     C->reports += L.reports;
-    C->last_jobs = (uint32_t)L.reqs.size();
     if (rc) {
       finish_lane(C, L, rc, err);
     } else {
       L.state = RUNNING;
+      C->nrunning++;
       C->running.push_back((int)(&L - C->lanes));
-      C->cv.notify_all();
+      C->cv_comp.notify_one();
     }
   }
 }
@@ -311,7 +320,7 @@ static void completer_main(Coalescer* C) {
   (void)hipSetDevice(C->device);
   std::unique_lock<std::mutex> lk(C->mu);
   for (;;) {
-    C->cv.wait(lk, [&] { return C->stop || !C->running.empty(); });
+    C->cv_comp.wait(lk, [&] { return C->stop || !C->running.empty(); });
     if (C->running.empty() && C->stop) return;
     Lane& L = C->lanes[C->running.front()];
     C->running.pop_front();
@@ -321,6 +330,8 @@ static void completer_main(Coalescer* C) {
     lk.lock();
     C->ewma_us = C->ewma_us > 0 ? 0.8 * C->ewma_us + 0.2 * us : us;
     C->t_device += us;
+    C->nrunning--;
+    C->cv_disp.notify_one();  // a gathering lane may close now
     finish_lane(C, L, s == hipSuccess ? JX_OK : JX_E_HIP,
                 s == hipSuccess ? std::string() : std::string("coalesced launch: ") + hipGetErrorString(s));
   }
@@ -400,7 +411,9 @@ void coalescer_release(jx_engine* e) {
     std::lock_guard<std::mutex> lk(C->mu);
     C->stop = true;
   }
-  C->cv.notify_all();
+  C->cv_disp.notify_all();
+  C->cv_comp.notify_all();
+  C->cv_lane.notify_all();
   C->dispatcher.join();
   C->completer.join();
   uint4* consts = C->base->d_consts;
@@ -452,11 +465,11 @@ static Lane* reserve(Coalescer* C, std::unique_lock<std::mutex>& lk, CReq* r, in
         L.last_arrival = clk::now();
         L.reqs.push_back(r);
         L.copying++;
-        C->cv.notify_all();
+        C->cv_disp.notify_one();
         return &L;
       }
       L.full = true;  // close it now; wait for the next lane
-      C->cv.notify_all();
+      C->cv_disp.notify_one();
     } else {
       for (uint32_t k = 0; k < kLanes; k++) {
         Lane& L = C->lanes[k];
@@ -481,7 +494,7 @@ static Lane* reserve(Coalescer* C, std::unique_lock<std::mutex>& lk, CReq* r, in
       }
       if (C->open >= 0) continue;
     }
-    C->cv.wait(lk);
+    C->cv_lane.wait(lk);
   }
 }
 
@@ -542,9 +555,8 @@ static int32_t coalesced(jx_engine* e, bool leader, uint64_t n, const uint8_t* n
     for (uint64_t i = 0; i < n; i++) memcpy(dst + i * vb, row, vb);
   }
   lk.lock();
-  L->copying--;
-  C->cv.notify_all();
-  C->cv.wait(lk, [&] { return r.done; });
+  if (--L->copying == 0) C->cv_disp.notify_one();
+  r.cv.wait(lk, [&] { return r.done; });
   lk.unlock();
   if (r.rc == JX_OK) {
     memcpy(out_verdicts, L->h_out + L->r_ver + f, n);
@@ -554,7 +566,7 @@ static int32_t coalesced(jx_engine* e, bool leader, uint64_t n, const uint8_t* n
   lk.lock();
   if (--L->unconsumed == 0) {
     L->state = FREE;
-    C->cv.notify_all();
+    C->cv_lane.notify_all();
   }
   lk.unlock();
   if (r.rc) {

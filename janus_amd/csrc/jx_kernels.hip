@@ -854,6 +854,10 @@ __device__ __forceinline__ uint32_t lower_to_upper(uint32_t v) {
 // (chain-latency-bound waves, at most two per SIMD).
 template <bool WIDE>  // WIDE (bits > 32) carries 4 more truncation words
 __global__ __launch_bounds__(64 * K1_WAVES, 2) void xof_lanes_kernel(Cfg c, Bufs b) {
+  // Issue priority over co-resident waves of other kernels: this kernel runs the helper's chain-latency-bound
+  // launches, which in the two-jobs shape share SIMDs with the leader's K1 waves; the helper's chain is the
+  // step's critical path (the leader's init has slack), so its waves take the issue slots first.
+  __builtin_amdgcn_s_setprio(2);
   const uint32_t lane = threadIdx.x & 63;
   const bool jh = lane >= 32;
   const uint64_t gw = (uint64_t)blockIdx.x * K1_WAVES + (threadIdx.x >> 6);  // 32 reports per wave
