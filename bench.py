@@ -57,7 +57,7 @@ OPS_PER_FMUL = 16
 ALG_OPS_PER_PERM = 3720
 ALG_OPS_PER_FMUL = 160
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_summary.json")
-K1_KERNEL = "jx::xof_kernel<false>"
+K1_KERNEL = "jx::xof_kernel<false, 0>"  # rocprofv3 name of the helper K1 (jx_kernels.hip)
 KERNEL_SOURCES = ["janus_amd/csrc/jx_kernels.hip", "janus_amd/csrc/jx_engine.cpp", "janus_amd/csrc/jx_kernels.h",
                   "janus_amd/csrc/jx_field.h", "janus_amd/csrc/jx_keccak.h", "janus_amd/csrc/jx_sha256.h"]
 
@@ -744,9 +744,42 @@ def secondary_configs(cpu: dict, threads: int) -> dict:
                                            kernel="K1 leader xof_leader_kernel (two-jobs shape)")
     fp["driver_seconds"] = round(time.perf_counter() - t, 1)
     sec["configs[4]"] = fp
+    sec["jobs"] = job_granularity(threads)
     log(f"configs[4]: {fp['value']:.0f} reports/s (two jobs), verified={fp['verified']} ({fp['driver_seconds']} s); "
         f"secondary configs {time.perf_counter() - t0:.1f} s")
     return sec
+
+
+def job_granularity(threads: int) -> dict:
+    """The headline VDAF at Janus's aggregation-job size: 64 native threads submit 100-report
+    SumVec 8x1000/88 jobs to ONE engine through the host-buffer ABI (jx_helper_prep_batch -> jx_accumulate per
+    job; tools/jobs_driver.cpp in a child process), with the device coalescer on and off; every job's verdicts
+    and prep messages and the final aggregate verified against the oracle (tools/bench_jobs.py)."""
+    import tempfile
+
+    from janus_amd.vdaf import Prio3
+    from tools import bench_jobs as BJ
+
+    t = time.perf_counter()
+    v = Prio3.sum_vec(8, 1000, 88)
+    vk = bytes(range(16))
+    pool = BJ.make_pool(v, vk, 2048, threads)
+    BJ.build_driver()
+    out = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        for mode in ("coalesce", "direct"):
+            r = BJ.run_case_cpp(v, vk, pool, 100, 64, 2.0, mode, 0, tmp)
+            out[mode] = {k: r.get(k) for k in ("reports_per_s", "prep_ms_p50", "prep_ms_p99", "jobs", "jobs_per_launch",
+                                               "device_ms", "verified", "error") if k in r}
+    ok = all(x.get("verified") for x in out.values())
+    res = {"metric": "helper reports/sec at Janus's job size: 100-report Prio3SumVec 8x1000/88 jobs from 64 threads on "
+                     "one engine (prep_init+prep_next+aggregate per job)",
+           "value": out["coalesce"].get("reports_per_s"), "unit": "reports/s", "coalesced": out["coalesce"],
+           "one_call_at_a_time": out["direct"], "verified": ok,
+           "driver_seconds": round(time.perf_counter() - t, 1)}
+    log(f"jobs: coalesced {res['value']} reports/s, one call at a time {out['direct'].get('reports_per_s')}, "
+        f"verified={ok} ({res['driver_seconds']} s)")
+    return res
 
 
 def issue_roofline(v, role: str, reports: int, kernels: dict, kernel: str | None = None) -> dict:

@@ -96,6 +96,8 @@ struct Coalescer {
   uint32_t window_us = 0;         // 0: automatic
   double ewma_us = 0;             // launch latency
   uint32_t nrunning = 0;          // launches queued on the device and not yet done
+  uint32_t expect = 0;            // jobs of completed launches not yet back (closed-loop callers return)
+  clk::time_point expect_until;   // ... expected until then
   uint64_t max_reports = 0;       // reports per launch
   uint64_t launches = 0, jobs = 0, reports = 0;
   // per-phase totals (microseconds, summed over launches): gathering (first job -> closed), the callers'
@@ -112,9 +114,16 @@ static std::string coal_key(const jx_engine* e) {
          std::to_string(c.length) + "/" + std::to_string(c.chunk) + "/" + std::to_string(c.np);
 }
 
-// A gathering lane also closes once no job has joined it for this long: the callers a finished launch
-// wakes come back in a burst, and the launch should not wait out the whole window for a straggler.
+// A gathering lane closes once no job has joined it for kQuietUs, fewer than kMaxRunning launches are on the
+// device, and the callers of the launches that completed meanwhile have come back (up to kRejoinUs after the
+// completion: copying their results, accumulating, preparing their next job), so closed-loop callers share a
+// launch per round trip instead of splitting into fragments; open-loop arrivals wait at most the window. A
+// launch's device time is nearly flat in its size below a K1 round (the per-report sponge chain), so two
+// launches in flight, each carrying every job that is back, is the measured optimum (64
+// threads x 100-report jobs, 1 / 2 / 3 running and 1 / 3 ms rejoin).
 constexpr uint32_t kQuietUs = 100;
+constexpr uint32_t kRejoinUs = 3000;
+constexpr uint32_t kMaxRunning = 2;
 
 // The longest a gathering lane waits for more jobs (automatic: 1.5x the recent launch latency, 0.1-20 ms). It
 // matters while another launch runs: the jobs that launch returns join this one instead of starting a
@@ -276,15 +285,20 @@ static void dispatcher_main(Coalescer* C) {
     if (C->stop) return;
     Lane& L = C->lanes[C->open];
     const auto deadline = L.opened + std::chrono::microseconds(cur_window_us(C));
-    // Close when full; otherwise once the arrivals have gone quiet AND no other launch is running (or this one
-    // is already big enough to fill the device with its own phases); at the latest at the window's end.
+    // Close when full; otherwise once the arrivals have gone quiet, the callers of completed launches are back
+    // and fewer than kMaxRunning launches run (or this one is already big enough to fill the device with its own
+    // phases); at the latest at the window's end.
     for (;;) {
       if (C->stop || L.full || L.reports >= L.cap_reports || L.reqs.size() >= MAX_JOBS_PER_LAUNCH) break;
       const auto now = clk::now();
       if (now >= deadline) break;
       const auto quiet_at = L.last_arrival + std::chrono::microseconds(kQuietUs);
-      if (now >= quiet_at && (C->nrunning == 0 || L.reports >= C->max_reports / 4)) break;
-      C->cv_disp.wait_until(lk, now < quiet_at && quiet_at < deadline ? quiet_at : deadline);
+      const bool back = C->expect == 0 || now >= C->expect_until;
+      if (now >= quiet_at && ((back && C->nrunning < kMaxRunning) || L.reports >= C->max_reports / 4)) break;
+      auto until = deadline;
+      if (now < quiet_at && quiet_at < until) until = quiet_at;
+      if (!back && C->expect_until < until) until = C->expect_until;
+      C->cv_disp.wait_until(lk, until);
     }
     if (C->stop) return;
     L.state = SEALED;  // no more reservations; new callers open the next lane
@@ -331,6 +345,8 @@ static void completer_main(Coalescer* C) {
     C->ewma_us = C->ewma_us > 0 ? 0.8 * C->ewma_us + 0.2 * us : us;
     C->t_device += us;
     C->nrunning--;
+    C->expect += (uint32_t)L.reqs.size();  // this launch's callers will be back with their next jobs
+    C->expect_until = clk::now() + std::chrono::microseconds(kRejoinUs);
     C->cv_disp.notify_one();  // a gathering lane may close now
     finish_lane(C, L, s == hipSuccess ? JX_OK : JX_E_HIP,
                 s == hipSuccess ? std::string() : std::string("coalesced launch: ") + hipGetErrorString(s));
@@ -463,6 +479,7 @@ static Lane* reserve(Coalescer* C, std::unique_lock<std::mutex>& lk, CReq* r, in
         r->first = L.reports;
         L.reports += r->n;
         L.last_arrival = clk::now();
+        if (C->expect) C->expect--;
         L.reqs.push_back(r);
         L.copying++;
         C->cv_disp.notify_one();

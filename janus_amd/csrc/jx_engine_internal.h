@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -113,33 +114,42 @@ enum : uint32_t {
 
 struct Coalescer;  // jx_coalesce.cpp
 
-// The engine mutex, handed over in arrival order: an engine serves many host threads (one per job in
-// flight), and with std::mutex a thread could wait behind a stream of others (measured: 2 s tail latency at
-// 64 threads). Each waiter sleeps on its own condition variable; unlock wakes only the next one.
+// The engine mutex, bounded-fair: an engine serves many host threads (one per job in flight). With
+// std::mutex a thread could wait behind a stream of others (measured: 2 s tail latency at 64 threads); handing
+// the lock over in strict arrival order instead makes every contended acquisition wait for the next waiter's
+// wake-up (a convoy: three acquisitions per coalesced job). So a running thread may take a free lock unless the
+// oldest waiter has waited kBargeUs; waiters queue in arrival order, each on its own condition variable, and
+// unlock wakes only the oldest.
 class FairMutex {
  public:
   void lock() {
     std::unique_lock<std::mutex> l(m_);
-    if (!locked_ && q_.empty()) {
+    if (!locked_ && (q_.empty() || std::chrono::steady_clock::now() < q_.front()->since + kBarge)) {
       locked_ = true;
       return;
     }
-    std::condition_variable cv;
-    q_.push_back(&cv);
-    cv.wait(l, [&] { return !locked_ && q_.front() == &cv; });
+    Waiter w;
+    w.since = std::chrono::steady_clock::now();
+    q_.push_back(&w);
+    w.cv.wait(l, [&] { return !locked_ && q_.front() == &w; });
     q_.pop_front();
     locked_ = true;
   }
   void unlock() {
     std::lock_guard<std::mutex> l(m_);
     locked_ = false;
-    if (!q_.empty()) q_.front()->notify_one();
+    if (!q_.empty()) q_.front()->cv.notify_one();
   }
 
  private:
+  static constexpr std::chrono::microseconds kBarge{1000};
+  struct Waiter {
+    std::condition_variable cv;
+    std::chrono::steady_clock::time_point since;
+  };
   std::mutex m_;
   bool locked_ = false;
-  std::deque<std::condition_variable*> q_;
+  std::deque<Waiter*> q_;
 };
 
 }  // namespace jxi

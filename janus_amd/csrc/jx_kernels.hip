@@ -854,10 +854,6 @@ __device__ __forceinline__ uint32_t lower_to_upper(uint32_t v) {
 // (chain-latency-bound waves, at most two per SIMD).
 template <bool WIDE>  // WIDE (bits > 32) carries 4 more truncation words
 __global__ __launch_bounds__(64 * K1_WAVES, 2) void xof_lanes_kernel(Cfg c, Bufs b) {
-  // Issue priority over co-resident waves of other kernels: this kernel runs the helper's chain-latency-bound
-  // launches, which in the two-jobs shape share SIMDs with the leader's K1 waves; the helper's chain is the
-  // step's critical path (the leader's init has slack), so its waves take the issue slots first.
-  __builtin_amdgcn_s_setprio(2);
   const uint32_t lane = threadIdx.x & 63;
   const bool jh = lane >= 32;
   const uint64_t gw = (uint64_t)blockIdx.x * K1_WAVES + (threadIdx.x >> 6);  // 32 reports per wave
@@ -3058,12 +3054,8 @@ hipError_t launch_xof_slow(const Cfg& c, const Bufs& b, hipStream_t s) {
 // Slots per FLP group. Each slot holds two 9-column wide accumulators (36 VGPRs); PPW = 2
 // (152 VGPRs, 3 waves/SIMD) measured fastest on MI355X for SumVec(8x1000/88): K3 11.8 ms vs
 // 13.6 (PPW 1) and 12.5 (PPW 4, spills) per 312,500 reports. PPW = 1 only when it wastes
-// fewer padded slot-lanes (chunk_length 1). JX_PPW overrides (4/8 spill; experiments only).
+// fewer padded slot-lanes (chunk_length 1). (4 and 8 slots per wave spill, 0.3-4 KB/lane: removed.)
 int psum_ppw(uint32_t chunk) {
-  if (const char* env = getenv("JX_PPW")) {
-    int v = atoi(env);
-    if (v == 2 || v == 1) return v;  // (4 and 8 slots per wave spill: 0.3-4 KB/lane, removed)
-  }
   const int cands[] = {2, 1};
   int best = 2, best_cost = 1 << 30;
   for (int p : cands) {

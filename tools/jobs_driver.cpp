@@ -29,7 +29,7 @@ static void die(const char* what, int32_t st, const jx_engine* e) {
 }
 
 int main(int argc, char** argv) {
-  if (argc != 15) {
+  if (argc < 15) {
     fprintf(stderr, "usage: jobs_driver IN OUT algo bits length chunk proofs vk_hex n threads seconds coalesce window_us warmup\n");
     return 2;
   }
@@ -48,6 +48,7 @@ int main(int argc, char** argv) {
   const int coalesce = atoi(argv[12]);
   const uint32_t window = (uint32_t)atoi(argv[13]);
   const int warm = atoi(argv[14]);
+  const bool no_acc = argc > 15 && atoi(argv[15]) == 0;  // measurement: prepare only, batches released unaccumulated
 
   FILE* f = fopen(in_path, "rb");
   if (!f) return 3;
@@ -113,7 +114,7 @@ int main(int argc, char** argv) {
           int32_t s = jx_helper_prep_batch(e, n, jb.non.data(), PS ? jb.ps.data() : nullptr, jb.his.data(), jb.lps.data(),
                                            PM ? m.data() : nullptr, v.data(), nullptr, &bid);
           const auto b = clk::now();
-          if (s == 0) s = jx_accumulate(e, bid, n, nullptr, nullptr);
+          if (s == 0) s = no_acc ? jx_batch_release(e, bid) : jx_accumulate(e, bid, n, nullptr, nullptr);
           const auto c = clk::now();
           if (s) {
             errs[t] = std::string(jx_status_str(s)) + " " + jx_last_error(e);
