@@ -335,7 +335,8 @@ int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]);
  *   option 2: accumulate report chunks, 1..4096 (frees the staging);
  *   option 3: helper K1 kernel: 0 automatic (the fused two-sponge kernel; the lane-split kernel for
  *             launches under one fused wave per SIMD; the lane-pair kernel under one lane-split wave
- *             per SIMD), 3 lane-split, 5 fused, 6 lane pairs (bits <= 32).
+ *             per SIMD; a word per lane up to one report-wave per SIMD), 3 lane-split, 5 fused,
+ *             6 lane pairs, 7 a word per lane (6 and 7: bits <= 32).
  *   option 4: pipelines of jx_helper_prep_aggregate_device / jx_helper_prep_aggregate: 0 automatic
  *             (when a call of one segment spans two or more launches: 2 for the device form, 3 for the
  *             host form), 1 one stream, 2..4 that many (each with its own stream and staging; the

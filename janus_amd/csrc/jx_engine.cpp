@@ -627,12 +627,15 @@ int32_t jxi::prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const ui
   b.k1_lds = lanes_lds_bytes(e->lanes_wg_cap);
   // A helper launch that would give the fused two-sponge K1 less than one wave per SIMD is bound by
   // the per-report sponge latency, not by issue: the lane-split kernel runs it in twice the waves
-  // (FixedPointBoundedL2VecSum 16 x 10000, 24,576 reports: 153 -> 92 ms on MI355X), and below one
-  // lane-split wave per SIMD the lane-pair kernel splits every sponge over two lanes (round_reports:
-  // the fused kernel's two waves per SIMD, 4 x that many lane-split or 8 x lane-pair lanes).
+  // (FixedPointBoundedL2VecSum 16 x 10000, 24,576 reports: 153 -> 92 ms on MI355X), below one
+  // lane-split wave per SIMD the lane-pair kernel splits every sponge over two lanes, and up to one
+  // report-wave per SIMD the word-per-lane kernel spreads it over 25 (round_reports: the fused kernel's
+  // two waves per SIMD, 4 x that many lane-split or 8 x lane-pair lanes; profiles/r05_words_sweep.jsonl).
   const bool wide = c.bits > 32 && (c.algo == ALGO_SUM || c.algo == ALGO_SUMVEC);
   if (e->k1_split == 0 && !leader && !wide && e->round_reports) {
-    if (4 * n <= e->round_reports)
+    if (128 * n <= e->round_reports)  // a report per wave, <= one wave per SIMD (1,024 on MI355X): 2.9 vs 4.0 ms
+      b.k1_split = 7;
+    else if (4 * n <= e->round_reports)
       b.k1_split = 6;
     else if (2 * n <= e->round_reports)
       b.k1_split = 3;
@@ -693,7 +696,10 @@ static int32_t accumulate_one(jx_engine* e, const AccSrc& src, const uint8_t* d_
   a.count = t.count;
   hipEvent_t ev = nullptr;
   HIPCHK(e, stage_begin(e, &ev));
-  HIPCHK(e, launch_accumulate(c, a, t.agg, e->stream));
+  if (src.n <= ACC_SMALL)
+    HIPCHK(e, launch_accumulate_small(c, a, t.agg, e->stream));
+  else
+    HIPCHK(e, launch_accumulate(c, a, t.agg, e->stream));
   HIPCHK(e, stage_end(e, ST_ACC, ev));
   return JX_OK;
 }
@@ -1462,7 +1468,8 @@ int32_t jx_accumulate(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t
   auto run = [&]() -> int32_t {
     if (n == 0) return JX_OK;
     Stage st;
-    int32_t r = stage_acquire(e, n, SG_ACC, st);  // mask / index scratch and the accumulate partials
+    // mask / index scratch and the accumulate partials (a small unmasked batch needs neither)
+    int32_t r = accept_mask || segment || n > ACC_SMALL ? stage_acquire(e, n, SG_ACC, st) : JX_OK;
     if (r) return r;
     std::vector<uint32_t> ids{0};
     std::vector<std::pair<const void*, size_t>> src;
@@ -1974,9 +1981,10 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
     return JX_OK;
   }
   if (option == 3) {  // helper K1 kernel
-    if (value != 0 && value != 3 && value != 5 && value != 6) return JX_E_INVALID;
+    if (value != 0 && value != 3 && value != 5 && value != 6 && value != 7) return JX_E_INVALID;
     // 0: automatic (fused; lane-split below one fused wave per SIMD, lane pairs below one lane-split
-    // wave per SIMD), 3: lane-split, 5: fused, 6: lane pairs (bits <= 32)
+    // wave per SIMD, a word per lane for the smallest launches), 3: lane-split, 5: fused, 6: lane pairs,
+    // 7: a word per lane (6, 7: bits <= 32)
     e->k1_split = (uint32_t)value;
     return JX_OK;
   }

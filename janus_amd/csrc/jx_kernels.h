@@ -185,6 +185,9 @@ hipError_t launch_leader_finish(const Cfg& c, const Bufs& b, const uint8_t* prep
                                 hipStream_t s);
 hipError_t launch_flp(const Cfg& c, const Bufs& b, hipStream_t s);
 hipError_t launch_accumulate(const Cfg& c, const AccArgs& a, uint4* agg, hipStream_t s);
+// Accumulations of at most ACC_SMALL reports: one kernel, no partials or selection scratch (a.partials unused).
+constexpr uint64_t ACC_SMALL = 1024;
+hipError_t launch_accumulate_small(const Cfg& c, const AccArgs& a, uint4* agg, hipStream_t s);
 hipError_t launch_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, uint32_t* err,
                           hipStream_t s);
 // ns records of contiguous segment state (agg [ns][out_len], count [ns], checksum [ns][8])

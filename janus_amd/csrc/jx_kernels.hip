@@ -1453,6 +1453,260 @@ __global__ __launch_bounds__(64 * K1_WAVES, 2) void xof_pairs_kernel(Cfg c, Bufs
   }
 }
 
+// ---------------------------------------------------------------------------- K1, small helper launches
+// A launch of a thousand reports or fewer (Janus's 10-1,000-report aggregation jobs, one at a time or a few
+// coalesced) leaves most SIMDs empty, so K1's time is ONE report's chain: 762 squeeze + 763 absorb blocks for
+// SumVec 8x1000, each a Keccak-p[1600,12]. The lane-pair kernel runs that chain at 124 dependent VALU per
+// round per lane (4.0 ms per launch, profiles/r05_small_launch_kernels.json). This kernel spreads each
+// sponge over 25 lanes, one 64-bit word per lane (lane = x + 5y), one report per wave: lanes 0..24 squeeze
+// the measurement share (S), lanes 32..56 absorb the joint_rand_part (J). A round is 26 VALU per lane and
+// two exchanges through the wave's own LDS region (no barrier: a wave's LDS operations complete in order):
+//   theta: every lane writes its word into a column-major table whose columns are padded with wrap copies
+//          (slot c + 1 holds column c, slot 0 column 4, slot 6 column 0), then reads columns x - 1 and
+//          x + 1 as five ds_read2_b64 at offsets (k, k + 10) from one base;
+//   rho:   a per-lane rotation, two v_alignbit_b32 on operands ordered once per lane;
+//   pi + chi: every lane writes its rotated word at its pi destination into a row-major table with rows
+//          padded by wrap copies (slots 5, 6 = 0, 1), then reads B[x], B[x+1], B[x+2] of its row.
+// Measured (tools/kernel_probe sweep, profiles/r05_words_sweep.jsonl): 2.7-2.9 ms per launch up to 1,024
+// reports against 4.0 ms for the lane pairs; equal at 2,048; beyond, issue-bound and slower. One exchange
+// per round instead (each lane reading columns x - 1 .. x + 3 of the chi table and computing the next
+// round's parities itself, 54 VALU per round) measured 3.5-3.8 ms: a lone wave pays more for the doubled
+// VALU chain than for the second LDS round trip.
+// S hands each squeezed block to J through a 27-word message window in LDS (the previous block's words
+// 15..20, then the block), from which J lane w forms its message word w as one 48-bit funnel shift; the
+// 42-byte header sits in the window's prefix for block 0. The output-share truncation runs afterwards in
+// trunc_kernel (it needs `bits` consecutive elements that lie on different lanes here).
+constexpr uint32_t KW_WAVES = 4;  // waves (reports) per workgroup
+// per-wave LDS region, in 8-byte words: theta tables S / J, chi tables S / J, message window, init block, sink
+constexpr uint32_t KW_AS = 0, KW_AJ = 35, KW_BS = 70, KW_BJ = 105, KW_MSG = 140, KW_INIT = 167, KW_SINK = 188,
+                   KW_WORDS = 189;
+__constant__ uint8_t kw_rot_tab[25] = {JX_ROT_LIST};
+
+struct KwLane {
+  uint32_t aw1, aw2, ab;  // theta: write (own slot, wrap copy), read base (column x - 1)
+  uint32_t bw1, bw2, bb;  // chi: write (pi destination, wrap copy), read base (B[x] of the lane's row)
+  uint32_t pm, s;         // rho: operand order mask, v_alignbit amount
+  uint32_t m0;            // iota: all-ones on word 0
+};
+
+__device__ __forceinline__ void kw_round(uint2* L, const KwLane& k, uint32_t& lo, uint32_t& hi, uint32_t rlo,
+                                         uint32_t rhi) {
+  L[k.aw1] = make_uint2(lo, hi);
+  L[k.aw2] = make_uint2(lo, hi);
+  uint2 cm[5], cp[5];
+#pragma unroll
+  for (int j = 0; j < 5; j++) {
+    cm[j] = L[k.ab + j];
+    cp[j] = L[k.ab + j + 10];
+  }
+  const uint32_t cml = xor3(xor3(cm[0].x, cm[1].x, cm[2].x), cm[3].x, cm[4].x);
+  const uint32_t cmh = xor3(xor3(cm[0].y, cm[1].y, cm[2].y), cm[3].y, cm[4].y);
+  const uint32_t cpl = xor3(xor3(cp[0].x, cp[1].x, cp[2].x), cp[3].x, cp[4].x);
+  const uint32_t cph = xor3(xor3(cp[0].y, cp[1].y, cp[2].y), cp[3].y, cp[4].y);
+  // D[x] = C[x - 1] ^ rotl64(C[x + 1], 1)
+  lo = xor3(lo, cml, alignbit(cpl, cph, 31));
+  hi = xor3(hi, cmh, alignbit(cph, cpl, 31));
+  // rho: (P, Q) = the halves in the order this lane's rotation needs (see xof_words_kernel)
+  const uint32_t P = msel(k.pm, hi, lo);
+  const uint32_t Q = xor3(lo, hi, P);
+  const uint32_t nh = alignbit(P, Q, k.s), nl = alignbit(Q, P, k.s);
+  L[k.bw1] = make_uint2(nl, nh);
+  L[k.bw2] = make_uint2(nl, nh);
+  const uint2 b0 = L[k.bb], b1 = L[k.bb + 1], b2 = L[k.bb + 2];
+  lo = (b0.x ^ (~b1.x & b2.x)) ^ (rlo & k.m0);
+  hi = (b0.y ^ (~b1.y & b2.y)) ^ (rhi & k.m0);
+}
+__device__ __forceinline__ void kw_p12(uint2* L, const KwLane& k, uint32_t& lo, uint32_t& hi) {
+#pragma unroll 1
+  for (int ir = 12; ir < 24; ir++) kw_round(L, k, lo, hi, KECCAK_RC_LO[ir], KECCAK_RC_HI[ir]);
+}
+
+__global__ __launch_bounds__(64 * KW_WAVES) void xof_words_kernel(Cfg c, Bufs b) {
+  __shared__ uint2 lds[KW_WAVES][KW_WORDS];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t r = (uint64_t)blockIdx.x * KW_WAVES + wv;
+  if (r >= b.n) return;
+  uint2* L = lds[wv];
+  const uint64_t blk = r >> 6;
+  const uint32_t il = (uint32_t)r & 63u;
+  const bool jg = lane >= 32;         // J lanes
+  const uint32_t i = lane & 31u;      // this lane's word of its sponge
+  const bool act = i < 25;
+  const bool sw21 = !jg && i < 21;    // S lanes holding a rate word
+  const bool jw21 = jg && i < 21;     // J lanes absorbing a message word
+  const uint32_t ia = act ? i : 0u, x = ia % 5u, y = ia / 5u;
+  KwLane k;
+  {
+    const uint32_t A0 = jg ? KW_AJ : KW_AS, B0 = jg ? KW_BJ : KW_BS;
+    const uint32_t xp = y, yp = (2u * x + 3u * y) % 5u;  // pi destination (column, row)
+    k.aw1 = act ? A0 + (x + 1u) * 5u + y : KW_SINK;
+    k.aw2 = !act ? KW_SINK : x == 4u ? A0 + y : x == 0u ? A0 + 30u + y : k.aw1;
+    k.ab = A0 + x * 5u;
+    k.bw1 = act ? B0 + yp * 7u + xp : KW_SINK;
+    k.bw2 = !act ? KW_SINK : xp < 2u ? k.bw1 + 5u : k.bw1;
+    k.bb = B0 + y * 7u + x;
+    // rotl64 by R: with sw = R >= 32 and M = R mod 32, new hi = alignbit(P, Q, (32 - M) mod 32) and new lo =
+    // alignbit(Q, P, ...), where P is the low half iff sw != (M == 0) (alignbit by 0 returns its second operand)
+    const uint32_t R = kw_rot_tab[ia], M = R & 31u;
+    k.pm = ((R >= 32u) != (M == 0u)) ? 0xFFFFFFFFu : 0u;
+    k.s = (32u - M) & 31u;
+    k.m0 = act && ia == 0u ? 0xFFFFFFFFu : 0u;
+  }
+  const uint8_t* hs = b.his + (uint64_t)c.his_bytes * r;
+  const uint32_t MB = c.meas_len * 16;
+  const uint32_t ML = 42 + MB;
+  const uint32_t NM = (MB + 167) / 168;
+  const uint32_t b_last = ML / 168;
+  uint32_t lo = 0, hi = 0, gmax = 0;
+
+  // S := the permuted one-block sponge of `m` (block word i on S lane i); J keeps its state
+  auto s_init = [&](const Block& m) {
+    if (lane == 0) {
+#pragma unroll
+      for (int w = 0; w < 21; w++) L[KW_INIT + w] = make_uint2(m.w[2 * w], m.w[2 * w + 1]);
+    }
+    const uint2 v = L[KW_INIT + (i < 21u ? i : 0u)];
+    const uint32_t jlo = lo, jhi = hi;
+    lo = sw21 ? v.x : 0u;
+    hi = sw21 ? v.y : 0u;
+    kw_p12(L, k, lo, hi);
+    if (jg) {
+      lo = jlo;
+      hi = jhi;
+    }
+  };
+  // S lanes: block m's word i is stream word q = 21 m + i, half q & 1 of element q >> 1
+  auto s_emit = [&](uint4* base, uint32_t len, uint32_t m) {
+    if (sw21) {
+      const uint32_t q = 21u * m + i, e = q >> 1;
+      if (e < len) {
+        reinterpret_cast<uint2*>(base + il_idx(blk, len, e, il))[q & 1u] = make_uint2(lo, hi);
+        if (q & 1u) gmax = max(gmax, hi & (lo | 0x1Fu));  // ge_screen on the element's (z, w)
+      }
+    }
+  };
+  // J lanes: message word w of a block = stream bytes [8 w - 42, 8 w - 34) relative to the block = window
+  // words (w, w + 1) shifted by 48 bits; the last absorbed block keeps bytes [0, nb) and takes the padding
+  auto j_absorb = [&](bool last, uint32_t nb) {
+    if (jw21) {
+      const uint2 v0 = L[KW_MSG + i], v1 = L[KW_MSG + i + 1];
+      uint32_t wd[2] = {alignbit(v1.x, v0.y, 16), alignbit(v1.y, v1.x, 16)};
+      if (last) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const uint32_t d = 2u * i + (uint32_t)h, lb = 4u * d;
+          if (lb >= nb)
+            wd[h] = 0;
+          else if (lb + 4u > nb)
+            wd[h] &= (1u << (8u * (nb - lb))) - 1u;
+          if (d == (nb >> 2)) wd[h] ^= 1u << (8u * (nb & 3u));
+          if (d == 41u) wd[h] ^= 0x80000000u;
+        }
+      }
+      lo ^= wd[0];
+      hi ^= wd[1];
+    }
+  };
+
+  {  // S: XOF(k_meas, DST(1), [1]) -> measurement-share block 0
+    uint32_t kmeas[4];
+    load16(hs, kmeas);
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.dst_id, 1, kmeas);
+    blk_put_byte(m, pos, 1);
+    blk_pad(m, pos + 1);
+    s_init(m);
+  }
+  {  // the window's prefix: J's 42-byte header [agg_id || nonce after the XOF prefix] at stream bytes [-42, 0)
+    uint32_t nonce[4], kblind[4];
+    load16(b.nonces + 16 * r, nonce);
+    load16(hs + 32, kblind);
+    Block h;
+    blk_zero(h);
+    int pos = blk_xof_prefix(h, c.dst_id, 7, kblind);
+    blk_put_byte(h, pos, 1);  // agg_id
+#pragma unroll
+    for (int q = 0; q < 4; q++) blk_put_word(h, pos + 1 + 4 * q, nonce[q]);
+    if (lane == 0) {
+      // window word t covers stream bytes [8 t - 48, 8 t - 40): header bytes 8 t - 6 ..
+      L[KW_MSG + 0] = make_uint2(0u, h.w[0] << 16);
+#pragma unroll
+      for (int t = 1; t < 6; t++)
+        L[KW_MSG + t] = make_uint2(alignbit(h.w[2 * t - 1], h.w[2 * t - 2], 16), alignbit(h.w[2 * t], h.w[2 * t - 1], 16));
+    }
+  }
+  s_emit(b.meas, c.meas_len, 0);
+  if (sw21) L[KW_MSG + 6 + i] = make_uint2(lo, hi);
+  j_absorb(b_last == 0, ML);  // J's state is zero: absorbing block 0 sets it
+  if (sw21 && i >= 15u) L[KW_MSG + i - 15u] = make_uint2(lo, hi);
+#pragma unroll 1
+  for (uint32_t m = 1; m <= b_last; m++) {
+    kw_p12(L, k, lo, hi);  // S: squeeze block m; J: absorb block m - 1
+    if (m < NM) s_emit(b.meas, c.meas_len, m);
+    if (sw21) L[KW_MSG + 6 + i] = make_uint2(lo, hi);
+    j_absorb(m == b_last, ML - 168u * m);
+    if (sw21 && i >= 15u) L[KW_MSG + i - 15u] = make_uint2(lo, hi);
+  }
+  kw_p12(L, k, lo, hi);  // J: absorb block b_last
+  // J's joint_rand_part = its state words 0, 1 (lanes 32, 33)
+  uint32_t own_part[4] = {(uint32_t)__builtin_amdgcn_readlane((int)lo, 32), (uint32_t)__builtin_amdgcn_readlane((int)hi, 32),
+                          (uint32_t)__builtin_amdgcn_readlane((int)lo, 33), (uint32_t)__builtin_amdgcn_readlane((int)hi, 33)};
+  {  // proof share: XOF(k_proofs, DST(2), [PROOFS=1, agg_id=1])
+    uint32_t kproof[4];
+    load16(hs + 16, kproof);
+    Block m;
+    blk_zero(m);
+    int pos = blk_xof_prefix(m, c.dst_id, 2, kproof);
+    blk_put_byte(m, pos, 1);
+    blk_put_byte(m, pos + 1, 1);
+    blk_pad(m, pos + 2);
+    s_init(m);
+  }
+  const uint32_t NP = (c.proof_len * 16 + 167) / 168;
+  s_emit(b.proof, c.proof_len, 0);
+#pragma unroll 1
+  for (uint32_t m = 1; m < NP; m++) {
+    kw_p12(L, k, lo, hi);
+    s_emit(b.proof, c.proof_len, m);
+  }
+  const bool slow = __ballot(gmax == 0xFFFFFFFFu) != 0;
+  if (lane == 0) {
+    uint32_t flags = slow ? FLAG_SLOW : 0u;
+    uint32_t nonce[4], part_l[4], lead_part[4];
+    load16(b.nonces + 16 * r, nonce);
+    load16(b.ps + (uint64_t)c.ps_bytes * r, part_l);
+    load16(b.lps + (uint64_t)c.lps_bytes * r + c.lps_bytes - 16, lead_part);
+    flags = xof_tail(c, b, blk, il, r, true, nonce, part_l, lead_part, own_part, flags, false);
+    if (b.force_slow) flags |= FLAG_SLOW;
+    b.flags[r] = flags;
+  }
+}
+
+// The output-share truncation of the small-launch kernel, one thread per (report, output element), the
+// report fastest within its 64-report block: out_i = sum_{j < bits} 2^j x_{bits i + j} mod p over the staged
+// measurement share (the same word-column sums as emit_meas). Reports the slow kernel redoes get their
+// output share rewritten there.
+__global__ __launch_bounds__(256) void trunc_kernel(Cfg c, Bufs b, uint32_t nout) {
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t il = (uint32_t)(t & 63u);
+  const uint64_t gi = t >> 6;
+  const uint32_t i = (uint32_t)(gi % nout);
+  const uint64_t blk = gi / nout;
+  const uint64_t r = blk * 64 + il;
+  if (r >= b.n) return;
+  TruncW tr;
+  truncw_zero(tr);
+  for (uint32_t j = 0; j < c.bits; j++) {
+    const uint4 v = b.meas[il_idx(blk, c.meas_len, i * c.bits + j, il)];
+    tr.T[0] += (uint64_t)v.x << j;
+    tr.T[1] += (uint64_t)v.y << j;
+    tr.T[2] += (uint64_t)v.z << j;
+    tr.T[3] += (uint64_t)v.w << j;
+  }
+  b.outs[il_idx(blk, c.out_len, i, il)] = f_to_u4(truncw_value(tr));
+}
+
 // ---------------------------------------------------------------------------- K1, leader role
 // leader_initialized (aggregation_job_driver.rs:345): prepare_init with agg_id 0 on the explicit leader
 // input share [meas || proofs || k_blind], one report per lane. Only the joint_rand_part absorb runs
@@ -2616,6 +2870,83 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(Cfg c, const uint6
   }
 }
 
+// K4 for a small batch (<= ACC_SMALL reports, e.g. one Janus aggregation job): one kernel instead of select +
+// accumulate + reduce_partials, nothing staged. Wave w of the grid sums output element w over the selected
+// reports and adds it into the aggregation; every thread also folds a grid-stride share of the selected
+// reports' SHA-256(id) and count, reduced per workgroup into one set of atomics (as select_kernel).
+__device__ __forceinline__ bool acc_selected(const AccArgs& a, uint64_t r) {
+  return a.verdicts[r] == 0 && (!a.mask || a.mask[r]) && (!a.seg || a.seg[r] == a.seg_id);
+}
+__global__ __launch_bounds__(256) void accumulate_small_kernel(Cfg c, AccArgs a, uint4* agg) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i < a.out_len) {
+    acc192 acc;
+    acc_zero(acc);
+    const uint64_t nblk = (a.n + 63) / 64;
+    for (uint64_t bk = 0; bk < nblk; bk++) {
+      const uint64_t r = bk * 64 + lane;
+      if (r < a.n && acc_selected(a, r)) acc_add128(acc, u4_to_f(a.outs[il_idx(bk, a.out_len, i, lane)]));
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      uint64_t o0 = ((uint64_t)__shfl_xor((uint32_t)(acc.w0 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w0, off);
+      uint64_t o1 = ((uint64_t)__shfl_xor((uint32_t)(acc.w1 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w1, off);
+      uint64_t o2 = ((uint64_t)__shfl_xor((uint32_t)(acc.w2 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w2, off);
+      uint32_t cc = 0;
+      acc.w0 = addc64(acc.w0, o0, cc);
+      acc.w1 = addc64(acc.w1, o1, cc);
+      acc.w2 = acc.w2 + o2 + cc;
+    }
+    if (lane == 0) {
+      acc_add128(acc, u4_to_f(agg[i]));
+      if (c.fb == 8) {
+        const uint64_t v = reduce192_p64(acc.w0, acc.w1, acc.w2);
+        agg[i] = make_uint4(lo32(v), hi32(v), 0, 0);
+      } else {
+        agg[i] = f_to_u4(acc_reduce(acc));
+      }
+    }
+  }
+  uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t cnt = 0;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += (uint64_t)gridDim.x * blockDim.x) {
+    if (acc_selected(a, r)) {
+      uint32_t id[4], h[8];
+      load16(a.nonces + 16 * r, id);
+      sha256_16(id, h);
+#pragma unroll
+      for (int k = 0; k < 8; k++) d[k] ^= h[k];
+      cnt++;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    uint32_t v = d[k];
+    for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off);
+    d[k] = v;
+  }
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  __shared__ uint32_t red[4][9];
+  const uint32_t w = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) red[w][k] = d[k];
+    red[w][8] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x < 9) {
+    const uint32_t k = threadIdx.x;
+    uint32_t v = 0;
+    for (uint32_t q = 0; q < 4; q++) v = k < 8 ? (v ^ red[q][k]) : (v + red[q][k]);
+    if (v) {
+      if (k < 8)
+        atomicXor(&a.checksum[k], v);
+      else
+        atomicAdd(a.count, (unsigned long long)v);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------- K4 segmented
 // One pass for any number of batch aggregations: a device counting sort of the selected reports by
 // segment (LDS histograms, one global atomic per (workgroup, segment)), work items of <= L sorted
@@ -2994,7 +3325,14 @@ hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
     hipLaunchKernelGGL((xof_leader_kernel<false, true>), grid, block, 0, s, c, b);
   else if (b.leader)
     hipLaunchKernelGGL((xof_leader_kernel<false, false>), grid, block, 0, s, c, b);
-  else if (b.k1_split == 6 && !wide)  // lane pairs: 16 reports per wave
+  else if (b.k1_split == 7 && !wide) {  // a word per lane: one report per wave, then the truncation
+    hipLaunchKernelGGL(xof_words_kernel, dim3((uint32_t)((b.n + KW_WAVES - 1) / KW_WAVES)), dim3(64 * KW_WAVES), 0, s, c, b);
+    const uint32_t nout = c.out_is_meas ? 0u : (c.trunc_len < c.meas_len ? c.trunc_len : c.meas_len) / c.bits;
+    if (nout) {
+      const uint64_t threads = (uint64_t)nblk_of(b.n) * 64 * nout;
+      hipLaunchKernelGGL(trunc_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, c, b, nout);
+    }
+  } else if (b.k1_split == 6 && !wide)  // lane pairs: 16 reports per wave
     hipLaunchKernelGGL(xof_pairs_kernel, dim3((4 * nb + K1_WAVES - 1) / K1_WAVES), block, 0, s, c, b);
   else if (b.k1_split == 3) {  // lane-split: 32 reports per wave
     const dim3 g2((2 * nb + K1_WAVES - 1) / K1_WAVES);
@@ -3157,6 +3495,11 @@ hipError_t launch_accumulate(const Cfg& c, const AccArgs& a, uint4* agg, hipStre
                      (const uint8_t*)sel);
   hipLaunchKernelGGL(reduce_partials_kernel, dim3((c.out_len + 3) / 4), dim3(256), 0, s, c,
                      (const uint64_t*)a.partials, a.nchunks, agg);
+  return hipGetLastError();
+}
+
+hipError_t launch_accumulate_small(const Cfg& c, const AccArgs& a, uint4* agg, hipStream_t s) {
+  hipLaunchKernelGGL(accumulate_small_kernel, dim3((c.out_len + 3) / 4), dim3(256), 0, s, c, a, agg);
   return hipGetLastError();
 }
 

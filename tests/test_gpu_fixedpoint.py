@@ -171,8 +171,8 @@ def test_reference_e2e_result(bits):
     assert vdaf.decode_fixedpoint_result(total, 4) == [0.5, 0.5, 0.6875]
 
 
-@pytest.mark.parametrize("split,padded", [(0, False), (3, False), (6, False), (5, False), (0, True)],
-                         ids=["auto", "lanes", "pairs", "fused", "auto-padded-rows"])
+@pytest.mark.parametrize("split,padded", [(0, False), (3, False), (6, False), (7, False), (5, False), (0, True)],
+                         ids=["auto", "lanes", "pairs", "words", "fused", "auto-padded-rows"])
 def test_two_jobs_in_flight(split, padded):
     """configs[4]'s bench shape (tools/bench_fixedpoint.py, two jobs in flight): while the helper engine
     prepares job i-1 on its stream, the leader engine initializes job i on its own; then the leader

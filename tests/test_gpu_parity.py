@@ -262,15 +262,17 @@ def test_shard_records_device_merge(name):
         e.close()
 
 
-@pytest.mark.parametrize("split", [3, 5, 6], ids=["lanes", "fused", "pairs"])
+@pytest.mark.parametrize("split", [3, 5, 6, 7], ids=["lanes", "fused", "pairs", "words"])
 @pytest.mark.parametrize("name", ["sumvec_8x1000_88", "histogram_256_16", "sum64", "sumvec_small", "sumvec_64x20_9",
                                   "sum5", "sum32"])
 def test_k1_split_variants(name, split):
-    """The three helper K1 kernels == the oracle, fast and slow path: the lane-pair kernel (every sponge
-    split over two lanes; the engine's choice below one lane-split wave per SIMD, i.e. every small test
-    batch), the lane-split kernel (S and J sponges in the two halves of a wave) and the fused two-sponge
-    kernel (the engine's choice for large launches). sum5 has its whole joint_rand_part message in one
-    block; sum64 and sumvec_64x20_9 (bits > 32) run the fused kernel when pairs are asked for."""
+    """The four helper K1 kernels == the oracle, fast and slow path: the word-per-lane kernel (each sponge
+    over 25 lanes, a report per wave, the truncation in its own kernel; the engine's choice up to one
+    report-wave per SIMD, i.e. every small test batch), the lane-pair kernel (every sponge split over two
+    lanes), the lane-split kernel (S and J sponges in the two halves of a wave) and the fused two-sponge
+    kernel (the engine's choice for large launches). n = 150 spans three 64-report blocks and a partial
+    workgroup. sum5 has its whole joint_rand_part message in one block; sum64 and sumvec_64x20_9
+    (bits > 32) run the fused kernel when pairs or words are asked for."""
     vdaf = CASES[name]
     vk = bytes(range(60, 76))
     orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)

@@ -11,8 +11,11 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/kernel_probe.hip -Iinclude -Ljanus_amd/lib -ljanus_prio3 \
 //         -Wl,-rpath,'$ORIGIN/../../janus_amd/lib' -o tools/bin/kernel_probe
 //   tools/bin/kernel_probe [reports=262144] [launches=5]
+//   tools/bin/kernel_probe sweep   (small launches: the lane-pair K1 against the word-per-lane K1 + its
+//                                   truncation kernel, ms per launch at 16 .. 32,768 reports)
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "../janus_amd/csrc/jx_engine_internal.h"
@@ -59,7 +62,47 @@ static double time_ms(F launch, int n, hipStream_t s) {
   return ms / n;
 }
 
+static int sweep() {
+  jx_prio3_params p{2, 8, 1000, 88, 1};
+  uint8_t vk[16] = {0};
+  jx_engine* e = nullptr;
+  if (jx_engine_create(&p, vk, 0, &e)) return 2;
+  const jx::Cfg c = e->cfg;
+  const uint64_t N = 32768;
+  jx::Bufs b{};
+  b.nonces = (const uint8_t*)dalloc(N * 16, 1);
+  b.ps = (const uint8_t*)dalloc(N * c.ps_bytes, 2);
+  b.his = (const uint8_t*)dalloc(N * c.his_bytes, 3);
+  b.lps = (const uint8_t*)dalloc(N * c.lps_bytes, 4);
+  b.meas = (uint4*)dalloc(N * c.meas_len * 16, 5);
+  b.proof = (uint4*)dalloc(N * c.proof_len * 16, 6);
+  b.outs = (uint4*)dalloc(N * c.out_len * 16, 7);
+  b.coef = (uint4*)dalloc(N * c.ncoef * 16, 8);
+  b.flags = (uint32_t*)dalloc(N * 4, 9);
+  b.part = (uint4*)dalloc(N * 64 * c.ngt, 10);
+  b.verdicts = (uint8_t*)dalloc(N, 11);
+  b.msgs = (uint8_t*)dalloc(N * 16, 12);
+  b.consts = e->d_consts;
+  b.lis_rs = c.lis_bytes;
+  CK(hipDeviceSynchronize());
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  const uint64_t sizes[] = {16, 100, 256, 512, 1024, 2048, 3072, 4096, 6400, 8192, 16384, 32768};
+  for (uint64_t n : sizes) {
+    b.n = n;
+    b.k1_split = 6;
+    const double pairs = time_ms([&] { CK(jx::launch_xof(c, b, s)); }, 3, s);
+    b.k1_split = 7;
+    const double words = time_ms([&] { CK(jx::launch_xof(c, b, s)); }, 3, s);
+    printf("{\"reports\": %llu, \"pairs_ms\": %.3f, \"words_ms\": %.3f}\n", (unsigned long long)n, pairs, words);
+    fflush(stdout);
+  }
+  jx_engine_destroy(e);
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "sweep") return sweep();
   const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 262144;
   const int iters = argc > 2 ? atoi(argv[2]) : 5;
   jx_prio3_params p{2, 8, 1000, 88, 1};
