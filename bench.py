@@ -751,10 +751,12 @@ def secondary_configs(cpu: dict, threads: int) -> dict:
 
 
 def job_granularity(threads: int) -> dict:
-    """The headline VDAF at Janus's aggregation-job size: 64 native threads submit 100-report
+    """The headline VDAF at Janus's aggregation-job size: native threads submit 100-report
     SumVec 8x1000/88 jobs to ONE engine through the host-buffer ABI (jx_helper_prep_batch -> jx_accumulate per
     job; tools/jobs_driver.cpp in a child process), with the device coalescer on and off; every job's verdicts
-    and prep messages and the final aggregate verified against the oracle (tools/bench_jobs.py)."""
+    and prep messages and the final aggregate verified against the oracle (tools/bench_jobs.py). Two shapes:
+    64 threads (value), and 10 = max_concurrent_job_workers of the reference's sample job driver
+    (docs/samples/basic_config/aggregation_job_driver.yaml:16)."""
     import tempfile
 
     from janus_amd.vdaf import Prio3
@@ -765,19 +767,23 @@ def job_granularity(threads: int) -> dict:
     vk = bytes(range(16))
     pool = BJ.make_pool(v, vk, 2048, threads)
     BJ.build_driver()
-    out = {}
+    keys = ("reports_per_s", "prep_ms_p50", "prep_ms_p99", "jobs", "jobs_per_launch", "device_ms", "verified", "error")
+    shapes = {}
     with tempfile.TemporaryDirectory() as tmp:
-        for mode in ("coalesce", "direct"):
-            r = BJ.run_case_cpp(v, vk, pool, 100, 64, 2.0, mode, 0, tmp)
-            out[mode] = {k: r.get(k) for k in ("reports_per_s", "prep_ms_p50", "prep_ms_p99", "jobs", "jobs_per_launch",
-                                               "device_ms", "verified", "error") if k in r}
-    ok = all(x.get("verified") for x in out.values())
+        for T in (64, 10):
+            shapes[T] = {}
+            for mode in ("coalesce", "direct"):
+                r = BJ.run_case_cpp(v, vk, pool, 100, T, 2.0, mode, 0, tmp)
+                shapes[T][mode] = {k: r.get(k) for k in keys if k in r}
+    ok = all(x.get("verified") for sh in shapes.values() for x in sh.values())
     res = {"metric": "helper reports/sec at Janus's job size: 100-report Prio3SumVec 8x1000/88 jobs from 64 threads on "
                      "one engine (prep_init+prep_next+aggregate per job)",
-           "value": out["coalesce"].get("reports_per_s"), "unit": "reports/s", "coalesced": out["coalesce"],
-           "one_call_at_a_time": out["direct"], "verified": ok,
-           "driver_seconds": round(time.perf_counter() - t, 1)}
-    log(f"jobs: coalesced {res['value']} reports/s, one call at a time {out['direct'].get('reports_per_s')}, "
+           "value": shapes[64]["coalesce"].get("reports_per_s"), "unit": "reports/s", "coalesced": shapes[64]["coalesce"],
+           "one_call_at_a_time": shapes[64]["direct"],
+           "ten_workers": {"threads": 10, "coalesced": shapes[10]["coalesce"], "one_call_at_a_time": shapes[10]["direct"]},
+           "verified": ok, "driver_seconds": round(time.perf_counter() - t, 1)}
+    log(f"jobs: 64 threads coalesced {res['value']} reports/s (one call at a time {shapes[64]['direct'].get('reports_per_s')}); "
+        f"10 threads {shapes[10]['coalesce'].get('reports_per_s')} / {shapes[10]['direct'].get('reports_per_s')}; "
         f"verified={ok} ({res['driver_seconds']} s)")
     return res
 

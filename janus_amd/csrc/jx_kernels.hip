@@ -1467,8 +1467,9 @@ __global__ __launch_bounds__(64 * K1_WAVES, 2) void xof_pairs_kernel(Cfg c, Bufs
 //   rho:   a per-lane rotation, two v_alignbit_b32 on operands ordered once per lane;
 //   pi + chi: every lane writes its rotated word at its pi destination into a row-major table with rows
 //          padded by wrap copies (slots 5, 6 = 0, 1), then reads B[x], B[x+1], B[x+2] of its row.
-// Measured (tools/kernel_probe sweep, profiles/r05_words_sweep.jsonl): 2.7-2.9 ms per launch up to 1,024
-// reports against 4.0 ms for the lane pairs; equal at 2,048; beyond, issue-bound and slower. One exchange
+// Measured (tools/kernel_probe sweep, profiles/r05_words_sweep.jsonl): 2.5-2.7 ms per launch up to 1,024
+// reports against 4.0 ms for the lane pairs (2.7-2.9 with the rounds in a loop: the unrolled rounds take
+// the round constants as literals); equal at 2,048; beyond, issue-bound and slower. One exchange
 // per round instead (each lane reading columns x - 1 .. x + 3 of the chi table and computing the next
 // round's parities itself, 54 VALU per round) measured 3.5-3.8 ms: a lone wave pays more for the doubled
 // VALU chain than for the second LDS round trip.
@@ -1517,7 +1518,7 @@ __device__ __forceinline__ void kw_round(uint2* L, const KwLane& k, uint32_t& lo
   hi = (b0.y ^ (~b1.y & b2.y)) ^ (rhi & k.m0);
 }
 __device__ __forceinline__ void kw_p12(uint2* L, const KwLane& k, uint32_t& lo, uint32_t& hi) {
-#pragma unroll 1
+#pragma unroll
   for (int ir = 12; ir < 24; ir++) kw_round(L, k, lo, hi, KECCAK_RC_LO[ir], KECCAK_RC_HI[ir]);
 }
 
