@@ -633,7 +633,7 @@ int32_t jxi::prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const ui
   // two waves per SIMD, 4 x that many lane-split or 8 x lane-pair lanes; profiles/r05_words_sweep.jsonl).
   const bool wide = c.bits > 32 && (c.algo == ALGO_SUM || c.algo == ALGO_SUMVEC);
   if (e->k1_split == 0 && !leader && !wide && e->round_reports) {
-    if (128 * n <= e->round_reports)  // a report per wave, <= one wave per SIMD (1,024 on MI355X): 2.7 vs 4.0 ms
+    if (128 * n <= e->round_reports)  // a report per wave, <= one wave per SIMD (1,024 on MI355X): 2.6 vs 3.6 ms
       b.k1_split = 7;
     else if (4 * n <= e->round_reports)
       b.k1_split = 6;

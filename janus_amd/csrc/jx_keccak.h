@@ -132,6 +132,17 @@ JX_HD void keccak_p12(uint32_t* s) {
   for (int ir = 12; ir < 24; ir++) keccak_round(s, KECCAK_RC_LO[ir], KECCAK_RC_HI[ir]);
 }
 
+// Keccak-p[1600, 12] with the rounds unrolled: the round constants become literals (no per-round scalar
+// load, no loop control). It pays in the block loops of kernels that run one wave per SIMD, where a lone
+// wave waits on each round's constant load: the word-per-lane K1 2.7-2.9 -> 2.5-2.7 ms, the lane-pair K1
+// 4.03 -> 3.59 ms (profiles/r05_words_sweep*.jsonl). In the lane-split helper and the leader K1, whose
+// configs[4] launches put two waves on some SIMDs, it measured slower (helper 152 -> 156 ms, leader 94 ->
+// 99 ms beside each other; profiles/r05_unroll_fixedpoint.json), so they keep the loop.
+JX_HD void keccak_p12_unrolled(uint32_t* s) {
+#pragma unroll
+  for (int ir = 12; ir < 24; ir++) keccak_round(s, KECCAK_RC_LO[ir], KECCAK_RC_HI[ir]);
+}
+
 // Two independent Keccak-p[1600, 12] permutations advanced round by round in one loop:
 // two independent instruction streams for the scheduler (the measurement-share squeeze and
 // the joint-randomness-part absorb of K1).

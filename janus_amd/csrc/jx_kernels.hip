@@ -1018,7 +1018,7 @@ __global__ __launch_bounds__(64 * K1_WAVES, 2) void xof_lanes_kernel(Cfg c, Bufs
   }
 #pragma unroll 1
   for (uint32_t m = 1; m <= b_last; m++) {
-    keccak_p12(st);  // S: squeeze block m; J: absorb block m - 1
+    keccak_p12(st);  // S: squeeze block m; J: absorb block m - 1 (unrolled: slower, see keccak_p12_unrolled)
     const bool have = m < NM;
     if (have) {
       if (!jh) s_emit_block(m);
@@ -1194,6 +1194,11 @@ __device__ __forceinline__ void keccak_round_half(uint32_t* s, uint32_t rc) {
 }
 __device__ __forceinline__ void keccak_p12_half(uint32_t* s, bool hi) {
 #pragma unroll 1
+  for (int ir = 12; ir < 24; ir++) keccak_round_half(s, hi ? KECCAK_RC_HI[ir] : KECCAK_RC_LO[ir]);
+}
+// the same with the rounds unrolled (round constants as literals; see keccak_p12_unrolled)
+__device__ __forceinline__ void keccak_p12_half_unrolled(uint32_t* s, bool hi) {
+#pragma unroll
   for (int ir = 12; ir < 24; ir++) keccak_round_half(s, hi ? KECCAK_RC_HI[ir] : KECCAK_RC_LO[ir]);
 }
 // a ? x1 : x0 as bit operations on an opaque all-ones / zero mask: a select between two array elements
@@ -1373,7 +1378,7 @@ __global__ __launch_bounds__(64 * K1_WAVES, 2) void xof_pairs_kernel(Cfg c, Bufs
   }
 #pragma unroll 1
   for (uint32_t m = 1; m <= b_last; m++) {
-    keccak_p12_half(h, hi);  // S: squeeze block m; J: absorb block m - 1
+    keccak_p12_half_unrolled(h, hi);  // S: squeeze block m; J: absorb block m - 1
     const bool have = m < NM;
     if (have) {
       if (!jh) s_emit_block(m);
@@ -1468,7 +1473,7 @@ __global__ __launch_bounds__(64 * K1_WAVES, 2) void xof_pairs_kernel(Cfg c, Bufs
 //   pi + chi: every lane writes its rotated word at its pi destination into a row-major table with rows
 //          padded by wrap copies (slots 5, 6 = 0, 1), then reads B[x], B[x+1], B[x+2] of its row.
 // Measured (tools/kernel_probe sweep, profiles/r05_words_sweep.jsonl): 2.5-2.7 ms per launch up to 1,024
-// reports against 4.0 ms for the lane pairs (2.7-2.9 with the rounds in a loop: the unrolled rounds take
+// reports against 3.6 ms for the lane pairs (2.7-2.9 with the rounds in a loop: the unrolled rounds take
 // the round constants as literals); equal at 2,048; beyond, issue-bound and slower. One exchange
 // per round instead (each lane reading columns x - 1 .. x + 3 of the chi table and computing the next
 // round's parities itself, 54 VALU per round) measured 3.5-3.8 ms: a lone wave pays more for the doubled
@@ -1866,7 +1871,7 @@ __global__ __launch_bounds__(64 * K1_WAVES) void xof_leader_kernel(Cfg c, Bufs b
     for (; m < b_last && m + 1 < NF; m++) {  // the next block is wholly inside the share
       step(m);
       load_block_full(m + 1);
-      keccak_p12(J);
+      keccak_p12(J);  // (unrolled: slower, see keccak_p12_unrolled)
     }
 #pragma unroll 1
     for (; m < b_last; m++) {

@@ -1,0 +1,16 @@
+# Round 5: unrolled permutations in the chain-latency-bound K1 block loops (lane-split / lane-pair helper,
+# leader): parity of those kernels, the small-launch sweep, and configs[4] (two jobs in flight + serial).
+# usage: bash scripts/gpu_r05_unroll.sh <name>
+set -o pipefail
+N=${1:?name}
+OUT=gpurun_out/$N
+mkdir -p $OUT
+timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_leader.py tests/test_gpu_fixedpoint.py -k "k1_split or leader or two_jobs or fixedpoint" -x -v --timeout 300 --timeout-method thread > $OUT/parity.log 2>&1 || { echo PARITY_FAIL; tail -30 $OUT/parity.log; exit 1; }
+tail -1 $OUT/parity.log
+timeout -k 10 120 tools/bin/kernel_probe sweep > $OUT/sweep.jsonl 2> $OUT/sweep.err || { echo SWEEP_FAIL; exit 1; }
+cat $OUT/sweep.jsonl
+timeout -k 10 400 python -u tools/bench_fixedpoint.py --skip cpu,helper,leader --steps 3 --warmup 1 > $OUT/fp.json 2> $OUT/fp.err || { echo FP_FAIL; tail -5 $OUT/fp.err; exit 1; }
+python3 -c "
+import json; d=json.loads(open('$OUT/fp.json').read().strip().splitlines()[-1])
+print('serial', d['value'], d['kernels']); p=d['pipelined']; print('two jobs', p['reports_per_s'], p['ms_per_step'], p['kernels'], p['verified'], d['verified'])"
+echo UNROLL_OK
