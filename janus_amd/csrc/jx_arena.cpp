@@ -103,7 +103,8 @@ hipError_t arena_get(Arena* A, size_t bytes, hipStream_t s, bool staging, bool m
       account_out(A, out);
       A->reuses++;
       if (out.last && out.last != s) A->cross_waits += pick == busy;
-      return hipStreamWaitEvent(s, out.ev, 0);  // after the slab's last user (a never-recorded event: no wait)
+      // after the slab's last user (a never-recorded event: no wait); on its own stream, stream order does it
+      return out.last == s ? hipSuccess : hipStreamWaitEvent(s, out.ev, 0);
     }
     while (A->allocated + bytes > A->budget && trim_one(A)) {
     }

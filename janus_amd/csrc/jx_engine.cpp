@@ -640,6 +640,8 @@ int32_t jxi::prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const ui
     else if (2 * n <= e->round_reports)
       b.k1_split = 3;
   }
+  // the lane pairs with unrolled rounds while each pair-wave has a SIMD to itself (<= 16,384 reports on MI355X)
+  if (b.k1_split == 6 && 8 * n <= e->round_reports) b.k1_split = 8;
   hipEvent_t ev = nullptr;
   if (c.algo == ALGO_COUNT) {
     HIPCHK(e, stage_begin(e, &ev));

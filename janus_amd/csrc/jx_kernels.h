@@ -123,6 +123,7 @@ struct Bufs {
   const uint4* consts;
   uint32_t force_slow;  // debug: route every report through the slow XOF kernel
   uint32_t k1_split;    // helper K1 kernel: 3 = lane-split (xof_lanes_kernel), 6 = lane pairs (xof_pairs_kernel,
+                        // bits <= 32), 8 = lane pairs with unrolled rounds, 7 = a word per lane (xof_words_kernel,
                         // bits <= 32), otherwise the fused kernel
   uint32_t k1_lds;      // dynamic LDS of the lane-split kernel: caps its workgroups per CU (lanes_lds_bytes)
 };

@@ -1214,6 +1214,10 @@ __device__ __forceinline__ void sponge_oneblock_half(uint32_t* s, const Block& m
   keccak_p12_half(s, hi);
 }
 
+// UNR: the rounds of the block loop unrolled (round constants as literals): 4.03 -> 3.59 ms for launches of
+// at most one pair-wave per SIMD, but slower with several waves per SIMD (64 x 1,000-report coalesced jobs:
+// 12.5 -> 15.2 ms per launch), so the engine picks it only for the former (prep_core, k1_split 8).
+template <bool UNR>
 __global__ __launch_bounds__(64 * K1_WAVES, 2) void xof_pairs_kernel(Cfg c, Bufs b) {
   const uint32_t lane = threadIdx.x & 63;
   const bool jh = lane >= 32;     // J lanes
@@ -1378,7 +1382,10 @@ __global__ __launch_bounds__(64 * K1_WAVES, 2) void xof_pairs_kernel(Cfg c, Bufs
   }
 #pragma unroll 1
   for (uint32_t m = 1; m <= b_last; m++) {
-    keccak_p12_half_unrolled(h, hi);  // S: squeeze block m; J: absorb block m - 1
+    if constexpr (UNR)
+      keccak_p12_half_unrolled(h, hi);  // S: squeeze block m; J: absorb block m - 1
+    else
+      keccak_p12_half(h, hi);
     const bool have = m < NM;
     if (have) {
       if (!jh) s_emit_block(m);
@@ -3338,8 +3345,10 @@ hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
       const uint64_t threads = (uint64_t)nblk_of(b.n) * 64 * nout;
       hipLaunchKernelGGL(trunc_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, c, b, nout);
     }
-  } else if (b.k1_split == 6 && !wide)  // lane pairs: 16 reports per wave
-    hipLaunchKernelGGL(xof_pairs_kernel, dim3((4 * nb + K1_WAVES - 1) / K1_WAVES), block, 0, s, c, b);
+  } else if (b.k1_split == 8 && !wide)  // lane pairs, unrolled rounds (<= one pair-wave per SIMD)
+    hipLaunchKernelGGL(xof_pairs_kernel<true>, dim3((4 * nb + K1_WAVES - 1) / K1_WAVES), block, 0, s, c, b);
+  else if (b.k1_split == 6 && !wide)  // lane pairs: 16 reports per wave
+    hipLaunchKernelGGL(xof_pairs_kernel<false>, dim3((4 * nb + K1_WAVES - 1) / K1_WAVES), block, 0, s, c, b);
   else if (b.k1_split == 3) {  // lane-split: 32 reports per wave
     const dim3 g2((2 * nb + K1_WAVES - 1) / K1_WAVES);
     if (wide)
@@ -3376,7 +3385,7 @@ uint64_t k1_round_reports(const Cfg& c, int device, uint32_t k1_split) {
     st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_lanes_kernel<false>, threads, lanes_lds_bytes(2));
     per_wg = threads / 2;
   } else if (k1_split == 6) {
-    st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_pairs_kernel, threads, 0);
+    st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_pairs_kernel<false>, threads, 0);
     per_wg = threads / 4;
   } else {
     st = hipOccupancyMaxActiveBlocksPerMultiprocessor(&wgs, xof_kernel<false>, threads, 0);

@@ -11,8 +11,8 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/kernel_probe.hip -Iinclude -Ljanus_amd/lib -ljanus_prio3 \
 //         -Wl,-rpath,'$ORIGIN/../../janus_amd/lib' -o tools/bin/kernel_probe
 //   tools/bin/kernel_probe [reports=262144] [launches=5]
-//   tools/bin/kernel_probe sweep   (small launches: the lane-pair K1 against the word-per-lane K1 + its
-//                                   truncation kernel, ms per launch at 16 .. 32,768 reports)
+//   tools/bin/kernel_probe sweep   (small launches: the lane-pair K1, rounds unrolled and looped, against the
+//                                   word-per-lane K1 + its truncation kernel, ms per launch at 16 .. 32,768 reports)
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -90,11 +90,14 @@ static int sweep() {
   const uint64_t sizes[] = {16, 100, 256, 512, 1024, 2048, 3072, 4096, 6400, 8192, 16384, 32768};
   for (uint64_t n : sizes) {
     b.n = n;
-    b.k1_split = 6;
+    b.k1_split = 8;  // the lane pairs as the engine picks them below one pair-wave per SIMD (unrolled rounds)
     const double pairs = time_ms([&] { CK(jx::launch_xof(c, b, s)); }, 3, s);
+    b.k1_split = 6;
+    const double pairs_loop = time_ms([&] { CK(jx::launch_xof(c, b, s)); }, 3, s);
     b.k1_split = 7;
     const double words = time_ms([&] { CK(jx::launch_xof(c, b, s)); }, 3, s);
-    printf("{\"reports\": %llu, \"pairs_ms\": %.3f, \"words_ms\": %.3f}\n", (unsigned long long)n, pairs, words);
+    printf("{\"reports\": %llu, \"pairs_ms\": %.3f, \"pairs_looped_ms\": %.3f, \"words_ms\": %.3f}\n",
+           (unsigned long long)n, pairs, pairs_loop, words);
     fflush(stdout);
   }
   jx_engine_destroy(e);
