@@ -511,3 +511,30 @@ def test_helper_batch_keep_false_and_resident_scope():
         with pytest.raises(EngineError, match="no resident"):
             eng.release(res.batch_id)
         eng.release(res.batch_id, missing_ok=True)
+
+
+@pytest.mark.parametrize("vdaf", [Prio3.count(), Prio3.sum_vec(4, 12, 4)], ids=["count-field64", "sumvec-field128"])
+def test_small_accumulate_boundary(vdaf):
+    """jx_accumulate of an unmasked batch of <= ACC_SMALL (1,024) reports runs the one-kernel accumulate
+    (accumulate_small_kernel: no staging, no partials); 1,025 reports or an accept mask take select +
+    accumulate + reduce_partials. Both sides of the boundary, added into one aggregation, == the oracle."""
+    vk = bytes(range(120, 136))
+    n = 2049
+    orc, nonces, ps, his, lps = _batch(vdaf, vk, n, seed=1024)
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
+    parts = [(0, 1024), (1024, 2049)]  # the small path, then the large one
+    rng = np.random.default_rng(5)
+    mask = rng.integers(0, 2, size=n).astype(bool)
+    with HelperEngine(vdaf, vk) as eng:
+        for a, b in parts:
+            res = eng.helper_initialized_batch(nonces[a:b], ps[a:b], his[a:b], lps[a:b])
+            np.testing.assert_array_equal(res.verdicts, want["verdicts"][a:b])
+            eng.accumulate(b - a, batch_id=res.batch_id)
+        assert eng.aggregate_share(0) == (want["agg"], want["count"], want["checksum"])
+        # a masked small batch (staged mask upload, the three-kernel path) into a second aggregation
+        eng.reset_aggregates()
+        res = eng.helper_initialized_batch(nonces[:512], ps[:512], his[:512], lps[:512])
+        eng.accumulate(512, accept_mask=mask[:512].astype(np.uint8), batch_id=res.batch_id)
+        sel = (want["verdicts"][:512] == 0) & mask[:512]
+        exp = _expected(orc, want, nonces, np.concatenate([sel, np.zeros(n - 512, bool)]))
+        assert eng.aggregate_share(0) == exp
