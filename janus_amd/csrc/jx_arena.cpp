@@ -177,4 +177,34 @@ void arena_engine_remove(Arena* A) {
     }
 }
 
+hipError_t arena_big_record(Arena* A, const void* owner, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(A->mu);
+  hipEvent_t& ev = A->big[owner];
+  if (!ev) {
+    const hipError_t st = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (st != hipSuccess) {
+      A->big.erase(owner);
+      return st;
+    }
+  }
+  return hipEventRecord(ev, s);
+}
+
+bool arena_big_busy(Arena* A, const void* owner) {
+  std::lock_guard<std::mutex> lk(A->mu);
+  bool busy = false;
+  for (auto& kv : A->big)
+    if (kv.first != owner && hipEventQuery(kv.second) == hipErrorNotReady) busy = true;
+  (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
+  return busy;
+}
+
+void arena_big_forget(Arena* A, const void* owner) {
+  std::lock_guard<std::mutex> lk(A->mu);
+  auto it = A->big.find(owner);
+  if (it == A->big.end()) return;
+  (void)hipEventDestroy(it->second);
+  A->big.erase(it);
+}
+
 }  // namespace jxi

@@ -642,6 +642,17 @@ int32_t jxi::prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const ui
   }
   // the lane pairs with unrolled rounds while each pair-wave has a SIMD to itself (<= 16,384 reports on MI355X)
   if (b.k1_split == 6 && 8 * n <= e->round_reports) b.k1_split = 8;
+  // A lane-split launch past one wave per SIMD puts two of its long chains on some SIMDs and the launch waits
+  // for those. Instead the first round_reports / 4 reports (a lane-split wave per SIMD) run lane-split and the
+  // rest as lane pairs beside them on the side stream: FixedPointBoundedL2VecSum 16 x 10000, 40,960 reports,
+  // 148.4 -> 123.5 ms (tools/kernel_probe fpmix, profiles/r05_fp_mixed_k1.jsonl). Only while no other engine
+  // on the device has a large K1 launch in flight: beside the leader's 640 K1 waves (configs[4] with two jobs in
+  // flight) the 1,536 mixed waves pack worse than 1,280 lane-split ones (helper K1 154 -> 161 ms, every split
+  // point tried; profiles/r05_fp_mixed_k1.jsonl).
+  const uint64_t split_at = e->round_reports / 4 / 64 * 64;
+  const bool big = split_at && n > split_at;
+  const bool mixed = e->k1_split == 0 && b.k1_split == 3 && !wide && big && c.algo != ALGO_COUNT &&
+                     c.algo != ALGO_SUMVEC_F64_MULTIPROOF && !arena_big_busy(e->arena, e);
   hipEvent_t ev = nullptr;
   if (c.algo == ALGO_COUNT) {
     HIPCHK(e, stage_begin(e, &ev));
@@ -661,7 +672,23 @@ int32_t jxi::prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const ui
     HIPCHK(e, stage_end(e, ST_FLP, ev));
   } else {
     HIPCHK(e, stage_begin(e, &ev));
-    HIPCHK(e, launch_xof(c, b, e->stream));
+    if (mixed) {
+      if (!e->side) HIPCHK(e, hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
+      if (!e->ev_fork) HIPCHK(e, hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+      if (!e->ev_side) HIPCHK(e, hipEventCreateWithFlags(&e->ev_side, hipEventDisableTiming));
+      Bufs head = b, tail = bufs_tail(c, b, split_at);
+      head.n = split_at;
+      tail.k1_split = 8 * tail.n <= e->round_reports ? 8u : 6u;
+      HIPCHK(e, hipEventRecord(e->ev_fork, e->stream));
+      HIPCHK(e, hipStreamWaitEvent(e->side, e->ev_fork, 0));
+      HIPCHK(e, launch_xof(c, head, e->stream));
+      HIPCHK(e, launch_xof(c, tail, e->side));
+      HIPCHK(e, hipEventRecord(e->ev_side, e->side));
+      HIPCHK(e, hipStreamWaitEvent(e->stream, e->ev_side, 0));
+    } else {
+      HIPCHK(e, launch_xof(c, b, e->stream));
+    }
+    if (big) HIPCHK(e, arena_big_record(e->arena, e, e->stream));
     HIPCHK(e, stage_end(e, ST_XOF, ev));
     if (!leader) {  // the leader's shares are explicit: no rejection-sampled streams to redo
       HIPCHK(e, stage_begin(e, &ev));
@@ -1092,6 +1119,10 @@ void jx_engine_destroy(jx_engine* e) {
   if (e->ev_hacc) (void)hipEventDestroy(e->ev_hacc);
   if (e->ev_wait) (void)hipEventDestroy(e->ev_wait);
   if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+  if (e->arena) arena_big_forget(e->arena, e);
+  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  if (e->ev_side) (void)hipEventDestroy(e->ev_side);
+  if (e->side) (void)hipStreamDestroy(e->side);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   if (e->arena && !e->is_pipe) arena_engine_remove(e->arena);
   delete e;

@@ -45,6 +45,9 @@ struct Arena {
   uint64_t allocs = 0, reuses = 0, waits = 0, frees = 0, cross_waits = 0;
   uint32_t engines = 0;          // live engines on this device (the last one out trims the free slabs)
   std::multimap<size_t, Slab> free;
+  // per engine (owner pointer): an event recorded after its latest large K1 launch (more reports than a
+  // lane-split wave per SIMD), so a launch can tell whether it would share the device with one
+  std::map<const void*, hipEvent_t> big;
 };
 
 Arena* arena_for(int device);
@@ -58,6 +61,11 @@ void arena_put(Arena* A, Slab& slab, hipStream_t s);
 void arena_trim(Arena* A);
 void arena_engine_add(Arena* A);
 void arena_engine_remove(Arena* A);
+// Large K1 launches on the device: record one of `owner`'s after it on stream s; is one of another owner's
+// still running; forget an owner (engine teardown).
+hipError_t arena_big_record(Arena* A, const void* owner, hipStream_t s);
+bool arena_big_busy(Arena* A, const void* owner);
+void arena_big_forget(Arena* A, const void* owner);
 
 // ---------------------------------------------------------------------------- engine state
 
@@ -158,6 +166,10 @@ struct jx_engine {
   jxi::Cfg cfg{};
   int device = 0;
   hipStream_t stream = nullptr;
+  // helper K1 launches split over two kernels (prep_core): the lane-pair part runs on this side stream,
+  // forked from and joined back into `stream` by events
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_side = nullptr;
   jxi::FairMutex mu;  // held by every entry point for the duration of the call (coalesced prepares: not while waiting)
   jxi::Arena* arena = nullptr;
   // per-call staging, carved from an arena slab by stage_acquire and cleared by its release

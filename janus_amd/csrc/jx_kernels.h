@@ -212,6 +212,9 @@ hipError_t launch_scatter_jobs(const Cfg& c, const JobSlice* d_jobs, uint32_t nj
                                hipStream_t s);
 // multiproof Field64 SumVec (jx_mp64.hip)
 uint64_t k1_round_reports(const Cfg& c, int device, uint32_t k1_split = 0);
+// The helper reports [S, b.n) of a launch as Bufs of their own (S a multiple of 64: every staging array is
+// interleaved by 64-report blocks), for a K1 launch over part of the reports.
+Bufs bufs_tail(const Cfg& c, const Bufs& b, uint64_t S);
 uint32_t lanes_lds_bytes(uint32_t wgs_per_cu);
 uint64_t mp_k1_round_reports(int device);
 hipError_t launch_mp_xof(const Cfg& c, const Bufs& b, hipStream_t s);

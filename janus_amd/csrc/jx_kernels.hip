@@ -3361,6 +3361,24 @@ hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
     hipLaunchKernelGGL((xof_kernel<false>), grid, block, 0, s, c, b);
   return hipGetLastError();
 }
+Bufs bufs_tail(const Cfg& c, const Bufs& b, uint64_t S) {
+  Bufs t = b;
+  const uint64_t blk = S / 64;
+  t.n = b.n - S;
+  t.nonces += S * 16;
+  t.ps += S * c.ps_bytes;
+  t.his += S * c.his_bytes;
+  t.lps += S * c.lps_bytes;
+  t.meas += blk * c.meas_len * IL;
+  t.proof += blk * c.proof_len * IL;
+  t.outs += blk * c.out_len * IL;
+  t.coef += blk * c.ncoef * IL;
+  t.flags += S;
+  t.verdicts += S;
+  t.msgs += S * 16;
+  return t;
+}
+
 // Dynamic LDS that caps the lane-split kernel at `wgs_per_cu` workgroups per CU (0: no cap).
 uint32_t lanes_lds_bytes(uint32_t wgs_per_cu) {
   if (wgs_per_cu == 0) return 0;

@@ -324,3 +324,33 @@ def test_k3_ring_padded_groups(name):
     for i in range(24):
         rc, share, _, _ = orc.prep_init(vk, 0, ln[i].tobytes(), lps_[i].tobytes(), lis_[i].tobytes())
         assert rc == 0 and init.prep_shares[i].tobytes() == share, i
+
+
+@pytest.mark.parametrize("name", ["sumvec_small", "histogram_256_16"])
+def test_mixed_k1_launch(name):
+    """A helper launch past one lane-split wave per SIMD (40,960 reports on MI355X: round_reports / 4 = 32,768)
+    runs its first 32,768 reports lane-split on the engine stream and the rest as lane pairs on the side stream
+    (prep_core, bufs_tail). Every verdict, finished prep message and output share, and the aggregate, == the
+    oracle's (a 512-report pool tiled)."""
+    vdaf = CASES[name]
+    vk = bytes(range(140, 156))
+    orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
+    K, n = 512, 40960
+    nonces, ps, his, lps = _random_batch(orc, vk, K, seed=4096 + sum(map(ord, name)))
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
+    idx = np.arange(n) % K
+    with HelperEngine(vdaf, vk) as eng:
+        res = eng.helper_initialized_batch(nonces[idx], ps[idx], his[idx], lps[idx], want_out_shares=True)
+        np.testing.assert_array_equal(res.verdicts, want["verdicts"][idx])
+        fin = want["verdicts"][idx] == 0
+        np.testing.assert_array_equal(res.prep_msgs[fin], want["prep_msgs"][idx][fin])
+        np.testing.assert_array_equal(res.out_shares[fin], want["out_shares"][idx][fin])
+        eng.accumulate(n)
+        agg, count, cs = eng.aggregate_share(0)
+        assert count == int(fin.sum())
+        assert agg == orc.aggregate([want["out_shares"][i].tobytes() for i in idx[fin]])
+        exp_cs = bytes(32)
+        for i, f in zip(idx, fin):  # XOR of SHA-256(id): tiled ids cancel in pairs
+            if f:
+                exp_cs = bytes(a ^ b for a, b in zip(exp_cs, O.sha256(nonces[i].tobytes())))
+        assert cs == exp_cs

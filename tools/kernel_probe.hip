@@ -11,6 +11,8 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/kernel_probe.hip -Iinclude -Ljanus_amd/lib -ljanus_prio3 \
 //         -Wl,-rpath,'$ORIGIN/../../janus_amd/lib' -o tools/bin/kernel_probe
 //   tools/bin/kernel_probe [reports=262144] [launches=5]
+//   tools/bin/kernel_probe fpmix   (configs[4] helper K1: lane-split alone against lane-split + lane pairs on two
+//                                   streams, 40,960 FixedPoint 16 x 10000 reports)
 //   tools/bin/kernel_probe sweep   (small launches: the lane-pair K1, rounds unrolled and looped, against the
 //                                   word-per-lane K1 + its truncation kernel, ms per launch at 16 .. 32,768 reports)
 #include <cstdio>
@@ -104,8 +106,95 @@ static int sweep() {
   return 0;
 }
 
+// configs[4]'s helper K1 (FixedPointBoundedL2VecSum 16 x 10000, 40,960 reports, lone): the lane-split kernel
+// over all reports against a mixed launch (the first S reports lane-split on one stream, the rest as lane pairs on
+// a second stream at the same time), for a few split points.
+static int fpmix() {
+  jx_prio3_params p{5, 16, 10000, 0, 1};
+  uint8_t vk[16] = {0};
+  jx_engine* e = nullptr;
+  if (jx_engine_create(&p, vk, 0, &e)) return 2;
+  const jx::Cfg c = e->cfg;
+  const uint64_t N = 40960;
+  jx::Bufs b{};
+  b.n = N;
+  b.nonces = (const uint8_t*)dalloc(N * 16, 1);
+  b.ps = (const uint8_t*)dalloc(N * c.ps_bytes, 2);
+  b.his = (const uint8_t*)dalloc(N * c.his_bytes, 3);
+  b.lps = (const uint8_t*)dalloc(N * c.lps_bytes, 4);
+  b.meas = (uint4*)dalloc(N * (uint64_t)c.meas_len * 16, 5);
+  b.proof = (uint4*)dalloc(N * (uint64_t)c.proof_len * 16, 6);
+  b.outs = (uint4*)dalloc(N * (uint64_t)c.out_len * 16, 7);
+  b.coef = (uint4*)dalloc(N * (uint64_t)c.ncoef * 16, 8);
+  b.flags = (uint32_t*)dalloc(N * 4, 9);
+  b.verdicts = (uint8_t*)dalloc(N, 11);
+  b.msgs = (uint8_t*)dalloc(N * 16, 12);
+  b.consts = e->d_consts;
+  b.lis_rs = c.lis_bytes;
+  b.k1_lds = jx::lanes_lds_bytes(2);
+  CK(hipDeviceSynchronize());
+  hipStream_t s1, s2;
+  CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+  CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  hipEvent_t fork, join, t0, t1;
+  CK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+  CK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+  CK(hipEventCreate(&t0));
+  CK(hipEventCreate(&t1));
+  // the reports [S, N) as a Bufs of their own (whole 64-report blocks: every staging array is block-interleaved)
+  auto tail = [&](uint64_t S) {
+    jx::Bufs t = b;
+    const uint64_t blk = S / 64;
+    t.n = N - S;
+    t.nonces += S * 16;
+    t.ps += S * c.ps_bytes;
+    t.his += S * c.his_bytes;
+    t.lps += S * c.lps_bytes;
+    t.meas += blk * c.meas_len * jx::IL;
+    t.proof += blk * c.proof_len * jx::IL;
+    t.outs += blk * c.out_len * jx::IL;
+    t.coef += blk * c.ncoef * jx::IL;
+    t.flags += S;
+    t.verdicts += S;
+    t.msgs += S * 16;
+    return t;
+  };
+  auto run = [&](uint64_t S, uint32_t split_b, int reps) {
+    float best = 1e30f;
+    for (int it = 0; it < reps + 1; it++) {
+      jx::Bufs a = b, t = tail(S);
+      a.n = S;
+      a.k1_split = 3;
+      t.k1_split = split_b;
+      CK(hipEventRecord(t0, s1));
+      CK(hipEventRecord(fork, s1));
+      CK(hipStreamWaitEvent(s2, fork, 0));
+      if (S) CK(jx::launch_xof(c, a, s1));
+      if (S < N) CK(jx::launch_xof(c, t, s2));
+      CK(hipEventRecord(join, s2));
+      CK(hipStreamWaitEvent(s1, join, 0));
+      CK(hipEventRecord(t1, s1));
+      CK(hipEventSynchronize(t1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, t0, t1));
+      if (it > 0 && ms < best) best = ms;
+    }
+    return (double)best;
+  };
+  const uint64_t splits[] = {40960, 36864, 34816, 32768, 30720, 28672, 0};
+  for (uint64_t S : splits) {
+    const double ms = run(S, 8, 2);
+    printf("{\"lane_split_reports\": %llu, \"lane_pair_reports\": %llu, \"ms\": %.2f}\n", (unsigned long long)S,
+           (unsigned long long)(N - S), ms);
+    fflush(stdout);
+  }
+  jx_engine_destroy(e);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && std::string(argv[1]) == "sweep") return sweep();
+  if (argc > 1 && std::string(argv[1]) == "fpmix") return fpmix();
   const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 262144;
   const int iters = argc > 2 ? atoi(argv[2]) : 5;
   jx_prio3_params p{2, 8, 1000, 88, 1};
