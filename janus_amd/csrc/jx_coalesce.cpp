@@ -114,8 +114,10 @@ static std::string coal_key(const jx_engine* e) {
          std::to_string(c.length) + "/" + std::to_string(c.chunk) + "/" + std::to_string(c.np);
 }
 
-// A gathering lane closes once no job has joined it for kQuietUs, fewer than kMaxRunning launches are on the
-// device, and the callers of the launches that completed meanwhile have come back (up to kRejoinUs after the
+// A gathering lane closes at once while no launch runs and no caller of a completed launch is still due back
+// (a lone caller, or the device idle: nothing to wait for). Otherwise it closes once no job has joined it for
+// kQuietUs, fewer than kMaxRunning launches are on the device, and the callers of the launches that completed
+// meanwhile have come back (up to kRejoinUs after the
 // completion: copying their results, accumulating, preparing their next job), so closed-loop callers share a
 // launch per round trip instead of splitting into fragments; open-loop arrivals wait at most the window. A
 // launch's device time is nearly flat in its size below a K1 round (the per-report sponge chain), so two
@@ -294,6 +296,8 @@ static void dispatcher_main(Coalescer* C) {
       if (now >= deadline) break;
       const auto quiet_at = L.last_arrival + std::chrono::microseconds(kQuietUs);
       const bool back = C->expect == 0 || now >= C->expect_until;
+      // nothing on the device and no caller of a completed launch still to come: waiting buys nothing
+      if (C->nrunning == 0 && C->expect == 0) break;
       if (now >= quiet_at && ((back && C->nrunning < kMaxRunning) || L.reports >= C->max_reports / 4)) break;
       auto until = deadline;
       if (now < quiet_at && quiet_at < until) until = quiet_at;
