@@ -182,11 +182,13 @@ static int fpmix() {
     return (double)best;
   };
   const uint64_t splits[] = {40960, 36864, 34816, 32768, 30720, 28672, 0};
-  for (uint64_t S : splits) {
-    const double ms = run(S, 8, 2);
-    printf("{\"lane_split_reports\": %llu, \"lane_pair_reports\": %llu, \"ms\": %.2f}\n", (unsigned long long)S,
-           (unsigned long long)(N - S), ms);
-    fflush(stdout);
+  for (uint32_t pk : {8u, 6u}) {  // the lane-pair part with unrolled (8) or looped (6) rounds
+    for (uint64_t S : splits) {
+      const double ms = run(S, pk, 2);
+      printf("{\"lane_split_reports\": %llu, \"lane_pair_reports\": %llu, \"pairs_unrolled\": %s, \"ms\": %.2f}\n",
+             (unsigned long long)S, (unsigned long long)(N - S), pk == 8 ? "true" : "false", ms);
+      fflush(stdout);
+    }
   }
   jx_engine_destroy(e);
   return 0;
