@@ -26,7 +26,10 @@
  *    so any number of engines (tasks) share one GPU's HBM. Every entry point takes the engine's mutex
  *    for the duration of the call, so one engine can serve concurrent aggregation jobs from several
  *    host threads; the device work of the calls is serialized on the engine stream. What a job keeps
- *    between calls (its prepared reports) is a batch handle.
+ *    between calls (its prepared reports) is a batch handle. (A helper launch past one lane-split K1
+ *    wave per SIMD, while no other engine on the device runs a large K1 launch, puts part of its K1 on
+ *    a second stream of the engine, forked from and joined back into the engine stream by events: the
+ *    ordering below is unchanged.)
  *  - Coalesced prepares (jx_engine_coalesce): with coalescing on, jx_helper_prep_batch and
  *    jx_leader_prep_init_batch of jobs up to a quarter of a launch join the device's next shared launch
  *    with the concurrent jobs of every coalescing engine of the same Prio3 instance on the device (each
