@@ -121,10 +121,11 @@ static std::string coal_key(const jx_engine* e) {
 // completion: copying their results, accumulating, preparing their next job), so closed-loop callers share a
 // launch per round trip instead of splitting into fragments; open-loop arrivals wait at most the window. A
 // launch's device time is nearly flat in its size below a K1 round (the per-report sponge chain), so two
-// launches in flight, each carrying every job that is back, is the measured optimum (64
-// threads x 100-report jobs, 1 / 2 / 3 running and 1 / 3 ms rejoin).
+// launches in flight, each carrying every job that is back, is the measured optimum (DESIGN.md §5.4:
+// profiles/r05_coalesce_policy_ab.jsonl, 1 / 2 / 3 running; profiles/r05_coalesce_rejoin_retune.jsonl, the
+// rejoin window re-measured on the final kernels and host path: 1 ms, against 1.5 / 2 / 3 ms).
 constexpr uint32_t kQuietUs = 100;
-constexpr uint32_t kRejoinUs = 3000;
+constexpr uint32_t kRejoinUs = 1000;
 constexpr uint32_t kMaxRunning = 2;
 
 // The longest a gathering lane waits for more jobs (automatic: 1.5x the recent launch latency, 0.1-20 ms). It
