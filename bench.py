@@ -353,11 +353,56 @@ def _free_port() -> int:
         return so.getsockname()[1]
 
 
-def ensure_world(gpus: int) -> None:
+def _visible_filter(n: int) -> int:
+    """GPUs left after the HIP/ROCr visibility variables (comma lists of indices or UUIDs)."""
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
+def count_gpus(sysfs_root: str = "/sys/class/kfd/kfd/topology/nodes") -> int | None:
+    """GPUs on this node without starting a GPU runtime: amdsmi (the management library; no HIP) or,
+    failing that, the KFD topology in sysfs (nodes with SIMDs are GPUs). None when neither answers.
+    Never torch.cuda: its fallback (_cuda_getDeviceCount) initialises HIP, and a launcher started after
+    that would be a process that touched the GPU handing over to others."""
+    try:
+        import amdsmi
+
+        amdsmi.amdsmi_init()
+        try:
+            n = len(amdsmi.amdsmi_get_processor_handles())
+        finally:
+            amdsmi.amdsmi_shut_down()
+        if n > 0:
+            return _visible_filter(n)
+    except Exception:  # noqa: BLE001 - missing module or library, no permission: try sysfs
+        pass
+    try:
+        n = 0
+        for node in os.listdir(sysfs_root):
+            props = os.path.join(sysfs_root, node, "properties")
+            try:
+                with open(props) as f:
+                    kv = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            except OSError:
+                continue
+            if int(kv.get("simd_count", "0")) > 0:
+                n += 1
+        if n > 0:
+            return _visible_filter(n)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def ensure_world(gpus: int, sysfs_root: str = "/sys/class/kfd/kfd/topology/nodes") -> None:
     """`--gpus N` means N ranks, one per GPU. Without a torch.distributed launcher in the
     environment, start one (torch.distributed.run as a child process, before this process touches
-    the GPU) and exit with its status; refuse N beyond the visible GPUs or a launcher world of
-    another size, instead of silently measuring one GPU."""
+    the GPU) and exit with its status; refuse N beyond the GPUs that amdsmi / the KFD topology report
+    (or when neither can count them), or a launcher world of another size, instead of silently measuring
+    one GPU. Nothing here imports torch or starts HIP."""
     world = os.environ.get("WORLD_SIZE")
     if world is not None:
         if int(world) != gpus:
@@ -367,9 +412,10 @@ def ensure_world(gpus: int) -> None:
         return
     import subprocess
 
-    import torch  # device_count() does not initialise the HIP runtime on this image
-
-    have = torch.cuda.device_count()
+    have = count_gpus(sysfs_root)
+    if have is None:
+        sys.exit(f"bench.py: --gpus {gpus}: cannot count the node's GPUs (amdsmi and the KFD topology both "
+                 "unavailable); refusing to start a launcher")
     if gpus > have:
         sys.exit(f"bench.py: --gpus {gpus} but only {have} GPU(s) visible")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",

@@ -170,7 +170,9 @@ int32_t jx_engine_memory(const jx_engine* e, jx_memory_stats* out);
  * window_us: the longest a launch gathers jobs after its first one arrives (0 = automatic: 1.5x the recent
  * launch latency, 0.1 .. 20 ms). A launch closes earlier when it is full, or once no job has joined for
  * 100 us while no other launch of the coalescer is running (or it already holds a quarter of a full
- * launch). Calls already waiting are unaffected by a later disable. */
+ * launch). Calls already waiting are unaffected by a later disable. The window is a setting of the device
+ * coalescer, which every coalescing engine of the same Prio3 instance on the device shares: the last call
+ * sets it for all of them. */
 int32_t jx_engine_coalesce(jx_engine* e, int32_t enable, uint32_t window_us);
 
 /* Batched helper_initialized + evaluate for n reports (host buffers).
@@ -348,7 +350,9 @@ int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]);
  *   option 5: reports per launch of the fused paths: 0 automatic (whole K1 rounds within ~48 GiB of
  *             staging), else >= 64 (rounded down to a multiple of 64);
  *   option 6: lane-split K1 workgroups per CU (its placement for chain-latency-bound launches): 2 default
- *             (at most two waves per SIMD), 0 no cap, 1..8. */
+ *             (at most two waves per SIMD), 0 no cap, 1..8;
+ *   option 7: tests: the device coalescer's gathers wait, up to their window, until `value` jobs have joined
+ *             (0: off); needs coalescing on (JX_E_STATE otherwise). Applies to the whole device coalescer. */
 int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value);
 
 const char* jx_status_str(int32_t status);

@@ -94,6 +94,7 @@ struct Coalescer {
   bool stop = false;
   uint32_t refs = 0;
   uint32_t window_us = 0;         // 0: automatic
+  uint32_t min_jobs = 0;          // debug option 7 (tests): a gather waits (up to its window) for this many jobs
   double ewma_us = 0;             // launch latency
   uint32_t nrunning = 0;          // launches queued on the device and not yet done
   uint32_t expect = 0;            // jobs of completed launches not yet back (closed-loop callers return)
@@ -295,6 +296,10 @@ static void dispatcher_main(Coalescer* C) {
       if (C->stop || L.full || L.reports >= L.cap_reports || L.reqs.size() >= MAX_JOBS_PER_LAUNCH) break;
       const auto now = clk::now();
       if (now >= deadline) break;
+      if (L.reqs.size() < C->min_jobs) {  // a test holds the gather for its jobs
+        C->cv_disp.wait_until(lk, deadline);
+        continue;
+      }
       const auto quiet_at = L.last_arrival + std::chrono::microseconds(kQuietUs);
       const bool back = C->expect == 0 || now >= C->expect_until;
       // nothing on the device and no caller of a completed launch still to come: waiting buys nothing
@@ -453,6 +458,12 @@ void coalescer_set_window(jx_engine* e, uint32_t window_us) {
   if (!e->coal) return;
   std::lock_guard<std::mutex> lk(e->coal->mu);
   e->coal->window_us = window_us;
+}
+
+void coalescer_set_min_jobs(jx_engine* e, uint32_t jobs) {
+  if (!e->coal) return;
+  std::lock_guard<std::mutex> lk(e->coal->mu);
+  e->coal->min_jobs = jobs;
 }
 
 void coalescer_stats(const jx_engine* e, uint64_t out[12]) {

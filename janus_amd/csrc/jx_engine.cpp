@@ -1992,15 +1992,13 @@ int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]) {
 int32_t jx_engine_coalesce(jx_engine* e, int32_t enable, uint32_t window_us) {
   if (!e || e->is_pipe) return JX_E_INVALID;
   if (window_us > 1000000) return JX_E_INVALID;
-  {
-    LOCK(e);
-    HIPCHK(e, hipSetDevice(e->device));
-  }
-  if (enable) {
-    if (!e->coal) e->coal = coalescer_for(e);
+  // under the engine mutex: concurrent enables create (and reference) the device coalescer once
+  LOCK(e);
+  HIPCHK(e, hipSetDevice(e->device));
+  if (enable && !e->coal) {
+    e->coal = coalescer_for(e);
     if (!e->coal) return fail(e, JX_E_HIP, "coalesce: could not start the device coalescer");
   }
-  std::lock_guard<FairMutex> lk(e->mu);
   e->coalesce = enable != 0;
   if (e->coal) coalescer_set_window(e, window_us);
   return JX_OK;
@@ -2035,6 +2033,12 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
     if (value < 0 || value > 8) return JX_E_INVALID;
     e->lanes_wg_cap = (uint32_t)value;
     for (jx_engine* q : e->pipes) q->lanes_wg_cap = e->lanes_wg_cap;
+    return JX_OK;
+  }
+  if (option == 7) {  // tests: the device coalescer's gathers wait (up to their window) for this many jobs
+    if (value < 0 || value > (int64_t)MAX_JOBS_PER_LAUNCH) return JX_E_INVALID;
+    if (!e->coal) return fail(e, JX_E_STATE, "debug option 7: coalescing is off");
+    coalescer_set_min_jobs(e, (uint32_t)value);
     return JX_OK;
   }
   if (option == 5) {  // reports per launch of the fused paths: 0 automatic, else >= 64 (rounded down to 64)

@@ -299,6 +299,7 @@ int32_t coalesced_leader_init(jx_engine* e, uint64_t n, const uint8_t* nonces, c
                               uint8_t* out_prep_shares, uint8_t* out_verdicts, uint64_t* out_batch_id);
 void coalescer_stats(const jx_engine* e, uint64_t out[12]);
 void coalescer_set_window(jx_engine* e, uint32_t window_us);  // 0: automatic
+void coalescer_set_min_jobs(jx_engine* e, uint32_t jobs);     // debug option 7
 void coalescer_release(jx_engine* e);
 
 }  // namespace jxi

@@ -1472,7 +1472,8 @@ __global__ __launch_bounds__(64 * K1_WAVES, 2) void xof_pairs_kernel(Cfg c, Bufs
 // round per lane (4.0 ms per launch, profiles/r05_small_launch_kernels.json). This kernel spreads each
 // sponge over 25 lanes, one 64-bit word per lane (lane = x + 5y), one report per wave: lanes 0..24 squeeze
 // the measurement share (S), lanes 32..56 absorb the joint_rand_part (J). A round is 26 VALU per lane and
-// two exchanges through the wave's own LDS region (no barrier: a wave's LDS operations complete in order):
+// two exchanges through the wave's own LDS region (kw_sync at each hand-off: a wave's LDS operations complete in
+// order, so no barrier instruction is needed, only a compiler fence):
 //   theta: every lane writes its word into a column-major table whose columns are padded with wrap copies
 //          (slot c + 1 holds column c, slot 0 column 4, slot 6 column 0), then reads columns x - 1 and
 //          x + 1 as five ds_read2_b64 at offsets (k, k + 10) from one base;
@@ -1502,10 +1503,22 @@ struct KwLane {
   uint32_t m0;            // iota: all-ones on word 0
 };
 
+// A hand-off between the lanes of one wave through its LDS region: every lane's earlier LDS writes are
+// visible to every lane's later reads (and earlier reads complete before later writes). gfx950 completes a
+// wave's LDS operations in order, so this emits no instruction; it forbids the compiler from moving LDS
+// accesses across it, which it may otherwise do for pairs it proves distinct per thread (the C++ model does
+// not order plain accesses of different lanes).
+__device__ __forceinline__ void kw_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ void kw_round(uint2* L, const KwLane& k, uint32_t& lo, uint32_t& hi, uint32_t rlo,
                                          uint32_t rhi) {
   L[k.aw1] = make_uint2(lo, hi);
   L[k.aw2] = make_uint2(lo, hi);
+  kw_sync();  // theta table written -> read (the previous round's chi reads are behind the chi sync)
   uint2 cm[5], cp[5];
 #pragma unroll
   for (int j = 0; j < 5; j++) {
@@ -1525,6 +1538,7 @@ __device__ __forceinline__ void kw_round(uint2* L, const KwLane& k, uint32_t& lo
   const uint32_t nh = alignbit(P, Q, k.s), nl = alignbit(Q, P, k.s);
   L[k.bw1] = make_uint2(nl, nh);
   L[k.bw2] = make_uint2(nl, nh);
+  kw_sync();  // chi table written -> read (this round's theta reads are behind the theta sync)
   const uint2 b0 = L[k.bb], b1 = L[k.bb + 1], b2 = L[k.bb + 2];
   lo = (b0.x ^ (~b1.x & b2.x)) ^ (rlo & k.m0);
   hi = (b0.y ^ (~b1.y & b2.y)) ^ (rhi & k.m0);
@@ -1578,6 +1592,7 @@ __global__ __launch_bounds__(64 * KW_WAVES) void xof_words_kernel(Cfg c, Bufs b)
 #pragma unroll
       for (int w = 0; w < 21; w++) L[KW_INIT + w] = make_uint2(m.w[2 * w], m.w[2 * w + 1]);
     }
+    kw_sync();  // lane 0's init block -> every S lane
     const uint2 v = L[KW_INIT + (i < 21u ? i : 0u)];
     const uint32_t jlo = lo, jhi = hi;
     lo = sw21 ? v.x : 0u;
@@ -1651,14 +1666,18 @@ __global__ __launch_bounds__(64 * KW_WAVES) void xof_words_kernel(Cfg c, Bufs b)
   }
   s_emit(b.meas, c.meas_len, 0);
   if (sw21) L[KW_MSG + 6 + i] = make_uint2(lo, hi);
+  kw_sync();  // the header (lane 0) and S's block -> J's message words
   j_absorb(b_last == 0, ML);  // J's state is zero: absorbing block 0 sets it
+  kw_sync();  // J's window reads complete before S overwrites the window's prefix
   if (sw21 && i >= 15u) L[KW_MSG + i - 15u] = make_uint2(lo, hi);
 #pragma unroll 1
   for (uint32_t m = 1; m <= b_last; m++) {
     kw_p12(L, k, lo, hi);  // S: squeeze block m; J: absorb block m - 1
     if (m < NM) s_emit(b.meas, c.meas_len, m);
     if (sw21) L[KW_MSG + 6 + i] = make_uint2(lo, hi);
+    kw_sync();  // S's block -> J's message words
     j_absorb(m == b_last, ML - 168u * m);
+    kw_sync();  // J's window reads complete before S overwrites the window's prefix
     if (sw21 && i >= 15u) L[KW_MSG + i - 15u] = make_uint2(lo, hi);
   }
   kw_p12(L, k, lo, hi);  // J: absorb block b_last
@@ -3376,6 +3395,12 @@ Bufs bufs_tail(const Cfg& c, const Bufs& b, uint64_t S) {
   t.flags += S;
   t.verdicts += S;
   t.msgs += S * 16;
+  // per-report rows that a coalesced launch carries: the verify keys (16 B, or the 64-B HMAC pads of the
+  // multiproof instance) and, for a leader launch, its explicit input shares and outbound prep shares
+  if (t.vkeys) t.vkeys += S * (c.algo == ALGO_SUMVEC_F64_MULTIPROOF ? 64u : 16u);
+  if (t.lis) t.lis += S * b.lis_rs;
+  if (t.meas_src) t.meas_src += S * b.meas_rs;
+  if (t.lps_out) t.lps_out += S * c.lps_bytes;
   return t;
 }
 

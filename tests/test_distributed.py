@@ -126,6 +126,57 @@ def test_bench_refuses_world_mismatch():
     assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
 
 
+_NO_GPU_RUNTIME = """
+import sys, types
+class _Untouchable(types.ModuleType):
+    def __getattr__(self, k):
+        raise SystemExit("torch touched before the launcher: torch." + k)
+sys.modules["torch"] = _Untouchable("torch")
+am = types.ModuleType("amdsmi")
+def _fail(*a):
+    raise RuntimeError("amdsmi unavailable")
+am.amdsmi_init = _fail
+sys.modules["amdsmi"] = am
+sys.path.insert(0, ROOT)
+import bench
+"""
+
+
+def test_bench_refuses_when_gpus_cannot_be_counted():
+    """With amdsmi failing and no KFD topology, bench.py --gpus 2 refuses (exit != 0) before any launcher,
+    and never reaches torch (whose device count could initialise HIP in this process)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _NO_GPU_RUNTIME.replace("ROOT", repr(root)) + "bench.ensure_world(2, sysfs_root='/nonexistent/kfd')\n"
+    env = {k: v for k, v in os.environ.items() if k != "WORLD_SIZE"}
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "cannot count the node's GPUs" in r.stderr and "torch touched" not in r.stderr
+
+
+def test_count_gpus_from_kfd_topology(tmp_path):
+    """Without amdsmi, the GPU count comes from the KFD topology (nodes with SIMDs), limited by the
+    visibility variables; torch is never imported for it."""
+    import subprocess
+    import sys
+
+    for i, simds in enumerate((0, 1024, 1024, 0, 1024)):
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count 16\nsimd_count {simds}\nmax_waves_per_simd 8\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _NO_GPU_RUNTIME.replace("ROOT", repr(root)) + f"print(bench.count_gpus({str(tmp_path)!r}))\n"
+    env = {k: v for k, v in os.environ.items() if k not in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES",
+                                                             "CUDA_VISIBLE_DEVICES")}
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "3", r.stderr
+    r = subprocess.run([sys.executable, "-c", code], env=dict(env, HIP_VISIBLE_DEVICES="0,1"), capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "2", r.stderr
+
+
 def _bench_shard_rank(rank, world, port, name, R, q):
     """One rank of bench.py's N > 1 verification on CPU: the rank's global reports [r R, (r+1) R) of the
     cyclic pool tiling (here prepared by the oracle instead of the engine), its shard record checked

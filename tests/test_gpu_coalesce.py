@@ -122,7 +122,8 @@ def test_64_threads_of_100_report_jobs_two_tasks():
         assert tampered > 0
         m = engs[0].memory()
         assert m["coalesced_jobs"] == 64 * jobs_per_thread
-        assert m["coalesced_launches"] < m["coalesced_jobs"]  # jobs shared launches
+        # the jobs shared launches at scale: closed-loop callers gather into few launches per round trip
+        assert m["coalesced_jobs"] >= 8 * m["coalesced_launches"], m
         assert m["resident_batches"] == 0 and engs[1].memory()["resident_batches"] == 0
     finally:
         for e in engs:
@@ -315,5 +316,51 @@ def test_two_engines_share_the_arena_pipelined_calls():
         assert m["last_pipelines"] >= 1
         assert m["arena_reuses"] > 0  # later launches reuse the first ones' staging
     finally:
+        for e in engs:
+            e.close()
+
+
+def test_mixed_k1_launch_two_verify_keys():
+    """A coalesced helper launch past one lane-split K1 wave per SIMD takes the mixed K1 (the first
+    round_reports / 4 reports lane-split on the lane's stream, the rest as lane pairs on a side stream,
+    prep_core / bufs_tail). With jobs of two tasks in that launch, every report of the tail must still use its
+    own task's verify key: two 24,000-report jobs of engines with different keys (48,000 reports, past the
+    32,768-report split on MI355X and under a K1 round's half), gathered into ONE launch (debug option 7), each
+    equal to the oracle."""
+    v = Prio3.sum_vec(4, 50, 7)
+    vks = [bytes(range(16)), bytes(range(40, 56))]
+    K, n = 1024, 24000
+    pools = [_pool(v, vk, K, seed=900 + k, tamper_every=37) for k, vk in enumerate(vks)]
+    engs = [HelperEngine(v, vk) for vk in vks]
+    try:
+        for e in engs:
+            e.coalesce(True, window_us=1_000_000)
+        engs[0].debug(7, 2)  # the gather waits for both jobs (one launch of 48,000 reports)
+        m0 = engs[0].memory()
+        out = {}
+
+        def worker(k):
+            orc, nonces, ps, his, lps, want = pools[k]
+            idx = (311 * k + np.arange(n)) % K
+            r = engs[k].helper_initialized_batch(nonces[idx], ps[idx], his[idx], lps[idx])
+            out[k] = (idx, r.verdicts.copy(), r.prep_msgs.copy(), engs[k].aggregate_records(r.batch_id, n)[0])
+            engs[k].release(r.batch_id)
+
+        _run_threads(worker, 2)
+        m1 = engs[0].memory()
+        assert m1["coalesced_launches"] - m0["coalesced_launches"] == 1
+        assert m1["coalesced_reports"] - m0["coalesced_reports"] == 2 * n
+        for k in range(2):
+            orc, nonces, ps, his, lps, want = pools[k]
+            idx, verdicts, msgs, rec = out[k]
+            np.testing.assert_array_equal(verdicts, want["verdicts"][idx], err_msg=f"task {k}")
+            fin = want["verdicts"][idx] == 0
+            assert (~fin).sum() > 0 and fin.sum() > 0
+            np.testing.assert_array_equal(msgs[fin], want["prep_msgs"][idx][fin], err_msg=f"task {k}")
+            agg, cnt, cs = rec
+            exp_agg, exp_cnt, exp_cs = _record(orc, want, nonces, list(idx))
+            assert (cnt, cs, agg) == (exp_cnt, exp_cs, exp_agg), f"task {k}"
+    finally:
+        engs[0].debug(7, 0)
         for e in engs:
             e.close()
