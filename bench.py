@@ -158,6 +158,48 @@ def pmc_traffic(kernel: str, reports_per_launch: float):
         f"{wl['reports_per_launch']}-report launches"
 
 
+# PMC summaries of the secondary configs (scripts/gpu_pmc_r06_configs.sh): one rocprofv3 kernel trace and
+# separate --pmc passes over tools/bench_configs.py steps of that config
+CONFIG_PMC_SUMMARIES = {"configs[1]": os.path.join(ROOT, "profiles", "r06_sum32_pmc_summary.json"),
+                        "configs[2]": os.path.join(ROOT, "profiles", "r06_hist_pmc_summary.json")}
+
+
+def stage_roofline(summary_path: str, prefix: str, ms_per_launch: float, reports_per_launch: float, stage: str) -> dict:
+    """A stage's own VALU-issue roofline from a committed PMC summary: the instructions of the stage's kernels
+    (names starting with `prefix`: jx::xof for K1, jx::flp for K3) per report (SQ_INSTS_VALU x 64 lanes /
+    the summary's reports per launch) x this run's reports per launch / this run's HIP-event stage time per
+    launch, over the 78.6 T int32 issue peak; frac_pmc_run is the summary's own instructions / rocprof durations.
+    None (with a reason) when the summary is missing or was taken on other kernel sources."""
+    try:
+        d = json.load(open(summary_path))
+    except (OSError, ValueError) as e:
+        return {"frac": None, "note": f"no PMC summary: {e}"}
+    src = os.path.relpath(summary_path, ROOT)
+    wl = d.get("workload", {})
+    if wl.get("sources_digest") != sources_digest() or not wl.get("reports_per_launch"):
+        return {"frac": None, "source": src, "note": "PMC summary was taken on other kernel sources"}
+    ks = {k: e for k, e in d.get("kernels", {}).items() if k.startswith(prefix) and "SQ_INSTS_VALU" in e.get("pmc", {})}
+    if not ks or not ms_per_launch:
+        return {"frac": None, "source": src, "note": f"no {prefix}* kernel with SQ_INSTS_VALU in the summary"}
+    rpl = wl["reports_per_launch"]
+    # per launch: every kernel of the stage runs once per launch (per-dispatch averages)
+    insts = sum(e["pmc"]["SQ_INSTS_VALU"] for e in ks.values())
+    ns = sum(e["avg_ns"] for e in ks.values())
+    lane_ops_per_report = insts * 64 / rpl
+    ach = lane_ops_per_report * reports_per_launch / (ms_per_launch * 1e-3) / 1e12
+    run = insts * 64 / (ns * 1e-9) / 1e12
+    clk = [e.get("clock_GHz") for e in ks.values() if e.get("clock_GHz")]
+    return {"bound": "valu", "stage": stage, "kernels": sorted(ks), "achieved": round(ach, 3),
+            "peak": round(VALU_PEAK_TOPS, 2), "unit": "TOP/s int32 lane-op issue", "frac": round(ach / VALU_PEAK_TOPS, 4),
+            "frac_pmc_run": round(run / VALU_PEAK_TOPS, 4), "ms_per_launch": ms_per_launch,
+            "pmc_ms_per_launch": round(ns / 1e6, 3), "reports_per_launch": reports_per_launch,
+            "lane_ops_per_report": round(lane_ops_per_report, 1), "clock_GHz_pmc": round(max(clk), 3) if clk else None,
+            "valu_util_pmc": round(max(e.get("valu_util", 0) for e in ks.values()), 3),
+            "hbm_bytes_per_report": round(sum(e.get("hbm_bytes_per_report", 0) for e in ks.values()), 1),
+            "source": src, "note": "PMC SQ_INSTS_VALU x 64 per report (source) x reports / this run's HIP-event stage "
+                                   "time per launch; frac_pmc_run: the summary's instructions / its rocprof durations"}
+
+
 POOL_BLOCK = 256  # pool reports per stored block aggregate (CyclicPool prefix sums)
 
 
@@ -771,6 +813,12 @@ def secondary_configs(cpu: dict, threads: int) -> dict:
         t = time.perf_counter()
         r = BC.run(name, v, fn, R, 4096, nsteps, 1, 3.0, threads, cpu)
         r["roofline"] = issue_roofline(v, "helper", R, r["kernels"])
+        if key in CONFIG_PMC_SUMMARIES:  # each stage's own PMC-counted issue rate (K1 and K3)
+            kk = r["kernels"]
+            r["k1_roofline"] = stage_roofline(CONFIG_PMC_SUMMARIES[key], "jx::xof", kk["k1_ms_per_launch"],
+                                              kk["reports_per_launch"], "K1 (XOF)")
+            r["k3_roofline"] = stage_roofline(CONFIG_PMC_SUMMARIES[key], "jx::flp", kk["k3_ms_per_launch"],
+                                              kk["reports_per_launch"], "K3 (FLP)")
         r["driver_seconds"] = round(time.perf_counter() - t, 1)
         sec[key] = r
         log(f"{key}: {r['value']:.0f} reports/s verified={r['verified']} ({r['driver_seconds']} s)")
@@ -812,6 +860,10 @@ def job_granularity(threads: int) -> dict:
     v = Prio3.sum_vec(8, 1000, 88)
     vk = bytes(range(16))
     pool = BJ.make_pool(v, vk, 2048, threads)
+    # the same jobs from HPKE-sealed report shares (1,024 of the pool; 2 % corrupted ciphertexts, 1 % unknown config)
+    K = 1024
+    sub = tuple(a[:K] for a in pool[:4]) + ({k: x[:K] for k, x in pool[4].items() if isinstance(x, np.ndarray)},)
+    epool, enc = BJ.make_enc_pool(v, sub)
     BJ.build_driver()
     keys = ("reports_per_s", "prep_ms_p50", "prep_ms_p99", "jobs", "jobs_per_launch", "device_ms", "verified", "error")
     shapes = {}
@@ -821,15 +873,27 @@ def job_granularity(threads: int) -> dict:
             for mode in ("coalesce", "direct"):
                 r = BJ.run_case_cpp(v, vk, pool, 100, T, 2.0, mode, 0, tmp)
                 shapes[T][mode] = {k: r.get(k) for k in keys if k in r}
+            r = BJ.run_case_cpp(v, vk, epool, 100, T, 2.0, "coalesce", 0, tmp, enc=enc)
+            shapes[T]["encrypted"] = {k: r.get(k) for k in keys if k in r}
+            base = shapes[T]["coalesce"].get("reports_per_s") or 0
+            shapes[T]["encrypted"]["ratio_to_prepare_only"] = \
+                round((r.get("reports_per_s") or 0) / base, 3) if base else None
     ok = all(x.get("verified") for sh in shapes.values() for x in sh.values())
     res = {"metric": "helper reports/sec at Janus's job size: 100-report Prio3SumVec 8x1000/88 jobs from 64 threads on "
                      "one engine (prep_init+prep_next+aggregate per job)",
            "value": shapes[64]["coalesce"].get("reports_per_s"), "unit": "reports/s", "coalesced": shapes[64]["coalesce"],
            "one_call_at_a_time": shapes[64]["direct"],
-           "ten_workers": {"threads": 10, "coalesced": shapes[10]["coalesce"], "one_call_at_a_time": shapes[10]["direct"]},
+           "encrypted": shapes[64]["encrypted"],
+           "ten_workers": {"threads": 10, "coalesced": shapes[10]["coalesce"], "one_call_at_a_time": shapes[10]["direct"],
+                           "encrypted": shapes[10]["encrypted"]},
+           "encrypted_note": "the same jobs from HPKE-sealed report shares (jx_helper_prep_encrypted_batch: X25519 "
+                             "decap, key schedule, AES-128-GCM open, PlaintextInputShare decode inside the coalesced "
+                             "launch; 2 % corrupted ciphertexts, 1 % unknown config ids), every job's verdicts, prep "
+                             "messages and open statuses and the aggregate verified",
            "verified": ok, "driver_seconds": round(time.perf_counter() - t, 1)}
-    log(f"jobs: 64 threads coalesced {res['value']} reports/s (one call at a time {shapes[64]['direct'].get('reports_per_s')}); "
-        f"10 threads {shapes[10]['coalesce'].get('reports_per_s')} / {shapes[10]['direct'].get('reports_per_s')}; "
+    log(f"jobs: 64 threads coalesced {res['value']} reports/s (one call at a time {shapes[64]['direct'].get('reports_per_s')}, "
+        f"encrypted {shapes[64]['encrypted'].get('reports_per_s')}); 10 threads {shapes[10]['coalesce'].get('reports_per_s')} "
+        f"/ {shapes[10]['direct'].get('reports_per_s')} / encrypted {shapes[10]['encrypted'].get('reports_per_s')}; "
         f"verified={ok} ({res['driver_seconds']} s)")
     return res
 

@@ -10,7 +10,10 @@
  * next per-report CPU cost (X25519 + key schedule + AEAD per report).
  *
  * Conventions as in jx_prio3.h: int32 status (0 = OK), caller-owned buffers, one context per
- * (keypair, application info, GPU), not re-entrant.
+ * (keypair, application info, GPU). Calls on one context from several threads are serialized (a mutex per
+ * context); jx_hpke_last_error returns the calling thread's last failure. The host-buffer open takes its
+ * device buffers from the device's arena (shared with the prepare engines) and synchronizes only the
+ * context's stream. jx_helper_prep_encrypted_batch (jx_prio3.h) opens inside the prepare launch instead.
  *  - encs:        n x 32 bytes (HpkeCiphertext.encapsulated_key)
  *  - cts:         ciphertexts (payload || 16-byte tag) back to back; ct_offsets[n + 1], ciphertext i
  *                 is [ct_offsets[i], ct_offsets[i+1]) and at least 16 bytes

@@ -56,6 +56,8 @@
 
 #include <stdint.h>
 
+#include "jx_hpke.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -79,6 +81,27 @@ extern "C" {
 /* Leader only: the helper answered PrepareStepResult::Reject for this report (label
  * helper_step_failure, aggregation_job_driver.rs:646-660). */
 #define JX_HELPER_STEP_FAILURE 5
+/* Helper, encrypted inputs only: the report's input share did not open or decode; its out_open_status byte
+ * names why (not a prepare failure: the report never reached helper_initialized). */
+#define JX_OPEN_FAILURE 6
+
+/* Open status of an encrypted report share (jx_helper_prep_encrypted_batch out_open_status): the checks of
+ * the helper's loop before helper_initialized, in its order (aggregator/src/aggregator.rs:1781-1910), with the
+ * PrepareError each goes on the wire as and its janus_step_failures label. */
+#define JX_OPEN_OK 0
+#define JX_OPEN_HPKE_DECRYPT_ERROR 1         /* HpkeDecryptError, "decrypt_failure" */
+#define JX_OPEN_PLAINTEXT_DECODE_FAILURE 2   /* InvalidMessage, "plaintext_input_share_decode_failure" */
+#define JX_OPEN_DUPLICATE_EXTENSION 3        /* InvalidMessage, "duplicate_extension" */
+#define JX_OPEN_UNEXPECTED_TASKPROV 4        /* InvalidMessage, "unexpected_taskprov_extension" */
+#define JX_OPEN_MISSING_TASKPROV 5           /* InvalidMessage, "missing_or_malformed_taskprov_extension" */
+#define JX_OPEN_INPUT_SHARE_DECODE_FAILURE 6 /* InvalidMessage, "input_share_decode_failure" */
+#define JX_OPEN_UNKNOWN_CONFIG 7             /* HpkeUnknownConfigId, "unknown_hpke_config_id" */
+/* key_index values besides keypair indices */
+#define JX_KEY_NONE 0xFF      /* no keypair (first: the config id is unknown; second: no fallback) */
+#define JX_KEY_MALFORMED 0xFE /* first only: the encapsulated key is not 32 bytes (HpkeDecryptError) */
+#define JX_ENC_MAX_KEYPAIRS 8
+/* flags */
+#define JX_ENC_REQUIRE_TASKPROV 1u /* the task is provisioned by taskprov (aggregator.rs:1869-1879) */
 
 /* Prio3 instance, mirroring janus_core::vdaf::VdafInstance (core/src/vdaf.rs:65-108).
  * algo_id: 0 Prio3Count, 1 Prio3Sum{bits}, 2 Prio3SumVec{bits,length,chunk_length},
@@ -163,6 +186,15 @@ typedef struct {
   uint64_t coalesce_enqueue_us;
   uint64_t coalesce_device_us;
   uint64_t arena_cross_stream_waits; /* check-outs that had to wait for another stream's work */
+  /* the coalescer's pinned host rows (all its lanes; released after 2 s without jobs) and its launches / jobs
+   * by role (one gathering lane per role: leader and helper jobs never close each other's gathers) */
+  uint64_t coalesce_pinned_bytes;
+  uint64_t coalesced_helper_launches;
+  uint64_t coalesced_helper_jobs;
+  uint64_t coalesced_leader_launches;
+  uint64_t coalesced_leader_jobs;
+  uint64_t coalesced_encrypted_jobs;  /* helper jobs whose input shares were opened inside the launch */
+  uint64_t arena_frees;               /* slabs the arena returned to the device (trims) */
 } jx_memory_stats;
 int32_t jx_engine_memory(const jx_engine* e, jx_memory_stats* out);
 
@@ -183,6 +215,30 @@ int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, co
                              const uint8_t* helper_input_shares, const uint8_t* leader_prep_shares,
                              uint8_t* out_prep_msgs, uint8_t* out_verdicts, uint8_t* out_output_shares,
                              uint64_t* out_batch_id);
+/* The same prepare for report shares still under HPKE, the helper's whole per-report loop up to
+ * helper_initialized (aggregator/src/aggregator.rs:1763-1967): on the device, report i's encrypted input share
+ * is opened with keypairs[key_index[2i]] and, if that fails to decrypt, keypairs[key_index[2i + 1]] (the
+ * task's keypair, then the global one for the same config id, :1807-1820), the PlaintextInputShare is decoded
+ * and its extensions checked (:1834-1893), its payload decoded as the helper input share (:1895-1910), and the
+ * report prepared in the same launch (coalesced with other jobs like jx_helper_prep_batch). A report that fails
+ * before helper_initialized gets verdict JX_OPEN_FAILURE and out_open_status[i] (JX_OPEN_*); every other
+ * report gets JX_OPEN_OK and its verdict as from jx_helper_prep_batch.
+ *   times[n]            ReportMetadata.time (seconds); InputShareAad = task_id || id || time || public share
+ *   task_id             32 bytes
+ *   keypairs            nkeypairs (<= JX_ENC_MAX_KEYPAIRS) HPKE contexts on the engine's device, created with
+ *                       the input-share application info (Label::InputShare, Client -> Helper)
+ *   key_index[n x 2]    per report: first keypair, fallback keypair (JX_KEY_NONE / JX_KEY_MALFORMED above)
+ *   encs[n x 32]        HpkeCiphertext.encapsulated_key
+ *   payloads            ciphertexts back to back; report i's is [payload_offsets[i], payload_offsets[i+1])
+ *   flags               JX_ENC_REQUIRE_TASKPROV or 0
+ * Public shares are fixed-length rows: a report whose public share has another length cannot go here (the
+ * caller opens it alone and fails it with public_share_decode_failure, :1912-1925). out_open_status nullable. */
+int32_t jx_helper_prep_encrypted_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint64_t* times,
+                                       const uint8_t* public_shares, const uint8_t task_id[32],
+                                       jx_hpke* const* keypairs, uint32_t nkeypairs, const uint8_t* key_index,
+                                       const uint8_t* encs, const uint8_t* payloads, const uint64_t* payload_offsets,
+                                       uint32_t flags, const uint8_t* leader_prep_shares, uint8_t* out_prep_msgs,
+                                       uint8_t* out_verdicts, uint8_t* out_open_status, uint64_t* out_batch_id);
 /* Handle of the most recently prepared batch if it is still resident (0 otherwise). */
 int32_t jx_engine_batch_id(const jx_engine* e, uint64_t* batch_id);
 /* Resident batches and the device bytes they hold (either pointer nullable). */

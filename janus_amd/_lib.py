@@ -23,7 +23,7 @@ EXPORTED_SYMBOLS = (
     "jx_shard_record_combine_device", "jx_engine_sync", "jx_engine_stream", "jx_engine_timing",
     "jx_engine_timing_read", "jx_engine_debug", "jx_status_str", "jx_last_error",
     "jx_engine_wait_stream", "jx_engine_join_stream", "jx_engine_wait_event", "jx_engine_record_event",
-    "jx_engine_memory", "jx_engine_coalesce", "jx_leader_prep_init_device_ex",
+    "jx_engine_memory", "jx_engine_coalesce", "jx_leader_prep_init_device_ex", "jx_helper_prep_encrypted_batch",
 )
 
 _lib = None
@@ -39,7 +39,9 @@ class JxMemoryStats(ctypes.Structure):
         "resident_batches", "batch_bytes", "arena_budget", "arena_allocated", "arena_in_use", "arena_peak",
         "arena_allocs", "arena_reuses", "arena_waits", "arena_engines", "last_pipelines", "coalesced_launches",
         "coalesced_jobs", "coalesced_reports", "coalesce_window_us", "coalesce_gather_us", "coalesce_copy_us",
-        "coalesce_enqueue_us", "coalesce_device_us", "arena_cross_stream_waits")]
+        "coalesce_enqueue_us", "coalesce_device_us", "arena_cross_stream_waits", "coalesce_pinned_bytes",
+        "coalesced_helper_launches", "coalesced_helper_jobs", "coalesced_leader_launches", "coalesced_leader_jobs",
+        "coalesced_encrypted_jobs", "arena_frees")]
 
 
 class EngineError(RuntimeError):
@@ -72,6 +74,8 @@ def load():
         "jx_engine_sizes": (i32, [vp, P(u32), P(u32), P(u32), P(u32), P(u32), P(u32)]),
         "jx_engine_set_capacity": (i32, [vp, u64]),
         "jx_helper_prep_batch": (i32, [vp, u64, u8p, u8p, u8p, u8p, u8p, u8p, u8p, P(u64)]),
+        "jx_helper_prep_encrypted_batch": (i32, [vp, u64, u8p, P(u64), u8p, u8p, P(vp), u32, u8p, u8p, u8p, P(u64),
+                                                  u32, u8p, u8p, u8p, u8p, P(u64)]),
         "jx_engine_batch_id": (i32, [vp, P(u64)]),
         "jx_engine_batches": (i32, [vp, P(u64), P(u64)]),
         "jx_batch_release": (i32, [vp, u64]),

@@ -1,9 +1,9 @@
 """Helper aggregate-init over a batch of PrepareInits — the hot loop of Janus, batched.
 
 Mirror of VdafOps::handle_aggregate_init_generic, /root/reference/aggregator/src/
-aggregator.rs:1712-2161, minus what stays on the host and is out of scope here
-(HPKE open :1772-1832, the datastore transaction :2051-2156). Per report, the
-reference:
+aggregator.rs:1712-2161, minus the datastore transaction itself (:2051-2156).
+handle_aggregate_init_encrypted starts from the encrypted report shares (the HPKE open runs inside the
+prepare launch on the GPU); handle_aggregate_init from opened ones. Per report, the reference:
   * decodes the helper input share and public share -> PrepareError::InvalidMessage on
     failure (:1896-1926),
   * runs helper_initialized + evaluate (:1945-1967); any PingPongError becomes
@@ -93,15 +93,14 @@ def handle_aggregate_init(engine: HelperEngine, prepare_inits: list[PrepareInit]
         batch_idx.append(i)
     finished = np.zeros(n, bool)
     m = len(batch_idx)
+    res = None
+    accept = np.zeros(m, np.uint8)
     if m:
         nonces = np.frombuffer(b"".join(ids[i] for i in batch_idx), np.uint8).reshape(m, 16)
         ps = np.frombuffer(b"".join(prepare_inits[i].report_share.public_share for i in batch_idx), np.uint8)
         his = np.frombuffer(b"".join(input_shares[i] for i in batch_idx), np.uint8)
         lps = np.frombuffer(b"".join(prepare_inits[i].message.prep_share for i in batch_idx), np.uint8)
         res = engine.helper_initialized_batch(nonces, ps, his, lps)
-        accept = np.zeros(m, np.uint8)
-        row_seg = [int(segments[i]) if segments else 0 for i in batch_idx]
-        seg = np.zeros(m, np.uint32)
         for j, i in enumerate(batch_idx):
             verdict = int(res.verdicts[j])
             if verdict != FINISHED:
@@ -113,30 +112,43 @@ def handle_aggregate_init(engine: HelperEngine, prepare_inits: list[PrepareInit]
                 continue
             results[i] = PrepareStepResult(0, message=PingPongMessage.finish(res.prep_msgs[j].tobytes()))
             accept[j] = 1
-            seg[j] = segments[i] if segments else 0
             finished[i] = True
-        if writer is None:
-            with engine.resident(res.batch_id):  # accumulate consumes the batch; on an error it is released
-                engine.accumulate(m, accept, seg, batch_id=res.batch_id)
-    if writer is not None:
-        times = [(int(segments[i]) if segments else 0, p.report_share.metadata.time)
-                 for i, p in enumerate(prepare_inits)] + list(extra_report_times)
-        if m:
-            idx, seg_ids = _dense(row_seg)
-            try:
-                collected = writer.write_job(engine, res.batch_id, m, accept, idx, seg_ids, times,
-                                             initial_write=True, terminal=True, inject_failures=inject_tx_failures)
-            finally:
-                engine.release(res.batch_id)
-        else:
-            collected = writer.write_job(engine, 0, 0, None, None, [], times, initial_write=True, terminal=True,
-                                         inject_failures=inject_tx_failures)
-        for j, i in enumerate(batch_idx):  # fail_report_aggregations_for_collected_batches
-            if finished[i] and row_seg[j] in collected:
-                finished[i] = False
-                results[i] = PrepareStepResult(2, error=PrepareError.BatchCollected)
+    times = [(int(segments[i]) if segments else 0, p.report_share.metadata.time)
+             for i, p in enumerate(prepare_inits)] + list(extra_report_times)
+    _write_job(engine, res.batch_id if m else 0, batch_idx, accept, segments, writer, times, inject_tx_failures,
+               finished, results)
     responses = [PrepareResp(ids[i], results[i]) for i in range(n)]
     return AggregateInitOutcome(responses, finished, failures)
+
+
+def _write_job(engine: HelperEngine, batch_id: int, batch_idx: list[int], accept: np.ndarray, segments, writer,
+               times, inject_tx_failures: int, finished: np.ndarray, results: list) -> None:
+    """Accumulate a helper job's accepted rows (engine row j = report batch_idx[j]): with a writer, as
+    per-batch-identifier deltas in one retryable transaction (aggregation_job_writer.rs:476-553, 608-708; the
+    batch is released after), else into the engine's running aggregations (which consume the batch). Reports of
+    an already collected batch fail with BatchCollected."""
+    m = len(batch_idx)
+    row_seg = [int(segments[i]) if segments else 0 for i in batch_idx]
+    if writer is None:
+        if m:
+            seg = np.array(row_seg, np.uint32)
+            with engine.resident(batch_id):  # accumulate consumes the batch; on an error it is released
+                engine.accumulate(m, accept, seg, batch_id=batch_id)
+        return
+    if m:
+        idx, seg_ids = _dense(row_seg)
+        try:
+            collected = writer.write_job(engine, batch_id, m, accept, idx, seg_ids, times,
+                                         initial_write=True, terminal=True, inject_failures=inject_tx_failures)
+        finally:
+            engine.release(batch_id)
+    else:
+        collected = writer.write_job(engine, 0, 0, None, None, [], times, initial_write=True, terminal=True,
+                                     inject_failures=inject_tx_failures)
+    for j, i in enumerate(batch_idx):  # fail_report_aggregations_for_collected_batches
+        if finished[i] and row_seg[j] in collected:
+            finished[i] = False
+            results[i] = PrepareStepResult(2, error=PrepareError.BatchCollected)
 
 
 # ----------------------------------------------------------------------------- leader side
@@ -318,68 +330,157 @@ def leader_process_helper_response(engine: HelperEngine, step: LeaderStep, prepa
 
 def handle_aggregate_init_encrypted(engine: HelperEngine, opener, hpke_config_id: int, task_id: bytes,
                                     prepare_inits: list[PrepareInit], segments: list[int] | None = None,
-                                    replayed: set[bytes] | None = None, writer=None) -> AggregateInitOutcome:
-    """The helper's aggregate-init loop including the decryption of the report shares
-    (aggregator.rs:1763-1893): one batched HPKE open on the GPU (janus_amd.hpke.HpkeOpener) for
-    the whole request, then PlaintextInputShare decoding and extension checks on the host, then
-    handle_aggregate_init for the reports that survive. Failures map as in the reference:
-    unknown HPKE config id -> HpkeUnknownConfigId, HPKE failure -> HpkeDecryptError, plaintext
-    decode failure / duplicate or unexpected taskprov extension -> InvalidMessage."""
+                                    replayed: set[bytes] | None = None, writer=None, global_keypairs=None,
+                                    require_taskprov: bool = False, report_deadline: int | None = None,
+                                    inject_tx_failures: int = 0) -> AggregateInitOutcome:
+    """The helper's aggregate-init loop from the encrypted report shares (aggregator.rs:1763-2013), with the
+    HPKE open inside the prepare launch (jx_helper_prep_encrypted_batch; coalesced with other jobs when the
+    engine coalesces): per report, the task's keypair (opener, config id hpke_config_id) and then the
+    aggregator's global keypair for the report's config id (global_keypairs: {config_id: HpkeOpener}) are
+    tried (:1781-1832), the PlaintextInputShare is decoded and its extensions checked (:1834-1893), the payload
+    decoded as the helper input share (:1895-1910), the public share decoded (:1912-1925), reports from after
+    report_deadline rejected (:1929-1940), then helper_initialized + evaluate (:1945-1967). Failures map as in
+    the reference: HpkeUnknownConfigId, HpkeDecryptError, InvalidMessage (plaintext / extension / input share /
+    public share), ReportTooEarly, VdafPrepError. A report whose public share has the wrong length cannot ride
+    the fixed-stride device rows: it is opened alone (janus_amd.hpke) and fails with InvalidMessage unless an
+    earlier check fails it first."""
+    from .engine import KEY_MALFORMED, KEY_NONE, OPEN_STATUS
+
+    v = engine.vdaf
+    n = len(prepare_inits)
+    ids = [p.report_share.metadata.report_id for p in prepare_inits]
+    if len(set(ids)) != n:  # aggregator.rs:1750-1758
+        raise ValueError("aggregate request contains duplicate report IDs (invalidMessage)")
+    globals_ = dict(global_keypairs or {})
+    keypairs = [opener]
+    slot: dict[int, int] = {}
+
+    def key_slot(k) -> int:
+        if id(k) not in slot:
+            slot[id(k)] = len(keypairs) if k is not opener else 0
+            if k is not opener:
+                keypairs.append(k)
+        return slot[id(k)]
+
+    slot[id(opener)] = 0
+    failures: Counter = Counter()
+    results: list[PrepareStepResult | None] = [None] * n
+    rows: list[int] = []           # reports on the device, in row order
+    odd: list[int] = []            # public share of the wrong length: opened alone
+    key_index = []
+    for i, pi in enumerate(prepare_inits):
+        ct = pi.report_share.encrypted_input_share
+        task_k = opener if ct.config_id == hpke_config_id else None
+        glob_k = globals_.get(ct.config_id)
+        first, second = (task_k, glob_k) if task_k is not None else (glob_k, None)
+        if len(pi.report_share.public_share) != v.public_share_len:
+            odd.append(i)
+            continue
+        if first is None:
+            k0, k1 = KEY_NONE, KEY_NONE
+        elif len(ct.encapsulated_key) != 32:
+            k0, k1 = KEY_MALFORMED, KEY_NONE
+        else:
+            k0, k1 = key_slot(first), (key_slot(second) if second is not None else KEY_NONE)
+        if len(keypairs) > 8:
+            raise ValueError("more than JX_ENC_MAX_KEYPAIRS distinct keypairs in one request")
+        rows.append(i)
+        key_index.append((k0, k1))
+    finished = np.zeros(n, bool)
+    m = len(rows)
+    accept = np.zeros(m, np.uint8)
+    res = None
+    if m:
+        md = [prepare_inits[i].report_share.metadata for i in rows]
+        nonces = np.frombuffer(b"".join(x.report_id for x in md), np.uint8).reshape(m, 16)
+        times = np.array([x.time for x in md], np.uint64)
+        ps = np.frombuffer(b"".join(prepare_inits[i].report_share.public_share for i in rows), np.uint8)
+        encs = np.frombuffer(b"".join(
+            (lambda e: e if len(e) == 32 else bytes(32))(prepare_inits[i].report_share.encrypted_input_share
+                                                           .encapsulated_key) for i in rows), np.uint8).reshape(m, 32)
+        payloads = [prepare_inits[i].report_share.encrypted_input_share.payload for i in rows]
+        # a leader message that is not Initialize, or a prep share of the wrong length, fails inside
+        # helper_initialized, after the open: the row rides with a zero prep share and is fixed up below
+        msg_fail: dict[int, str] = {}
+        lps_rows = []
+        for j, i in enumerate(rows):
+            msg = prepare_inits[i].message
+            if msg.kind != PingPongMessage.INITIALIZE:  # PingPongError::PeerMessageMismatch
+                msg_fail[j] = "leader_ping_pong_message_mismatch"
+            elif len(msg.prep_share) != v.prep_share_len:  # PingPongError::CodecPrepShare
+                msg_fail[j] = "leader_prep_share_decode_failure"
+            lps_rows.append(msg.prep_share if j not in msg_fail else bytes(v.prep_share_len))
+        lps = np.frombuffer(b"".join(lps_rows), np.uint8)
+        res = engine.helper_initialized_encrypted_batch(nonces, times, ps, task_id, keypairs,
+                                                        np.array(key_index, np.uint8), encs, payloads, lps,
+                                                        require_taskprov=require_taskprov)
+        for j, i in enumerate(rows):
+            st = int(res.open_status[j])
+            if st:
+                label, err = OPEN_STATUS[st]
+                failures[label] += 1
+                results[i] = PrepareStepResult(2, error=PrepareError(err))
+            elif report_deadline is not None and md[j].time > report_deadline:
+                results[i] = PrepareStepResult(2, error=PrepareError.ReportTooEarly)
+            elif j in msg_fail:
+                failures[msg_fail[j]] += 1
+                results[i] = PrepareStepResult(2, error=PrepareError.VdafPrepError)
+            elif int(res.verdicts[j]) != FINISHED:
+                failures[VERDICT_LABELS[int(res.verdicts[j])]] += 1
+                results[i] = PrepareStepResult(2, error=PrepareError.VdafPrepError)
+            elif replayed and ids[i] in replayed:  # aggregator.rs:2127-2132
+                results[i] = PrepareStepResult(2, error=PrepareError.ReportReplayed)
+            else:
+                results[i] = PrepareStepResult(0, message=PingPongMessage.finish(res.prep_msgs[j].tobytes()))
+                accept[j] = 1
+                finished[i] = True
+    for i in odd:
+        results[i] = PrepareStepResult(2, error=_open_alone(prepare_inits[i], opener, hpke_config_id, globals_,
+                                                            task_id, v, require_taskprov, failures))
+    times_all = [(int(segments[i]) if segments else 0, p.report_share.metadata.time) for i, p in enumerate(prepare_inits)]
+    _write_job(engine, res.batch_id if m else 0, rows, accept, segments, writer, times_all, inject_tx_failures,
+               finished, results)
+    responses = [PrepareResp(ids[i], results[i]) for i in range(n)]
+    return AggregateInitOutcome(responses, finished, failures)
+
+
+def _open_alone(pi: PrepareInit, opener, hpke_config_id: int, globals_: dict, task_id: bytes, v, require_taskprov: bool,
+                failures: Counter) -> PrepareError:
+    """A report whose public share has the wrong length (it cannot ride the fixed-stride device rows): the
+    reference's checks in order on the host (batched HPKE open on the GPU for this one share); it always fails,
+    with public_share_decode_failure at the latest."""
     from .hpke import input_share_aad
 
-    n = len(prepare_inits)
-    failures: Counter = Counter()
-    errors: dict[int, PrepareError] = {}
-    to_open = []
-    for i, pi in enumerate(prepare_inits):
-        rs = pi.report_share
-        if rs.encrypted_input_share.config_id != hpke_config_id:
-            errors[i] = PrepareError.HpkeUnknownConfigId
-            failures["unknown_hpke_config_id"] += 1
-        else:
-            to_open.append(i)
-    opened = opener.open_batch(
-        [prepare_inits[i].report_share.encrypted_input_share.encapsulated_key for i in to_open],
-        [prepare_inits[i].report_share.encrypted_input_share.payload for i in to_open],
-        [input_share_aad(task_id, prepare_inits[i].report_share.metadata.report_id,
-                         prepare_inits[i].report_share.metadata.time, prepare_inits[i].report_share.public_share)
-         for i in to_open]) if to_open else []
-    payloads: dict[int, bytes] = {}
-    for i, pt in zip(to_open, opened):
-        if pt is None:
-            errors[i] = PrepareError.HpkeDecryptError
-            failures["decrypt_failure"] += 1
-            continue
-        try:
-            pis = PlaintextInputShare.decode(pt)
-        except CodecError:
-            errors[i] = PrepareError.InvalidMessage
-            failures["plaintext_input_share_decode_failure"] += 1
-            continue
-        types = [e.extension_type for e in pis.extensions]
-        if len(set(types)) != len(types):
-            errors[i] = PrepareError.InvalidMessage
-            failures["duplicate_extension"] += 1
-            continue
-        if EXTENSION_TASKPROV in types:  # taskprov is not enabled for these tasks
-            errors[i] = PrepareError.InvalidMessage
-            failures["unexpected_taskprov_extension"] += 1
-            continue
-        payloads[i] = pis.payload
-    keep = [i for i in range(n) if i in payloads]
-    # every report aggregation of the request is written, including the ones that failed to open
-    dropped = [(int(segments[i]) if segments else 0, prepare_inits[i].report_share.metadata.time)
-               for i in range(n) if i not in payloads]
-    inner = handle_aggregate_init(engine, [prepare_inits[i] for i in keep], [payloads[i] for i in keep],
-                                  [segments[i] for i in keep] if segments else None, replayed, writer, dropped)
-    failures.update(inner.step_failures)
-    by_row = dict(zip(keep, range(len(keep))))
-    finished = np.zeros(n, bool)
-    responses = []
-    for i, pi in enumerate(prepare_inits):
-        if i in errors:
-            responses.append(PrepareResp(pi.report_share.metadata.report_id, PrepareStepResult(2, error=errors[i])))
-        else:
-            responses.append(inner.responses[by_row[i]])
-            finished[i] = inner.finished[by_row[i]]
-    return AggregateInitOutcome(responses, finished, failures)
+    rs = pi.report_share
+    ct = rs.encrypted_input_share
+    keys = [k for k in ((opener if ct.config_id == hpke_config_id else None), globals_.get(ct.config_id)) if k]
+    if not keys:
+        failures["unknown_hpke_config_id"] += 1
+        return PrepareError.HpkeUnknownConfigId
+    aad = input_share_aad(task_id, rs.metadata.report_id, rs.metadata.time, rs.public_share)
+    pt = None
+    for k in keys:
+        pt = k.open_batch([ct.encapsulated_key], [ct.payload], [aad])[0]
+        if pt is not None:
+            break
+    if pt is None:
+        failures["decrypt_failure"] += 1
+        return PrepareError.HpkeDecryptError
+    try:
+        pis = PlaintextInputShare.decode(pt)
+    except CodecError:
+        failures["plaintext_input_share_decode_failure"] += 1
+        return PrepareError.InvalidMessage
+    types = [e.extension_type for e in pis.extensions]
+    if len(set(types)) != len(types):
+        failures["duplicate_extension"] += 1
+    elif require_taskprov and not any(e.extension_type == EXTENSION_TASKPROV and not e.extension_data
+                                      for e in pis.extensions):
+        failures["missing_or_malformed_taskprov_extension"] += 1
+    elif not require_taskprov and EXTENSION_TASKPROV in types:
+        failures["unexpected_taskprov_extension"] += 1
+    elif len(pis.payload) != v.helper_input_share_len:
+        failures["input_share_decode_failure"] += 1
+    else:
+        failures["public_share_decode_failure"] += 1
+    return PrepareError.InvalidMessage

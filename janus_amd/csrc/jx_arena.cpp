@@ -10,8 +10,9 @@
 // budget bounds everything the engines hold.
 //
 // Budget: JX_ARENA_GB, or 90 % of the device's memory at first use. A request that does not fit first
-// frees idle slabs, then (for per-call staging, by a caller that holds no slab) waits for another caller's
-// staging to come back; otherwise JX_E_NOMEM.
+// frees idle slabs (those whose last user has finished first; the waits and hipFree run outside the arena's
+// lock, so one trim never stalls another engine's check-out), then (for per-call staging, by a caller that
+// holds no slab) waits for another caller's staging to come back; otherwise JX_E_NOMEM.
 #include <cstdlib>
 
 #include "jx_engine_internal.h"
@@ -39,25 +40,50 @@ Arena* arena_for(int device) {
   return A;
 }
 
-static void slab_destroy(Arena* A, Slab& s) {
+// Waits for the slab's last user and frees it. Never with A->mu held: the wait can be a 100 ms K1 launch, and
+// every engine's check-outs on the device would stall behind it.
+static void slab_destroy(Slab& s) {
   if (s.ev) {
     (void)hipEventSynchronize(s.ev);  // its last user's work
     (void)hipEventDestroy(s.ev);
   }
   (void)hipFree(s.p);
-  A->allocated -= s.bytes;
-  A->frees++;
   s = Slab{};
 }
 
-// with A->mu held: free the largest idle slab
-static bool trim_one(Arena* A) {
-  if (A->free.empty()) return false;
-  auto it = std::prev(A->free.end());
-  Slab s = it->second;
-  A->free.erase(it);
-  slab_destroy(A, s);
-  return true;
+// With A->mu held: take idle slabs off the free list for destruction until `need` more bytes fit the budget
+// (need = ~0: all of them), those whose last user has finished first, largest first. Their bytes stay counted
+// in `allocated` (and in `freeing`) until free_slabs has returned them.
+static void take_idle(Arena* A, size_t need, std::vector<Slab>& dead) {
+  auto over = [&] { return need == ~(size_t)0 || A->allocated - A->freeing + need > A->budget; };
+  for (int pass = 0; pass < 2 && over(); pass++) {
+    for (auto it = A->free.end(); it != A->free.begin() && over();) {
+      --it;
+      const bool idle = !it->second.last || hipEventQuery(it->second.ev) == hipSuccess;
+      if (pass == 0 && !idle) continue;
+      dead.push_back(it->second);
+      A->freeing += it->second.bytes;
+      it = A->free.erase(it);
+    }
+    (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
+  }
+}
+
+// Destroy slabs taken by take_idle: drops the lock for the waits and frees, then accounts them.
+static void free_slabs(Arena* A, std::vector<Slab>& dead, std::unique_lock<std::mutex>& lk) {
+  if (dead.empty()) return;
+  lk.unlock();
+  size_t bytes = 0;
+  for (Slab& s : dead) {
+    bytes += s.bytes;
+    slab_destroy(s);
+  }
+  lk.lock();
+  A->allocated -= bytes;
+  A->freeing -= bytes;
+  A->frees += dead.size();
+  dead.clear();
+  A->cv.notify_all();
 }
 
 static void account_out(Arena* A, const Slab& s) {
@@ -106,7 +132,13 @@ hipError_t arena_get(Arena* A, size_t bytes, hipStream_t s, bool staging, bool m
       // after the slab's last user (a never-recorded event: no wait); on its own stream, stream order does it
       return out.last == s ? hipSuccess : hipStreamWaitEvent(s, out.ev, 0);
     }
-    while (A->allocated + bytes > A->budget && trim_one(A)) {
+    if (A->allocated + bytes > A->budget && !A->free.empty()) {  // make room from idle slabs, outside the lock
+      std::vector<Slab> dead;
+      take_idle(A, bytes, dead);
+      if (!dead.empty()) {
+        free_slabs(A, dead, lk);
+        continue;
+      }
     }
     if (A->allocated + bytes <= A->budget) {
       // the budget is reserved under the lock and the device allocation made outside it: a large hipMalloc
@@ -132,10 +164,16 @@ hipError_t arena_get(Arena* A, size_t bytes, hipStream_t s, bool staging, bool m
       (void)hipGetLastError();
       // the device (other users, torch) is fuller than the budget: give back the idle slabs and retry once
       if (!A->free.empty()) {
-        while (trim_one(A)) {
-        }
+        std::vector<Slab> dead;
+        take_idle(A, ~(size_t)0, dead);
+        free_slabs(A, dead, lk);
         continue;
       }
+    }
+    // slabs being freed by another caller come back to the budget shortly
+    if (A->freeing) {
+      A->cv.wait(lk);
+      continue;
     }
     // what is checked out holds the memory: staging comes back when its call has queued its work
     if (!may_wait || A->in_use_staging == 0) return hipErrorOutOfMemory;
@@ -159,9 +197,10 @@ void arena_put(Arena* A, Slab& slab, hipStream_t s) {
 }
 
 void arena_trim(Arena* A) {
-  std::lock_guard<std::mutex> lk(A->mu);
-  while (trim_one(A)) {
-  }
+  std::unique_lock<std::mutex> lk(A->mu);
+  std::vector<Slab> dead;
+  take_idle(A, ~(size_t)0, dead);
+  free_slabs(A, dead, lk);
 }
 
 void arena_engine_add(Arena* A) {
@@ -170,11 +209,13 @@ void arena_engine_add(Arena* A) {
 }
 
 void arena_engine_remove(Arena* A) {
-  std::lock_guard<std::mutex> lk(A->mu);
+  std::unique_lock<std::mutex> lk(A->mu);
   if (A->engines) A->engines--;
-  if (A->engines == 0)  // nothing left to reuse the idle slabs: give the memory back to the device
-    while (trim_one(A)) {
-    }
+  if (A->engines == 0) {  // nothing left to reuse the idle slabs: give the memory back to the device
+    std::vector<Slab> dead;
+    take_idle(A, ~(size_t)0, dead);
+    free_slabs(A, dead, lk);
+  }
 }
 
 hipError_t arena_big_record(Arena* A, const void* owner, hipStream_t s) {

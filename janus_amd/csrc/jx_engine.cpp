@@ -422,6 +422,13 @@ static size_t stage_layout(jx_engine* e, uint64_t cap, uint32_t fl, uint8_t* bas
   if (fl & SG_LMSG) take(e->d_in_msgs, cap * c.seed);
   if (fl & SG_VK) take(e->d_vkeys, cap * vk_row_bytes(c));
   if (fl & SG_JOBS) take(e->d_jobs, (size_t)MAX_JOBS_PER_LAUNCH * sizeof(JobSlice));
+  if (fl & SG_ENC) {
+    take(e->d_encrows, cap * sizeof(EncRow));
+    take(e->d_ct, e->enc_ct_bytes);
+    take(e->d_pt, e->enc_ct_bytes);
+    take(e->d_keys, (size_t)ENC_MAX_KEYS * sizeof(HpkeKeyRow));
+    take(e->d_status, cap);
+  }
   return off;
 }
 
@@ -437,6 +444,9 @@ static void stage_clear(jx_engine* e) {
   e->d_lis = e->d_lps_out = e->d_in_msgs = nullptr;
   e->d_vkeys = nullptr;
   e->d_jobs = nullptr;
+  e->d_encrows = nullptr;
+  e->d_ct = e->d_pt = e->d_status = nullptr;
+  e->d_keys = nullptr;
   e->cap = 0;
   e->stage_flags = 0;
 }
@@ -483,30 +493,59 @@ void Stage::release() {
 // the fused paths' output shares (engine staging)
 uint4* jxi::staging_outs(jx_engine* e) { return outs_alias_meas(e->cfg) ? e->d_meas : e->d_outs; }
 
-static int32_t get_segment(jx_engine* e, uint32_t id, Segment** out) {
-  auto it = e->segs.find(id);
-  if (it == e->segs.end()) {
-    Segment s;
-    HIPCHK(e, hipMalloc((void**)&s.agg, (size_t)e->cfg.out_len * 16));
-    HIPCHK(e, hipMalloc((void**)&s.checksum, 32));
-    HIPCHK(e, hipMalloc((void**)&s.count, 8));
-    HIPCHK(e, hipMemsetAsync(s.agg, 0, (size_t)e->cfg.out_len * 16, e->stream));
-    HIPCHK(e, hipMemsetAsync(s.checksum, 0, 32, e->stream));
-    HIPCHK(e, hipMemsetAsync(s.count, 0, 8, e->stream));
-    it = e->segs.emplace(id, s).first;
+// Per-call device scratch from the arena, handed back stream-ordered on the engine stream when it goes out of
+// scope: no hipMalloc / hipFree / stream synchronize on a call path (hipFree waits for the device, and every
+// engine's launches on it).
+namespace {
+struct Scratch {
+  jx_engine* e = nullptr;
+  Slab s;
+  Scratch() = default;
+  Scratch(const Scratch&) = delete;
+  Scratch& operator=(const Scratch&) = delete;
+  ~Scratch() {
+    if (s.p) arena_put(e->arena, s, e->stream);
   }
-  *out = &it->second;
+  uint8_t* p() const { return (uint8_t*)s.p; }
+};
+}  // namespace
+
+// may_wait: the caller holds no other staging (arena_get's rule)
+static int32_t scratch_get(jx_engine* e, size_t bytes, Scratch& out, bool may_wait = false) {
+  out.e = e;
+  const hipError_t st = arena_get(e->arena, bytes, e->stream, true, may_wait, out.s);
+  if (st == hipErrorOutOfMemory) return nomem(e, "scratch", bytes);
+  HIPCHK(e, st);
   return JX_OK;
 }
 
-static int32_t ensure_tmp(jx_engine* e, size_t bytes) {
-  if (bytes <= e->tmp_bytes) return JX_OK;
-  HIPCHK(e, hipStreamSynchronize(e->stream));
-  if (e->d_tmp) (void)hipFree(e->d_tmp);
-  e->d_tmp = nullptr;
-  e->tmp_bytes = 0;
-  HIPCHK(e, hipMalloc((void**)&e->d_tmp, bytes));
-  e->tmp_bytes = bytes;
+// Running aggregations: segment states (aggregate share | checksum | count) carved from arena slabs of
+// kSegsPerSlab states, so a new batch-aggregation id costs no device allocation on the call path (one slab per
+// kSegsPerSlab ids, held until the engine is destroyed).
+constexpr uint32_t kSegsPerSlab = 64;
+static size_t seg_state_bytes(const Cfg& c) { return align256((size_t)c.out_len * 16 + 32 + 8); }
+
+static int32_t get_segment(jx_engine* e, uint32_t id, Segment** out) {
+  auto it = e->segs.find(id);
+  if (it == e->segs.end()) {
+    const size_t sb = seg_state_bytes(e->cfg);
+    if (e->seg_slabs.empty() || e->seg_next == kSegsPerSlab) {
+      Slab sl;
+      const hipError_t st = arena_get(e->arena, sb * kSegsPerSlab, e->stream, false, false, sl);
+      if (st == hipErrorOutOfMemory) return nomem(e, "batch aggregations", sb * kSegsPerSlab);
+      HIPCHK(e, st);
+      e->seg_slabs.push_back(sl);
+      e->seg_next = 0;
+    }
+    uint8_t* m = (uint8_t*)e->seg_slabs.back().p + sb * e->seg_next++;
+    Segment s;
+    s.agg = (uint4*)m;
+    s.checksum = (uint32_t*)(m + (size_t)e->cfg.out_len * 16);
+    s.count = (unsigned long long*)(m + (size_t)e->cfg.out_len * 16 + 32);
+    HIPCHK(e, hipMemsetAsync(m, 0, sb, e->stream));
+    it = e->segs.emplace(id, s).first;
+  }
+  *out = &it->second;
   return JX_OK;
 }
 
@@ -595,7 +634,7 @@ static bool use_inplace(const jx_engine* e) { return leader_inplace(e->cfg); }
 // seeds to verdicts / msgs.
 int32_t jxi::prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* his,
                        const uint8_t* lps, uint8_t* verdicts, uint8_t* msgs, uint4* outs, const uint8_t* lis,
-                       uint8_t* lps_out, uint64_t lis_rs, const uint8_t* vkeys) {
+                       uint8_t* lps_out, uint64_t lis_rs, const uint8_t* vkeys, hipEvent_t before_flp) {
   const Cfg& c = e->cfg;
   const bool leader = lis != nullptr;
   Bufs b{};
@@ -695,6 +734,8 @@ int32_t jxi::prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const ui
       HIPCHK(e, launch_xof_slow(c, b, e->stream));
       HIPCHK(e, stage_end(e, ST_SLOW, ev));
     }
+    // the caller's upload of the rest of the leader prep shares (K1 reads only their joint-rand parts)
+    if (before_flp) HIPCHK(e, hipStreamWaitEvent(e->stream, before_flp, 0));
     HIPCHK(e, stage_begin(e, &ev));
     HIPCHK(e, launch_flp(c, b, e->stream));
     HIPCHK(e, stage_end(e, ST_FLP, ev));
@@ -733,18 +774,14 @@ static int32_t accumulate_one(jx_engine* e, const AccSrc& src, const uint8_t* d_
   return JX_OK;
 }
 
-// Upload the device pointer table (aggs, counts, checksums) of `targets` into d_ptrs. The pinned host
-// copy is double-buffered and reused only once the upload that last read it has completed, so the
-// host never waits for the call's own kernels.
-static int32_t upload_targets(jx_engine* e, const std::vector<Segment>& targets) {
+// Upload the device pointer table (aggs, counts, checksums) of `targets` into per-call scratch `tbl` (e->d_ptrs
+// points at it while it is held). The pinned host copy is double-buffered and reused only once the upload
+// that last read it has completed, so the host never waits for the call's own kernels.
+static int32_t upload_targets(jx_engine* e, const std::vector<Segment>& targets, Scratch& tbl) {
   const uint64_t S = targets.size();
-  if (e->ptrs_cap < S) {
-    HIPCHK(e, hipStreamSynchronize(e->stream));  // kernels may still read the old table
-    if (e->d_ptrs) (void)hipFree(e->d_ptrs);
-    e->d_ptrs = nullptr;
-    HIPCHK(e, hipMalloc((void**)&e->d_ptrs, 3 * S * sizeof(void*)));
-    e->ptrs_cap = S;
-  }
+  int32_t rc = scratch_get(e, 3 * S * sizeof(void*), tbl);
+  if (rc) return rc;
+  e->d_ptrs = (void**)tbl.p();
   const int k = e->ptrs_k;
   e->ptrs_k ^= 1;
   if (!e->ev_ptrs[k]) HIPCHK(e, hipEventCreateWithFlags(&e->ev_ptrs[k], hipEventDisableTiming));
@@ -790,23 +827,18 @@ static int32_t accumulate_many(jx_engine* e, const AccSrc& src, const uint8_t* d
   ns_max = ns_max > items_n + 64 ? ns_max - items_n : 64;
   if (ns_max > SEG_MAX) ns_max = SEG_MAX;
   const uint64_t wmax = items_n + (S < ns_max ? S : ns_max);
-  if (!e->d_segx) HIPCHK(e, hipMalloc((void**)&e->d_segx, (4 * SEG_MAX + 3) * sizeof(uint32_t)));
-  if (e->perm_cap < n || e->spart_wmax < wmax) HIPCHK(e, hipStreamSynchronize(e->stream));
-  if (e->perm_cap < n) {
-    if (e->d_perm) (void)hipFree(e->d_perm);
-    e->d_perm = nullptr;
-    HIPCHK(e, hipMalloc((void**)&e->d_perm, n * sizeof(uint32_t)));
-    e->perm_cap = n;
-  }
-  if (e->spart_wmax < wmax) {
-    if (e->d_items) (void)hipFree(e->d_items);
-    if (e->d_spart) (void)hipFree(e->d_spart);
-    e->d_items = nullptr;
-    e->d_spart = nullptr;
-    HIPCHK(e, hipMalloc((void**)&e->d_items, wmax * sizeof(uint4)));
-    HIPCHK(e, hipMalloc((void**)&e->d_spart, wmax * per_item));
-    e->spart_wmax = wmax;
-  }
+  // the counting-sort state, permutation, work items and partials: one per-call scratch slab (reused from the
+  // arena stream-ordered; no allocation or synchronization once warm)
+  const size_t o_segx = 0, o_perm = align256((4 * SEG_MAX + 3) * sizeof(uint32_t)),
+               o_items = o_perm + align256(n * sizeof(uint32_t)), o_spart = o_items + align256(wmax * sizeof(uint4)),
+               wbytes = o_spart + align256(wmax * per_item);
+  Scratch work;
+  int32_t rc = scratch_get(e, wbytes, work);
+  if (rc) return rc;
+  e->d_segx = (uint32_t*)(work.p() + o_segx);
+  e->d_perm = (uint32_t*)(work.p() + o_perm);
+  e->d_items = (uint4*)(work.p() + o_items);
+  e->d_spart = (uint64_t*)(work.p() + o_spart);
   uint64_t grid = (n + 255) / 256;
   if (grid > SELECT_WGS) grid = SELECT_WGS;
   for (uint64_t s0 = 0; s0 < S; s0 += ns_max) {
@@ -881,30 +913,26 @@ static int32_t accumulate_into(jx_engine* e, const AccSrc& src, const uint8_t* d
                                const std::vector<Segment>& targets, bool uploaded = false) {
   if (src.n == 0 || targets.empty()) return JX_OK;
   if (targets.size() == 1 || !d_dense) return accumulate_one(e, src, d_mask, d_dense, targets[0]);
+  Scratch tbl;
   if (!uploaded) {
-    int32_t rc = upload_targets(e, targets);
+    int32_t rc = upload_targets(e, targets, tbl);
     if (rc) return rc;
   }
   return accumulate_many(e, src, d_mask, d_dense, targets.size());
 }
 
-// Per-call delta aggregations (zeroed): ns contiguous segment states in d_delta.
-static int32_t delta_targets(jx_engine* e, uint32_t ns, std::vector<Segment>& out) {
+// Per-call delta aggregations (zeroed): ns contiguous segment states in per-call scratch `d`.
+static int32_t delta_targets(jx_engine* e, uint32_t ns, std::vector<Segment>& out, Scratch& d) {
   const size_t agg_b = (size_t)ns * e->cfg.out_len * 16, bytes = agg_b + (size_t)ns * 8 + (size_t)ns * 32;
-  if (bytes > e->delta_bytes) {
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    if (e->d_delta) (void)hipFree(e->d_delta);
-    e->d_delta = nullptr;
-    e->delta_bytes = 0;
-    HIPCHK(e, hipMalloc((void**)&e->d_delta, bytes));
-    e->delta_bytes = bytes;
-  }
-  HIPCHK(e, hipMemsetAsync(e->d_delta, 0, bytes, e->stream));
+  int32_t rc = scratch_get(e, bytes, d);
+  if (rc) return rc;
+  uint8_t* base = d.p();
+  HIPCHK(e, hipMemsetAsync(base, 0, bytes, e->stream));
   out.resize(ns);
   for (uint32_t s = 0; s < ns; s++) {
-    out[s].agg = (uint4*)e->d_delta + (size_t)s * e->cfg.out_len;
-    out[s].count = (unsigned long long*)(e->d_delta + agg_b) + s;
-    out[s].checksum = (uint32_t*)(e->d_delta + agg_b + (size_t)ns * 8) + 8 * s;
+    out[s].agg = (uint4*)base + (size_t)s * e->cfg.out_len;
+    out[s].count = (unsigned long long*)(base + agg_b) + s;
+    out[s].checksum = (uint32_t*)(base + agg_b + (size_t)ns * 8) + 8 * s;
   }
   return JX_OK;
 }
@@ -1096,21 +1124,16 @@ void jx_engine_destroy(jx_engine* e) {
     (void)hipEventDestroy(p.second.first);
     (void)hipEventDestroy(p.second.second);
   }
-  for (auto& kv : e->segs) {
-    (void)hipFree(kv.second.agg);
-    (void)hipFree(kv.second.checksum);
-    (void)hipFree(kv.second.count);
-  }
-  if (e->arena)
+  e->segs.clear();
+  if (e->arena) {
+    for (Slab& sl : e->seg_slabs) arena_put(e->arena, sl, e->stream);
     for (auto& kv : e->batches) arena_put(e->arena, kv.second.slab, e->stream);
+  }
+  e->seg_slabs.clear();
   e->batches.clear();
   if (e->d_consts && !e->is_pipe) (void)hipFree(e->d_consts);
   if (e->ev_pipe) (void)hipEventDestroy(e->ev_pipe);
-  if (e->d_tmp) (void)hipFree(e->d_tmp);
-  if (e->d_hout) (void)hipFree(e->d_hout);
-  for (void* q : {(void*)e->d_segx, (void*)e->d_perm, (void*)e->d_items, (void*)e->d_spart, (void*)e->d_ptrs,
-                  (void*)e->d_err, (void*)e->d_delta})
-    if (q) (void)hipFree(q);
+  if (e->d_err) (void)hipFree(e->d_err);
   for (int k = 0; k < 2; k++) {
     if (e->h_ptrs[k]) (void)hipHostFree(e->h_ptrs[k]);
     if (e->ev_ptrs[k]) (void)hipEventDestroy(e->ev_ptrs[k]);
@@ -1162,10 +1185,11 @@ static int32_t drop_on_error(jx_engine* e, uint64_t id, int32_t rc) {
 
 static int32_t copy_out_shares(jx_engine* e, const uint4* outs, uint64_t n, uint8_t* dst) {
   const Cfg& c = e->cfg;
-  int32_t rc = ensure_tmp(e, n * c.out_len * c.fb);
+  Scratch tmp;
+  int32_t rc = scratch_get(e, n * c.out_len * c.fb, tmp);
   if (rc) return rc;
-  HIPCHK(e, launch_transpose_out(c, outs, n, e->d_tmp, e->stream));
-  HIPCHK(e, hipMemcpyAsync(dst, e->d_tmp, n * c.out_len * c.fb, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, launch_transpose_out(c, outs, n, tmp.p(), e->stream));
+  HIPCHK(e, hipMemcpyAsync(dst, tmp.p(), n * c.out_len * c.fb, hipMemcpyDeviceToHost, e->stream));
   return JX_OK;
 }
 
@@ -1193,8 +1217,13 @@ static int32_t helper_prep_batch_locked(jx_engine* e, uint64_t n, const uint8_t*
   return drain_timing(e);
 }
 
-// Coalesced prepares take jobs up to this size; larger ones fill the device by themselves.
-static bool coalescible(const jx_engine* e, uint64_t n) { return e->coalesce && n > 0 && n <= e->default_chunk / 4; }
+// Coalesced prepares take jobs up to a quarter of a launch (larger ones fill the device by themselves) that fit
+// one of the coalescer's lanes for their role (a leader's explicit input shares can be MBs per report); the
+// rest take the direct path.
+static bool coalescible(const jx_engine* e, uint64_t n, bool leader = false, bool encrypted = false,
+                        uint64_t ct_bytes = 0) {
+  return e->coalesce && n > 0 && n <= e->default_chunk / 4 && coalescer_accepts(e, leader, n, encrypted, ct_bytes);
+}
 
 int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* public_shares,
                              const uint8_t* helper_input_shares, const uint8_t* leader_prep_shares,
@@ -1217,6 +1246,94 @@ int32_t jx_helper_prep_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, co
   if (n) {
     rc = helper_prep_batch_locked(e, n, nonces, public_shares, helper_input_shares, leader_prep_shares, out_prep_msgs,
                                   out_verdicts, out_output_shares, B);
+    if (rc) return drop_on_error(e, id, rc);
+  }
+  if (out_batch_id) *out_batch_id = id;
+  return JX_OK;
+}
+
+int32_t jx_helper_prep_encrypted_batch(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint64_t* times,
+                                       const uint8_t* public_shares, const uint8_t task_id[32],
+                                       jx_hpke* const* keypairs, uint32_t nkeypairs, const uint8_t* key_index,
+                                       const uint8_t* encs, const uint8_t* payloads, const uint64_t* payload_offsets,
+                                       uint32_t flags, const uint8_t* leader_prep_shares, uint8_t* out_prep_msgs,
+                                       uint8_t* out_verdicts, uint8_t* out_open_status, uint64_t* out_batch_id) {
+  if (out_batch_id) *out_batch_id = 0;
+  if (!e || (n && (!nonces || !times || !task_id || !key_index || !encs || !payload_offsets || !leader_prep_shares ||
+                   !out_verdicts)))
+    return JX_E_INVALID;
+  const Cfg& c = e->cfg;
+  if (n && c.ps_bytes && !public_shares) return JX_E_INVALID;
+  if (nkeypairs > JX_ENC_MAX_KEYPAIRS || (nkeypairs && !keypairs) || (flags & ~JX_ENC_REQUIRE_TASKPROV))
+    return fail(e, JX_E_INVALID, "encrypted prepare: at most JX_ENC_MAX_KEYPAIRS keypairs, flags JX_ENC_*");
+  for (uint32_t k = 0; k < nkeypairs; k++)
+    if (!keypairs[k] || hpke_device(keypairs[k]) != e->device)
+      return fail(e, JX_E_INVALID, "encrypted prepare: every keypair must be an HPKE context on the engine's device");
+  for (uint64_t i = 0; i < n; i++) {
+    const uint8_t k0 = key_index[2 * i], k1 = key_index[2 * i + 1];
+    if ((k0 >= nkeypairs && k0 != JX_KEY_NONE && k0 != JX_KEY_MALFORMED) || (k1 >= nkeypairs && k1 != JX_KEY_NONE) ||
+        payload_offsets[i + 1] < payload_offsets[i] || payload_offsets[i + 1] - payload_offsets[i] > 0xFFFFFFFFull)
+      return fail(e, JX_E_INVALID, "encrypted prepare: key_index out of range or payload offsets decreasing");
+  }
+  if (n && payload_offsets[n] > payload_offsets[0] && !payloads) return JX_E_INVALID;
+  EncJob job;
+  job.times = times;
+  job.task_id = task_id;
+  job.keypairs = keypairs;
+  job.nkeys = nkeypairs;
+  job.key_index = key_index;
+  job.encs = encs;
+  job.payloads = payloads;
+  job.payload_offsets = payload_offsets;
+  job.flags = flags;
+  const uint64_t ct = n ? job.ct_bytes(n) : 0;
+  if (coalescible(e, n, false, true, ct)) {
+    t_err.clear();
+    return coalesced_helper_prep(e, n, nonces, public_shares, nullptr, leader_prep_shares, out_prep_msgs, out_verdicts,
+                                 out_batch_id, &job, out_open_status);
+  }
+  LOCK(e);
+  HIPCHK(e, hipSetDevice(e->device));
+  uint64_t id = 0;
+  Batch* B = nullptr;
+  int32_t rc = batch_new(e, n, false, &id, &B);
+  if (rc) return rc;
+  if (n) {
+    auto run = [&]() -> int32_t {
+      // the job's rows in pageable host memory, uploaded with its inputs; the key table is the job's keypairs
+      std::vector<EncRow> rows(n);
+      uint8_t key_map[JX_ENC_MAX_KEYPAIRS];
+      std::vector<HpkeKeyRow> keys(nkeypairs ? nkeypairs : 1);
+      for (uint32_t k = 0; k < nkeypairs; k++) {
+        key_map[k] = (uint8_t)k;
+        hpke_key_row(keypairs[k], &keys[k]);
+      }
+      fill_enc_rows(job, n, rows.data(), 0, key_map);
+      e->enc_ct_bytes = ct ? ct : 1;
+      Stage st;
+      int32_t r = stage_acquire(e, n, SG_IN | SG_HIN | SG_ENC | helper_meas_flag(c) | SG_PREP, st);
+      if (r) return r;
+      HIPCHK(e, hipMemcpyAsync(B->nonces, nonces, n * 16, hipMemcpyHostToDevice, e->stream));
+      if (c.ps_bytes) HIPCHK(e, hipMemcpyAsync(e->d_ps, public_shares, n * c.ps_bytes, hipMemcpyHostToDevice, e->stream));
+      HIPCHK(e, hipMemcpyAsync(e->d_lps, leader_prep_shares, n * c.lps_bytes, hipMemcpyHostToDevice, e->stream));
+      HIPCHK(e, hipMemcpyAsync(e->d_encrows, rows.data(), n * sizeof(EncRow), hipMemcpyHostToDevice, e->stream));
+      if (ct) HIPCHK(e, hipMemcpyAsync(e->d_ct, payloads + payload_offsets[0], ct, hipMemcpyHostToDevice, e->stream));
+      if (nkeypairs)
+        HIPCHK(e, hipMemcpyAsync(e->d_keys, keys.data(), nkeypairs * sizeof(HpkeKeyRow), hipMemcpyHostToDevice, e->stream));
+      HpkeRowsArgs ha{n, e->d_encrows, e->d_ct, e->d_pt, e->d_keys, nkeypairs, B->nonces, e->d_ps, c.ps_bytes,
+                      e->d_his, c.his_bytes, e->d_status};
+      HIPCHK(e, launch_hpke_rows(ha, e->stream));
+      r = prep_core(e, n, B->nonces, e->d_ps, e->d_his, e->d_lps, B->verdicts, B->msgs, B->outs);
+      if (r) return r;
+      HIPCHK(e, launch_open_mask(e->d_status, B->verdicts, n, e->stream));
+      HIPCHK(e, hipMemcpyAsync(out_verdicts, B->verdicts, n, hipMemcpyDeviceToHost, e->stream));
+      if (out_prep_msgs && c.jr_len)
+        HIPCHK(e, hipMemcpyAsync(out_prep_msgs, B->msgs, n * c.seed, hipMemcpyDeviceToHost, e->stream));
+      if (out_open_status) HIPCHK(e, hipMemcpyAsync(out_open_status, e->d_status, n, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipStreamSynchronize(e->stream));  // the pageable rows and the caller's outputs
+      return drain_timing(e);
+    };
+    rc = run();
     if (rc) return drop_on_error(e, id, rc);
   }
   if (out_batch_id) *out_batch_id = id;
@@ -1262,8 +1379,14 @@ int32_t jx_engine_memory(const jx_engine* e, jx_memory_stats* out) {
     out->arena_waits = A->waits;
     out->arena_engines = A->engines;
   }
-  uint64_t cs[12] = {0};
+  uint64_t cs[16] = {0};
   coalescer_stats(e, cs);
+  out->coalesce_pinned_bytes = cs[9];
+  out->coalesced_helper_launches = cs[10];
+  out->coalesced_helper_jobs = cs[11];
+  out->coalesced_leader_launches = cs[12];
+  out->coalesced_leader_jobs = cs[13];
+  out->coalesced_encrypted_jobs = cs[14];
   out->coalesced_launches = cs[0];
   out->coalesced_jobs = cs[1];
   out->coalesced_reports = cs[2];
@@ -1275,6 +1398,7 @@ int32_t jx_engine_memory(const jx_engine* e, jx_memory_stats* out) {
   {
     std::lock_guard<std::mutex> lk(A->mu);
     out->arena_cross_stream_waits = A->cross_waits;
+    out->arena_frees = A->frees;
   }
   return JX_OK;
 }
@@ -1303,7 +1427,7 @@ int32_t jx_leader_prep_init_batch(jx_engine* e, uint64_t n, const uint8_t* nonce
   if (!e || (n && (!nonces || !leader_input_shares || !out_prep_shares || !out_verdicts))) return JX_E_INVALID;
   const Cfg& c = e->cfg;
   if (n && c.ps_bytes && !public_shares) return JX_E_INVALID;
-  if (coalescible(e, n)) {
+  if (coalescible(e, n, true)) {
     t_err.clear();
     return coalesced_leader_init(e, n, nonces, public_shares, leader_input_shares, out_prep_shares, out_verdicts,
                                  out_batch_id);
@@ -1566,7 +1690,8 @@ int32_t jx_accumulate_device(jx_engine* e, uint64_t batch_id, uint64_t n, const 
 static int32_t batch_records(jx_engine* e, Batch* B, const uint8_t* d_mask, const uint32_t* d_index, uint32_t ns,
                              uint8_t* d_out) {
   std::vector<Segment> targets;
-  int32_t rc = delta_targets(e, ns, targets);
+  Scratch deltas;
+  int32_t rc = delta_targets(e, ns, targets, deltas);
   if (rc) return rc;
   rc = accumulate_into(e, batch_src(*B), d_mask, d_index, targets);
   if (rc) return rc;
@@ -1596,11 +1721,12 @@ int32_t jx_batch_aggregate_records(jx_engine* e, uint64_t batch_id, uint64_t n, 
     HIPCHK(e, hipMemcpyAsync(e->d_seg, segment_index, n * 4, hipMemcpyHostToDevice, e->stream));
     di = e->d_seg;
   }
-  rc = ensure_tmp(e, rb * nsegments);
+  Scratch rec;
+  rc = scratch_get(e, rb * nsegments, rec);
   if (rc) return rc;
-  rc = batch_records(e, B, dm, di, nsegments, e->d_tmp);
+  rc = batch_records(e, B, dm, di, nsegments, rec.p());
   if (rc) return rc;
-  HIPCHK(e, hipMemcpyAsync(out_records, e->d_tmp, rb * nsegments, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(out_records, rec.p(), rb * nsegments, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   return drain_timing(e);
 }
@@ -1646,16 +1772,11 @@ int32_t jx_helper_prep_aggregate(jx_engine* e, uint64_t n, const uint8_t* nonces
     // host thread stages them) go out while the other pipeline's kernels run; the verdicts and prep
     // messages collect in an engine buffer and come back once, after the join
     const uint64_t ob = n + (c.jr_len ? n * c.seed : 0);
-    if (ob > e->hout_bytes) {
-      HIPCHK(e, hipStreamSynchronize(e->stream));
-      if (e->d_hout) (void)hipFree(e->d_hout);
-      e->d_hout = nullptr;
-      e->hout_bytes = 0;
-      HIPCHK(e, hipMalloc((void**)&e->d_hout, ob));
-      e->hout_bytes = ob;
-    }
-    uint8_t* dv = e->d_hout;
-    uint8_t* dm = e->d_hout + n;
+    Scratch hout;  // per call, from the arena (handed back after the copies below are queued)
+    rc = scratch_get(e, ob, hout);
+    if (rc) return rc;
+    uint8_t* dv = hout.p();
+    uint8_t* dm = hout.p() + n;
     HIPCHK(e, hipEventRecord(e->ev_pipe, e->stream));
     for (uint32_t k = 0; k < P; k++) HIPCHK(e, hipStreamWaitEvent(e->pipes[k]->stream, e->ev_pipe, 0));
     auto run = [&]() -> int32_t {
@@ -1783,8 +1904,9 @@ int32_t jx_helper_prep_aggregate_device(jx_engine* e, uint64_t n, const void* d_
   rc = stage_acquire(e, chunk, SG_MEAS | SG_PREP | SG_RES | SG_ACC, st);
   if (rc) return rc;
   // the pointer table is uploaded once for every launch of the call (no per-launch host sync)
+  Scratch tbl;
   if (many) {
-    rc = upload_targets(e, targets);
+    rc = upload_targets(e, targets, tbl);
     if (rc) return rc;
   }
   for (uint64_t off = 0; off < n; off += chunk) {
@@ -1810,10 +1932,11 @@ int32_t jx_aggregate_read(jx_engine* e, uint32_t segment, uint8_t* out_agg, uint
   Segment* s = nullptr;
   int32_t rc = get_segment(e, segment, &s);
   if (rc) return rc;
-  rc = ensure_tmp(e, (size_t)c.out_len * fb);
+  Scratch tmp;
+  rc = scratch_get(e, (size_t)c.out_len * fb, tmp, true);
   if (rc) return rc;
-  HIPCHK(e, launch_agg_encode(c, s->agg, e->d_tmp, e->stream));
-  if (out_agg) HIPCHK(e, hipMemcpyAsync(out_agg, e->d_tmp, (size_t)c.out_len * fb, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, launch_agg_encode(c, s->agg, tmp.p(), e->stream));
+  if (out_agg) HIPCHK(e, hipMemcpyAsync(out_agg, tmp.p(), (size_t)c.out_len * fb, hipMemcpyDeviceToHost, e->stream));
   unsigned long long cnt = 0;
   HIPCHK(e, hipMemcpyAsync(&cnt, s->count, 8, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));

@@ -38,7 +38,8 @@ struct Arena {
   std::mutex mu;
   std::condition_variable cv;
   uint64_t budget = 0;           // bytes the arena may hold (free + checked out)
-  uint64_t allocated = 0;        // bytes held (free + checked out)
+  uint64_t allocated = 0;        // bytes held (free + checked out + being freed)
+  uint64_t freeing = 0;          // bytes of slabs taken off the free list and being destroyed (lock dropped)
   uint64_t in_use = 0;           // checked out
   uint64_t in_use_staging = 0;   // checked out as per-call staging
   uint64_t peak = 0;             // max in_use
@@ -118,7 +119,31 @@ enum : uint32_t {
   SG_LMSG = 64,  // host-path leader finish: inbound prep messages
   SG_VK = 128,   // coalesced launches: one verify key per report (16 B; multiproof: HMAC pads, 64 B)
   SG_JOBS = 512, // coalesced launches: the job table (MAX_JOBS_PER_LAUNCH slices)
+  SG_ENC = 1024, // encrypted helper inputs: EncRows, ciphertext + plaintext bytes (enc_ct_bytes each), key table,
+                 // open status
 };
+
+// One job's encrypted input shares (jx_helper_prep_encrypted_batch), as the caller passed them.
+struct EncJob {
+  const uint64_t* times = nullptr;
+  const uint8_t* task_id = nullptr;
+  jx_hpke* const* keypairs = nullptr;
+  uint32_t nkeys = 0;
+  const uint8_t* key_index = nullptr;  // n x 2
+  const uint8_t* encs = nullptr;
+  const uint8_t* payloads = nullptr;
+  const uint64_t* payload_offsets = nullptr;  // n + 1
+  uint32_t flags = 0;
+  uint64_t ct_bytes(uint64_t n) const { return payload_offsets[n] - payload_offsets[0]; }
+};
+// The job's EncRows, ciphertexts at ct_base + their offset within the job; key_map: the job's keypair
+// index -> the launch's key-table row.
+void fill_enc_rows(const EncJob& j, uint64_t n, jx::EncRow* rows, uint64_t ct_base, const uint8_t* key_map);
+// jx_hpke.hip
+int hpke_device(const jx_hpke* h);
+void hpke_key_row(const jx_hpke* h, jx::HpkeKeyRow* out);
+hipError_t launch_hpke_rows(const jx::HpkeRowsArgs& a, hipStream_t s);
+hipError_t launch_open_mask(const uint8_t* status, uint8_t* verdicts, uint64_t n, hipStream_t s);
 
 struct Coalescer;  // jx_coalesce.cpp
 
@@ -190,28 +215,24 @@ struct jx_engine {
   uint8_t *d_lis = nullptr, *d_lps_out = nullptr, *d_in_msgs = nullptr;
   uint8_t* d_vkeys = nullptr;
   jx::JobSlice* d_jobs = nullptr;
+  // SG_ENC: encrypted helper inputs (enc_ct_bytes: the ciphertext region's size, set before stage_acquire)
+  jx::EncRow* d_encrows = nullptr;
+  uint8_t *d_ct = nullptr, *d_pt = nullptr, *d_status = nullptr;
+  jx::HpkeKeyRow* d_keys = nullptr;
+  uint64_t enc_ct_bytes = 0;
   uint32_t acc_chunks = 0;  // report chunks of the accumulate kernel (0: acc_nchunks picks)
-  // persistent per-engine scratch (small, or only for host output shares)
-  uint8_t* d_hout = nullptr;  // the host fused path with pipelines: verdicts || prep messages of the call
-  uint64_t hout_bytes = 0;
-  uint8_t* d_tmp = nullptr;  // output-share transpose / aggregate encode / records
-  size_t tmp_bytes = 0;
   std::map<uint32_t, jxi::Segment> segs;  // running batch aggregations (the engine as one shard)
+  std::vector<jxi::Slab> seg_slabs;       // their states, kSegsPerSlab per arena slab
+  uint32_t seg_next = 0;                  // next free state in seg_slabs.back()
   // resident prepared batches by handle; handles are never reused
   std::map<uint64_t, jxi::Batch> batches;
   uint64_t batch_gen = 0, last_batch = 0;
-  // per-call batch-aggregation deltas (jx_batch_aggregate_records): agg [ns][out_len] | count [ns] | checksum [ns][8]
-  uint8_t* d_delta = nullptr;
-  size_t delta_bytes = 0;
-  // segmented accumulation scratch (allocated on first use)
+  // segmented accumulation: pointers into the call's arena scratch while it runs (accumulate_many)
   uint32_t* d_segx = nullptr;  // cnt, off, cursor [SEG_MAX each], ioff [SEG_MAX + 1], nitems [2]
   uint32_t* d_perm = nullptr;
-  uint64_t perm_cap = 0;
   uint4* d_items = nullptr;
   uint64_t* d_spart = nullptr;
-  uint64_t spart_wmax = 0;
-  void** d_ptrs = nullptr;  // [3][nptrs]: aggs, counts, checksums of the call's segments
-  uint64_t ptrs_cap = 0;
+  void** d_ptrs = nullptr;  // [3][nptrs]: aggs, counts, checksums of the call's segments (upload_targets)
   // pinned host copies of the pointer table, double-buffered: buffer k is rewritten only after the
   // upload that last read it has completed (ev_ptrs[k]), so no call waits for its own work
   void** h_ptrs[2] = {nullptr, nullptr};
@@ -278,7 +299,8 @@ size_t stage_bytes(const jx_engine* e, uint64_t cap, uint32_t flags);
 
 int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* his,
                   const uint8_t* lps, uint8_t* verdicts, uint8_t* msgs, uint4* outs, const uint8_t* lis = nullptr,
-                  uint8_t* lps_out = nullptr, uint64_t lis_rs = 0, const uint8_t* vkeys = nullptr);
+                  uint8_t* lps_out = nullptr, uint64_t lis_rs = 0, const uint8_t* vkeys = nullptr,
+                  hipEvent_t before_flp = nullptr);  // the FLP stage (K3) also waits on this event
 uint4* staging_outs(jx_engine* e);
 int32_t batch_new(jx_engine* e, uint64_t n, bool leader, uint64_t* id, Batch** out);
 void batch_free(jx_engine* e, std::map<uint64_t, Batch>::iterator it);
@@ -293,11 +315,16 @@ Coalescer* coalescer_for(jx_engine* e);
 // A coalesced helper prepare / leader prepare_init of a job of n reports: joins the device's next launch
 // with other engines' (tasks') jobs of the same Prio3 instance. Blocks the calling thread until its results
 // are in the caller's buffers; the engine mutex is not held while waiting.
+// enc (nullable): the job's input shares are encrypted (his unused); out_status (nullable): their open status.
 int32_t coalesced_helper_prep(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* his,
-                              const uint8_t* lps, uint8_t* out_msgs, uint8_t* out_verdicts, uint64_t* out_batch_id);
+                              const uint8_t* lps, uint8_t* out_msgs, uint8_t* out_verdicts, uint64_t* out_batch_id,
+                              const EncJob* enc = nullptr, uint8_t* out_status = nullptr);
+// Whether a job of n reports (ct_bytes of ciphertexts when encrypted) fits one of the coalescer's launches for
+// its role; larger jobs take the direct path.
+bool coalescer_accepts(const jx_engine* e, bool leader, uint64_t n, bool encrypted, uint64_t ct_bytes);
 int32_t coalesced_leader_init(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* lis,
                               uint8_t* out_prep_shares, uint8_t* out_verdicts, uint64_t* out_batch_id);
-void coalescer_stats(const jx_engine* e, uint64_t out[12]);
+void coalescer_stats(const jx_engine* e, uint64_t out[16]);
 void coalescer_set_window(jx_engine* e, uint32_t window_us);  // 0: automatic
 void coalescer_set_min_jobs(jx_engine* e, uint32_t jobs);     // debug option 7
 void coalescer_release(jx_engine* e);

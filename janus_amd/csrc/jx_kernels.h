@@ -210,6 +210,50 @@ constexpr uint32_t MAX_JOBS_PER_LAUNCH = 4096;
 hipError_t launch_scatter_jobs(const Cfg& c, const JobSlice* d_jobs, uint32_t njobs, uint64_t max_job_reports,
                                const uint4* outs, const uint8_t* verdicts, const uint8_t* msgs, const uint8_t* nonces,
                                hipStream_t s);
+// ---- HPKE open inside a helper prepare launch (jx_hpke.hip; jx_helper_prep_encrypted_batch)
+// A recipient keypair as the rows kernel reads it: clamped X25519 scalar and public key (LE words) and the
+// RFC 9180 key_schedule_context of its application info (0x00 || psk_id_hash || info_hash, 65 bytes).
+struct HpkeKeyRow {
+  uint32_t sk[8];
+  uint32_t pk[8];
+  uint8_t ksc[68];
+  uint8_t pad[4];
+};
+static_assert(sizeof(HpkeKeyRow) == 136, "HpkeKeyRow layout");
+enum : uint8_t {
+  ENC_ROW_ENCRYPTED = 1,         // the report's helper input share is inside `enc` / the ciphertext (else: uploaded)
+  ENC_ROW_REQUIRE_TASKPROV = 2,  // the task is provisioned by taskprov (aggregator.rs:1869-1879)
+  ENC_ROW_MALFORMED = 4,         // the encapsulated key is not 32 bytes: HpkeDecryptError without an open
+};
+// One report's encrypted input share: the HpkeCiphertext's encapsulated key and ciphertext (at ct_off of the
+// launch's ciphertext bytes), what its InputShareAad needs besides the id and public share rows, and the
+// keypairs to try (launch key-table rows; key0 JX_KEY_NONE: the config id is unknown).
+struct EncRow {
+  uint8_t enc[32];
+  uint8_t task_id[32];
+  uint8_t time_be[8];  // ReportMetadata.time, big-endian as encoded
+  uint64_t ct_off;
+  uint32_t ct_len;
+  uint8_t key0, key1, flags, pad;
+  uint8_t pad2[8];
+};
+static_assert(sizeof(EncRow) == 96, "EncRow layout");
+constexpr uint32_t ENC_MAX_KEYS = 16;  // distinct keypairs in one launch's key table
+struct HpkeRowsArgs {
+  uint64_t n;
+  const EncRow* rows;
+  const uint8_t* cts;   // ciphertext bytes of the launch
+  uint8_t* pts;         // plaintext scratch (same offsets as cts)
+  const HpkeKeyRow* keys;
+  uint32_t nkeys;
+  const uint8_t* nonces;
+  const uint8_t* ps;
+  uint32_t ps_bytes;
+  uint8_t* his;  // out: the helper input-share rows K1 reads
+  uint32_t his_bytes;
+  uint8_t* status;  // out: JX_OPEN_* per report
+};
+
 // multiproof Field64 SumVec (jx_mp64.hip)
 uint64_t k1_round_reports(const Cfg& c, int device, uint32_t k1_split = 0);
 // The helper reports [S, b.n) of a launch as Bufs of their own (S a multiple of 64: every staging array is

@@ -48,6 +48,7 @@ PREP_SHARE_DECODE_FAILURE = 2
 PREPARE_MESSAGE_FAILURE = 3
 PREPARE_NEXT_FAILURE = 4
 HELPER_STEP_FAILURE = 5  # leader only: the helper rejected the report
+OPEN_FAILURE = 6  # encrypted inputs: the report never reached helper_initialized (see open_status)
 VERDICT_LABELS = {
     FINISHED: "finished",
     PREPARE_INIT_FAILURE: "prepare_init_failure",
@@ -55,6 +56,20 @@ VERDICT_LABELS = {
     PREPARE_MESSAGE_FAILURE: "prepare_message_failure",
     PREPARE_NEXT_FAILURE: "prepare_next_failure",
     HELPER_STEP_FAILURE: "helper_step_failure",
+}
+# open status of an encrypted input share (include/jx_prio3.h JX_OPEN_*; aggregator.rs:1781-1910):
+# (janus_step_failures label, PrepareError value)
+OPEN_OK = 0
+KEY_NONE, KEY_MALFORMED = 0xFF, 0xFE
+ENC_REQUIRE_TASKPROV = 1
+OPEN_STATUS = {
+    1: ("decrypt_failure", 4),                           # HpkeDecryptError
+    2: ("plaintext_input_share_decode_failure", 8),      # InvalidMessage
+    3: ("duplicate_extension", 8),
+    4: ("unexpected_taskprov_extension", 8),
+    5: ("missing_or_malformed_taskprov_extension", 8),
+    6: ("input_share_decode_failure", 8),
+    7: ("unknown_hpke_config_id", 3),                    # HpkeUnknownConfigId
 }
 
 
@@ -100,6 +115,14 @@ class BatchResult:
 
     def finished(self) -> np.ndarray:
         return self.verdicts == FINISHED
+
+
+@dataclass
+class EncryptedResult:
+    verdicts: np.ndarray       # uint8[n]: as BatchResult, OPEN_FAILURE where the share did not open / decode
+    prep_msgs: np.ndarray      # uint8[n, PM]
+    open_status: np.ndarray    # uint8[n]: OPEN_OK or an OPEN_STATUS key
+    batch_id: int = 0
 
 
 class HelperEngine:
@@ -237,6 +260,46 @@ class HelperEngine:
             bid.value = 0
         return BatchResult(verdicts[:n], msgs[:n, : self.prep_msg_len], outs[:n] if outs is not None else None,
                            bid.value)
+
+    def helper_initialized_encrypted_batch(self, nonces, times, public_shares, task_id: bytes, keypairs,
+                                           key_index, encs, payloads: list[bytes], leader_prep_shares,
+                                           require_taskprov: bool = False, keep: bool = True) -> "EncryptedResult":
+        """The helper's per-report loop from the encrypted report share to helper_initialized + evaluate
+        (aggregator.rs:1763-1967), on the GPU for the whole job (jx_helper_prep_encrypted_batch): report i
+        is opened with keypairs[key_index[i][0]] (then keypairs[key_index[i][1]] if that fails to decrypt;
+        KEY_NONE: none; KEY_MALFORMED: an encapsulated key that is not 32 bytes), its PlaintextInputShare
+        decoded and checked, and prepared. keypairs: janus_amd.hpke.HpkeOpener contexts on this engine's
+        device. Returns verdicts (OPEN_FAILURE where the share did not open / decode), prep messages, the
+        open status per report (OPEN_STATUS) and the batch handle."""
+        n = int(np.asarray(nonces).reshape(-1, 16).shape[0])
+        nn = _u8(nonces, n, 16, "nonces")
+        ps = _u8(public_shares, n, self.public_share_len, "public_shares")
+        lps = _u8(leader_prep_shares, n, self.prep_share_len, "leader_prep_shares")
+        tm = np.ascontiguousarray(np.asarray(times, dtype=np.uint64).reshape(n)) if n else np.zeros(1, np.uint64)
+        ki = np.ascontiguousarray(np.asarray(key_index, dtype=np.uint8).reshape(n, 2)) if n else np.zeros((1, 2), np.uint8)
+        en = _u8(encs, n, 32, "encs") if n else np.zeros((1, 32), np.uint8)
+        if len(task_id) != 32 or len(payloads) != n:
+            raise ValueError("task id is 32 bytes; one payload per report")
+        off = np.zeros(n + 1, np.uint64)
+        if n:
+            off[1:] = np.cumsum([len(p) for p in payloads])
+        ct = np.frombuffer(b"".join(payloads) or b"\0", np.uint8).copy()
+        task = np.frombuffer(task_id, np.uint8).copy()
+        hs = (ctypes.c_void_p * max(1, len(keypairs)))(*[k.handle for k in keypairs])
+        verdicts = np.zeros(max(n, 1), np.uint8)
+        status = np.zeros(max(n, 1), np.uint8)
+        msgs = np.zeros((max(n, 1), max(self.prep_msg_len, 1)), np.uint8)
+        bid = ctypes.c_uint64()
+        st = self._L.jx_helper_prep_encrypted_batch(
+            self._h, n, _ptr(nn), tm.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+            _ptr(ps) if self.public_share_len else None, _ptr(task), hs, len(keypairs), _ptr(ki), _ptr(en), _ptr(ct),
+            off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), ENC_REQUIRE_TASKPROV if require_taskprov else 0,
+            _ptr(lps), _ptr(msgs) if self.prep_msg_len else None, _ptr(verdicts), _ptr(status), ctypes.byref(bid))
+        check(st, self._h, "jx_helper_prep_encrypted_batch")
+        if not keep:
+            self.release(bid.value)
+            bid.value = 0
+        return EncryptedResult(verdicts[:n], msgs[:n, : self.prep_msg_len], status[:n], bid.value)
 
     def batch_id(self) -> int:
         """Handle of the most recently prepared batch if still resident (0 otherwise)."""
@@ -489,4 +552,5 @@ class HelperEngine:
 
 Prio3Engine = HelperEngine
 
-__all__ = ["HelperEngine", "Prio3Engine", "BatchResult", "LeaderInit", "EngineError", "VERDICT_LABELS", "FINISHED"]
+__all__ = ["HelperEngine", "Prio3Engine", "BatchResult", "EncryptedResult", "LeaderInit", "EngineError",
+           "VERDICT_LABELS", "FINISHED", "OPEN_STATUS"]

@@ -76,6 +76,11 @@ class HpkeOpener:
             raise EngineError(f"jx_hpke_create: status {st}")
         self._h = h
 
+    @property
+    def handle(self):
+        """The jx_hpke context (for jx_helper_prep_encrypted_batch)."""
+        return self._h
+
     def close(self):
         if getattr(self, "_h", None):
             self._L.jx_hpke_destroy(self._h)

@@ -364,3 +364,79 @@ def test_mixed_k1_launch_two_verify_keys():
         engs[0].debug(7, 0)
         for e in engs:
             e.close()
+
+
+def test_mixed_roles_32_leader_32_helper_threads():
+    """An aggregator that is leader for one task and helper for another on one Prio3 instance
+    (aggregator_core/src/task.rs:598): 32 threads of 100-report leader prepare_init jobs interleaved with 32
+    threads of helper jobs, all coalesced. Each role gathers in its own lane, so a leader job never closes a
+    helper gather (and back): every job equals the oracle, and both roles share launches as they would alone."""
+    v = Prio3.sum_vec(8, 1000, 88)
+    vk_l, vk_h = bytes(range(16)), bytes(range(50, 66))
+    K, n, per_thread = 512, 100, 3
+    orc = _oracle(v)
+    meas, nonces, ps, lis, his = _shard(orc, v, K, seed=123)
+    lead = [orc.prep_init(vk_l, 0, nonces[i].tobytes(), ps[i].tobytes(), lis[i].tobytes()) for i in range(K)]
+    horc, hn, hps, hhis, hlps, hwant = _pool(v, vk_h, K, seed=124)
+    leader, helper = HelperEngine(v, vk_l), HelperEngine(v, vk_h)
+    try:
+        leader.coalesce(True)
+        helper.coalesce(True)
+        m0 = leader.memory()
+        out = {}
+
+        def worker(t):
+            for j in range(per_thread):
+                idx = ((t // 2) * 37 + j * 11 + np.arange(n)) % K
+                if t % 2 == 0:
+                    r = leader.leader_initialized_batch(nonces[idx], ps[idx], lis[idx])
+                    leader.release(r.batch_id)
+                    out[(t, j)] = ("leader", idx, r.verdicts.copy(), r.prep_shares.copy())
+                else:
+                    r = helper.helper_initialized_batch(hn[idx], hps[idx], hhis[idx], hlps[idx])
+                    helper.release(r.batch_id)
+                    out[(t, j)] = ("helper", idx, r.verdicts.copy(), r.prep_msgs.copy())
+
+        _run_threads(worker, 64)
+        m1 = leader.memory()
+        for (t, j), (role, idx, verdicts, x) in out.items():
+            if role == "leader":
+                for k, i in enumerate(idx):
+                    rc, share, _, _ = lead[i]
+                    assert int(verdicts[k]) == (1 if rc else 0), (t, j, i)
+                    if rc == 0:
+                        assert x[k].tobytes() == share, (t, j, i)
+            else:
+                np.testing.assert_array_equal(verdicts, hwant["verdicts"][idx], err_msg=f"job {t}/{j}")
+                f = hwant["verdicts"][idx] == 0
+                np.testing.assert_array_equal(x[f], hwant["prep_msgs"][idx][f], err_msg=f"job {t}/{j}")
+        d = {k: m1[k] - m0[k] for k in ("coalesced_helper_launches", "coalesced_helper_jobs",
+                                        "coalesced_leader_launches", "coalesced_leader_jobs")}
+        assert d["coalesced_helper_jobs"] == d["coalesced_leader_jobs"] == 32 * per_thread, d
+        # closed-loop callers of each role share launches (>= 4 jobs per launch; alone: ~16-32)
+        assert d["coalesced_helper_jobs"] >= 4 * d["coalesced_helper_launches"], d
+        assert d["coalesced_leader_jobs"] >= 4 * d["coalesced_leader_launches"], d
+        assert m1["coalesce_pinned_bytes"] > 0
+    finally:
+        leader.close()
+        helper.close()
+
+
+def test_two_engines_under_a_small_arena_budget():
+    """Two SumVec engines of different tasks run fused device calls from their own threads under a 6 GB arena
+    budget (JX_ARENA_GB, read once per process: run in a child process), with launch sizes that change every
+    call, so the arena keeps trimming idle slabs of one engine for the other's check-outs (outside its lock).
+    Both aggregates and every verdict equal the oracle's, and the arena did free slabs."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, JX_ARENA_GB="6")
+    r = subprocess.run([sys.executable, "-u", os.path.join(here, "arena_trim_worker.py")], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["verified"], res
+    assert res["arena_frees"] > 0 and res["arena_allocated_max"] <= res["arena_budget"], res

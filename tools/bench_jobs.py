@@ -55,6 +55,72 @@ def make_pool(vdaf, vk, K, threads):
     return nonces, ps, his, lps, want
 
 
+def make_enc_pool(vdaf, pool, seed=0x5EA1):
+    """The pool's helper input shares sealed as DAP report shares (HPKE base mode, X25519 / HKDF-SHA256 /
+    AES-128-GCM, the input-share application info and InputShareAad): every 50th ciphertext corrupted
+    (HpkeDecryptError), every 97th report under an unknown HPKE config id (HpkeUnknownConfigId). Returns the
+    pool with expected verdicts JX_OPEN_FAILURE (6) for those, and the encrypted-input extras."""
+    import random
+
+    from oracle import hpke_oracle as H  # input generation and the checker only
+
+    nonces, ps, his, lps, want = pool
+    K = nonces.shape[0]
+    rnd = random.Random(seed)
+    sk = rnd.randbytes(32)
+    pk = H.x25519_base(sk)
+    task_id = rnd.randbytes(32)
+    info = H.dap_info()
+    times = np.array([1_700_000_000 + i for i in range(K)], np.uint64)
+    encs, cts, kidx = [], [], []
+    status = np.zeros(K, np.uint8)
+    for i in range(K):
+        rid, pub = nonces[i].tobytes(), ps[i].tobytes()
+        aad = task_id + rid + int(times[i]).to_bytes(8, "big") + len(pub).to_bytes(4, "big") + pub
+        pt = (0).to_bytes(2, "big") + len(his[i]).to_bytes(4, "big") + his[i].tobytes()
+        enc, ct = H.seal_base(pk, info, aad, pt, rnd.randbytes(32))
+        k = (0, 0xFF)
+        if i % 50 == 7:
+            ct = ct[:5] + bytes([ct[5] ^ 0x10]) + ct[6:]
+            status[i] = 1
+        elif i % 97 == 11:
+            k = (0xFF, 0xFF)
+            status[i] = 7
+        encs.append(enc)
+        cts.append(ct)
+        kidx.append(k)
+    want = dict(want)
+    want["verdicts"] = np.where(status != 0, 6, want["verdicts"]).astype(want["verdicts"].dtype)
+    cto = np.zeros(K + 1, np.uint64)
+    cto[1:] = np.cumsum([len(c) for c in cts])
+    extra = {"sk": sk, "pk": pk, "task_id": task_id, "times": times,
+             "encs": np.frombuffer(b"".join(encs), np.uint8), "cto": cto, "cts": b"".join(cts),
+             "kidx": np.array(kidx, np.uint8), "status": status}
+    return (nonces, ps, his, lps, want), extra
+
+
+def make_leader_pool(vdaf, vk, K, seed=0x1EAD):
+    """K leader jobs' inputs (C-oracle shards: nonce, public share, leader input share) and the oracle's
+    leader prepare_init results (verdict, prep share)."""
+    from oracle import oracle as O
+
+    orc = O.Prio3Oracle(vdaf.algo_id, vdaf.bits, vdaf.length, vdaf.chunk_length)
+    rng = np.random.default_rng(seed)
+    hi = 1 << vdaf.bits if vdaf.algo_id in (1, 2) else 2
+    meas = rng.integers(0, hi, size=(K, max(1, vdaf.length)), dtype=np.uint64)
+    nonces = rng.integers(0, 256, size=(K, 16), dtype=np.uint8)
+    rands = rng.integers(0, 256, size=(K, orc.sizes.client_rand), dtype=np.uint8)
+    ps, lis, verdicts, shares = [], [], np.zeros(K, np.uint8), []
+    for i in range(K):
+        a, b, _ = orc.shard(meas[i], nonces[i].tobytes(), rands[i].tobytes())
+        rc, share, _, _ = orc.prep_init(vk, 0, nonces[i].tobytes(), a, b)
+        ps.append(a)
+        lis.append(b)
+        verdicts[i] = 1 if rc else 0
+        shares.append(share if rc == 0 else bytes(orc.sizes.prep_share))
+    return nonces, ps, lis, verdicts, shares
+
+
 def weighted_aggregate(outs: np.ndarray, mult: np.ndarray, fb: int, p: int) -> bytes:
     """sum_i mult[i] * out_i mod p, by 32-bit limbs in int64 columns (mult < 2^20, K < 2^11)."""
     K, width = outs.shape
@@ -200,26 +266,45 @@ def build_driver() -> str:
     return DRIVER
 
 
-def run_case_cpp(vdaf, vk, pool, n, T, seconds, mode, window_us, tmp):
+def run_case_cpp(vdaf, vk, pool, n, T, seconds, mode, window_us, tmp, enc=None, leader=None, leader_threads=0):
     """One case through the native driver (no interpreter between the threads and the C ABI); the
-    aggregate it read is checked here against the oracle."""
+    aggregate it read is checked here against the oracle. enc: the make_enc_pool extras (the jobs start from
+    encrypted report shares); leader: (leader vk, make_leader_pool output) with leader_threads threads of
+    leader prepare_init jobs beside the helper's."""
     import subprocess
 
     nonces, ps, his, lps, want = pool
     K = nonces.shape[0]
     pm = vdaf.prep_msg_len
-    src = os.path.join(tmp, f"pool_{vdaf.algo_id}_{K}.bin")
+    src = os.path.join(tmp, f"pool_{vdaf.algo_id}_{K}{'_enc' if enc else ''}.bin")
     if not os.path.exists(src):
         with open(src + ".tmp", "wb") as f:
-            f.write(np.array([K, ps.shape[1], his.shape[1], lps.shape[1], pm, 0, 0, 0], np.uint64).tobytes())
+            f.write(np.array([K, ps.shape[1], his.shape[1], lps.shape[1], pm, 1 if enc else 0,
+                              len(enc["cts"]) if enc else 0, 0], np.uint64).tobytes())
             for a in (nonces, ps, his, lps, want["verdicts"].astype(np.uint8)):
                 f.write(np.ascontiguousarray(a).tobytes())
             f.write(np.ascontiguousarray(want["prep_msgs"][:, :pm]).tobytes() if pm else b"")
+            if enc:
+                f.write(enc["sk"] + enc["pk"] + enc["task_id"])
+                for a in (enc["times"], enc["encs"], enc["cto"]):
+                    f.write(np.ascontiguousarray(a).tobytes())
+                f.write(enc["cts"])
+                f.write(np.ascontiguousarray(enc["kidx"]).tobytes())
+                f.write(np.ascontiguousarray(enc["status"]).tobytes())
         os.replace(src + ".tmp", src)
     out = os.path.join(tmp, "jobs_out.bin")
     cmd = [DRIVER, src, out, str(vdaf.algo_id), str(vdaf.bits), str(vdaf.length), str(vdaf.chunk_length),
            str(vdaf.num_proofs), vk.hex(), str(n), str(T), str(seconds), str(int(mode == "coalesce")), str(window_us),
            "1"]
+    if leader is not None and leader_threads:
+        lvk, (ln, lps_, llis, lv, lsh) = leader
+        lsrc = os.path.join(tmp, f"leader_{vdaf.algo_id}_{len(lv)}.bin")
+        if not os.path.exists(lsrc):
+            with open(lsrc + ".tmp", "wb") as f:
+                f.write(np.array([len(lv), len(lps_[0]), len(llis[0]), len(lsh[0]), 0, 0, 0, 0], np.uint64).tobytes())
+                f.write(np.ascontiguousarray(ln).tobytes() + b"".join(lps_) + b"".join(llis) + lv.tobytes() + b"".join(lsh))
+            os.replace(lsrc + ".tmp", lsrc)
+        cmd += ["1", lsrc, lvk.hex(), str(leader_threads)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=120 + 4 * seconds)
     if r.returncode != 0:
         return {"vdaf": vdaf.name(), "mode": mode, "reports_per_job": n, "threads": T, "verified": False,
@@ -237,8 +322,9 @@ def run_case_cpp(vdaf, vk, pool, n, T, seconds, mode, window_us, tmp):
     agg_ok = agg == exp and int(head[3]) == int(m_fin.sum())
     res = {"vdaf": vdaf.name(), "mode": mode, "driver": "cpp", "reports_per_job": n, "threads": T}
     res.update(line)
-    res["verified"] = bool(agg_ok and line["bad_jobs"] == 0)
-    res["verification"] = {"aggregate_and_count": bool(agg_ok), "jobs_with_wrong_verdicts_or_msgs": line["bad_jobs"]}
+    res["verified"] = bool(agg_ok and line["bad_jobs"] == 0 and line.get("leader_bad_jobs", 0) == 0)
+    res["verification"] = {"aggregate_and_count": bool(agg_ok), "jobs_with_wrong_verdicts_or_msgs": line["bad_jobs"],
+                           "leader_jobs_with_wrong_verdicts_or_prep_shares": line.get("leader_bad_jobs", 0)}
     return res
 
 
@@ -255,6 +341,11 @@ def main():
     ap.add_argument("--keep-pool", default=None,
                     help="cpp driver: write the pool file(s) into this directory and keep them (for running "
                          "tools/bin/jobs_driver directly, e.g. under rocprofv3)")
+    ap.add_argument("--encrypted", action="store_true",
+                    help="cpp driver: the jobs start from HPKE-encrypted report shares (jx_helper_prep_encrypted_batch)")
+    ap.add_argument("--leader-threads", default="0",
+                    help="cpp driver: comma list; L threads of 100-report leader prepare_init jobs of another task "
+                         "beside the helper's (an aggregator that is leader for some tasks and helper for others)")
     ap.add_argument("--driver", default="cpp", choices=("cpp", "python"),
                     help="cpp: native threads (tools/jobs_driver.cpp) call the C ABI; python: Python threads "
                          "through janus_amd.engine (the interpreter's lock serialises their host work)")
@@ -277,17 +368,30 @@ def main():
             import tempfile
 
             build_driver()
+            enc = None
+            if a.encrypted:
+                t0 = time.perf_counter()
+                pool, enc = make_enc_pool(vdaf, pool)
+                print(f"# sealed {a.pool} report shares in {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+            lts = [int(x) for x in a.leader_threads.split(",")]
+            leader = None
+            if any(lts):
+                lvk = bytes(range(100, 116))
+                leader = (lvk, make_leader_pool(vdaf, lvk, min(a.pool, 512)))
             with tempfile.TemporaryDirectory() as tmp:
                 if a.keep_pool:
                     os.makedirs(a.keep_pool, exist_ok=True)
                     tmp = a.keep_pool
                 for n in [int(x) for x in a.sizes.split(",") if int(x) > 0]:
                     for T in [int(x) for x in a.threads.split(",")]:
-                        line = json.dumps(run_case_cpp(vdaf, vk, pool, n, T, a.seconds, a.mode, a.window_us, tmp))
-                        print(line, flush=True)
-                        if out:
-                            out.write(line + "\n")
-                            out.flush()
+                        for L in lts:
+                            r = run_case_cpp(vdaf, vk, pool, n, T, a.seconds, a.mode, a.window_us, tmp, enc=enc,
+                                             leader=leader, leader_threads=L)
+                            line = json.dumps(r)
+                            print(line, flush=True)
+                            if out:
+                                out.write(line + "\n")
+                                out.flush()
             continue
         import torch  # noqa: F401  (one HIP runtime: torch first, see janus_amd/_lib.py)
 
