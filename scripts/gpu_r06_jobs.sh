@@ -30,9 +30,18 @@ fi
 if [[ $STEPS == *trace* ]]; then
   timeout -k 10 200 python -u tools/bench_jobs.py --driver cpp --mode coalesce --vdafs sumvec --sizes 10 --threads 1 --seconds 0.2 --keep-pool /tmp/jp > $OUT/prep.log 2>&1 || { echo PREP_FAIL; tail -5 $OUT/prep.log; exit 1; }
   for T in 64 10; do
-    timeout -k 10 120 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace_$T -o run -- tools/bin/jobs_driver /tmp/jp/pool_2_2048.bin /tmp/jp/out.bin 2 8 1000 88 1 000102030405060708090a0b0c0d0e0f 100 $T 1 1 0 1 > $OUT/driver_$T.json 2> $OUT/driver_$T.err || { echo TRACE_FAIL $T; tail -5 $OUT/driver_$T.err; exit 1; }
+    timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace --stats -f csv -d $OUT/trace_$T -o run -- tools/bin/jobs_driver /tmp/jp/pool_2_2048.bin /tmp/jp/out.bin 2 8 1000 88 1 000102030405060708090a0b0c0d0e0f 100 $T 1 1 0 1 > $OUT/driver_$T.json 2> $OUT/driver_$T.err || { echo TRACE_FAIL $T; tail -5 $OUT/driver_$T.err; exit 1; }
     f=$(ls $OUT/trace_$T/*/run_kernel_trace.csv $OUT/trace_$T/run_kernel_trace.csv 2>/dev/null | head -1)
+    c=$(ls $OUT/trace_$T/*/run_memory_copy_trace.csv $OUT/trace_$T/run_memory_copy_trace.csv 2>/dev/null | head -1)
+    python3 tools/launch_anatomy.py $f ${c:+--copies $c} > $OUT/anatomy_$T.json || true
     python3 tools/trace_overlap.py $f > $OUT/overlap_$T.json && python3 -c "import json; d=json.load(open('$OUT/overlap_$T.json')); print('trace', $T, round(d['device_busy_frac'],3), d['span_ms'])" && cat $OUT/driver_$T.json
   done
+fi
+if [[ $STEPS == *noacc* ]]; then
+  [ -f /tmp/jp/pool_2_2048.bin ] || timeout -k 10 200 python -u tools/bench_jobs.py --driver cpp --mode coalesce --vdafs sumvec --sizes 10 --threads 1 --seconds 0.2 --keep-pool /tmp/jp > $OUT/prep.log 2>&1 || { echo PREP_FAIL; exit 1; }
+  for T in 64 10; do for A in 1 0; do
+    timeout -k 10 60 tools/bin/jobs_driver /tmp/jp/pool_2_2048.bin /tmp/jp/out.bin 2 8 1000 88 1 000102030405060708090a0b0c0d0e0f 100 $T 2 1 0 1 $A > $OUT/noacc_${T}_$A.json 2> $OUT/noacc_${T}_$A.err || { echo NOACC_FAIL; exit 1; }
+    echo "acc=$A T=$T $(cat $OUT/noacc_${T}_$A.json)"
+  done; done
 fi
 echo JOBS_OK
