@@ -309,7 +309,11 @@ int32_t jx_leader_prep_init_device_ex(jx_engine* e, uint64_t n, const void* d_no
  * in one pass over the batch (device counting sort by segment). The batch is released: it is
  * accumulated at most once (a second call returns JX_E_STATE). The call returns once the accumulation is
  * queued on the engine stream (the host arrays are consumed before it returns); later calls on the engine
- * see its result (jx_aggregate_read / jx_engine_sync wait for it). */
+ * see its result (jx_aggregate_read / jx_engine_sync wait for it). A job-sized batch (<= 1,024 reports, no
+ * accept_mask, one segment) is deferred: the engine keeps it and adds up to 64 such batches per aggregation
+ * in one launch, when its queue is full or at the next call that reads, exports, resets or orders work
+ * against the aggregations (jx_aggregate_*, jx_shard_record_export_device, jx_engine_sync,
+ * jx_engine_record_event, jx_engine_join_stream, jx_engine_stream). */
 int32_t jx_accumulate(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t* accept_mask,
                       const uint32_t* segment);
 /* Same with device arrays: d_accept_mask (nullable) and d_segment (nullable = all reports into
@@ -408,7 +412,10 @@ int32_t jx_engine_timing_read(jx_engine* e, float ms[4], uint64_t launches[4]);
  *   option 6: lane-split K1 workgroups per CU (its placement for chain-latency-bound launches): 2 default
  *             (at most two waves per SIMD), 0 no cap, 1..8;
  *   option 7: tests: the device coalescer's gathers wait, up to their window, until `value` jobs have joined
- *             (0: off); needs coalescing on (JX_E_STATE otherwise). Applies to the whole device coalescer. */
+ *             (0: off); needs coalescing on (JX_E_STATE otherwise). Applies to the whole device coalescer;
+ *   option 8: jx_accumulate of job-sized batches: 1 deferred and added together (default), 0 one launch per call
+ *             (queued deferrals run first);
+ *   option 9: run the deferred accumulations now. */
 int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value);
 
 const char* jx_status_str(int32_t status);

@@ -25,12 +25,13 @@
 //     the lane's stream: one upload per input region, the HPKE open of the encrypted reports into the helper
 //     input-share rows (jx_hpke.hip), K1 -> K1' -> K3 over all jobs (each report with its own task's verify
 //     key, Bufs::vkeys), the open-status mask, one scatter kernel that copies every job's slice into its
-//     batch, one download of the results, an event.
-//   completer thread: polls the running launches' events and wakes their callers.
+//     batch, one download of the results, a host flag (launch_host_signal).
+//   completer thread: spins on the running launches' host flags (no runtime call) and wakes their callers.
 // Up to kLanes launches are gathering or in flight, so jobs that arrive while one runs start on the next lane
 // at once. A lane's pinned rows are sized to the role's recent launches and returned after kIdleFreeMs
 // without jobs (jx_engine_memory: coalesce_pinned_bytes).
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <deque>
@@ -49,6 +50,7 @@ constexpr uint32_t kLanes = 4;                   // one gathering lane per role 
 constexpr size_t kPinnedBudget = 512ull << 20;   // the largest lane: pinned input rows
 constexpr uint32_t kIdleFreeMs = 2000;           // pinned rows go back to the OS after this long without jobs
 constexpr uint64_t kMinLaneReports = 1024;
+constexpr uint32_t kFlagStride = 16;             // uint32 per lane flag: one 64-byte line each
 enum Role { HELPER = 0, LEADER = 1, NROLES = 2 };
 
 struct CReq {
@@ -67,7 +69,10 @@ struct CReq {
   int32_t rc = 0;
   std::string err;
   bool done = false;
-  std::condition_variable cv;  // this job's caller waits here for its launch (no herd of wake-ups)
+  // this job's caller waits here for its launch: its own mutex and condition variable (no herd of wake-ups, and
+  // the callers of a completed launch do not queue on the coalescer's mutex to leave their wait)
+  std::mutex m;
+  std::condition_variable cv;
 };
 
 enum LaneState { FREE, GATHER, SEALED, RUNNING, DONE };
@@ -76,10 +81,12 @@ struct Lane {
   jx_engine* q = nullptr;  // child engine: own stream, staging from the arena per launch
   uint8_t* h_in = nullptr;
   size_t h_in_cap = 0;
-  uint8_t* h_out = nullptr;
+  uint8_t* h_out = nullptr;  // host-coherent: the launch's download kernel writes it over PCIe
   size_t h_out_cap = 0;
+  uint8_t *d_in = nullptr, *d_out = nullptr;  // the same pinned rows as the device addresses them
   clk::time_point grown;  // when the pinned rows were last (re)allocated
   hipEvent_t ev_done = nullptr;
+  uint32_t seq = 0;       // launches queued on this lane (the host flag's value once the latest is done)
   // the leader prep shares' upload beside K1 (K1 reads only their joint-rand parts; K3 the rest)
   hipStream_t up = nullptr;
   hipEvent_t ev_up0 = nullptr, ev_up = nullptr;
@@ -90,7 +97,8 @@ struct Lane {
   bool enc = false;       // the layout holds the encrypted-input regions
   bool has_enc = false;   // a job of this gather is encrypted
   uint64_t reports = 0, cap_reports = 0, ct_bytes = 0, ct_cap = 0;
-  uint32_t copying = 0, unconsumed = 0;
+  uint32_t copying = 0;
+  std::atomic<uint32_t> unconsumed{0};  // callers still to copy their results out (the last one frees the lane)
   std::vector<CReq*> reqs;
   std::vector<const jx_hpke*> keys;  // the launch's key table
   clk::time_point opened, launched, last_arrival;
@@ -125,6 +133,9 @@ struct Coalescer {
   Lane lanes[kLanes];
   RoleState role[NROLES];
   std::vector<int> running;
+  // per lane, a host-coherent pinned flag (one per 64-byte line) the lane's launch sets to its seq when done
+  uint32_t* hflag = nullptr;
+  uint32_t* dflag = nullptr;  // the same memory as the device addresses it
   std::thread completer;
   bool stop = false;
   uint32_t refs = 0;
@@ -194,7 +205,7 @@ static void lane_free_pinned(Coalescer* C, Lane& L) {
   if (L.h_in) (void)hipHostFree(L.h_in);
   if (L.h_out) (void)hipHostFree(L.h_out);
   C->pinned -= L.h_in_cap + L.h_out_cap;
-  L.h_in = L.h_out = nullptr;
+  L.h_in = L.h_out = L.d_in = L.d_out = nullptr;
   L.h_in_cap = L.h_out_cap = 0;
 }
 
@@ -212,7 +223,7 @@ static int32_t lane_layout(Coalescer* C, Lane& L, int role, uint64_t n, uint64_t
   const uint64_t recent = now - R.peak_at < std::chrono::seconds(1) ? R.peak : 0;
   uint64_t cap = kMinLaneReports;
   while (cap < 2 * recent || cap < n) cap <<= 1;
-  if (cap > cmax) cap = cmax;
+  if (cap > cmax || C->min_jobs) cap = cmax;  // a test holding the gather for its jobs (option 7): room for all
   size_t off = 0;
   auto take = [&](size_t& o, size_t bytes) {
     o = off;
@@ -248,18 +259,25 @@ static int32_t lane_layout(Coalescer* C, Lane& L, int role, uint64_t n, uint64_t
   const bool oversized = L.h_in_cap > 4 * in_bytes && now - L.grown > std::chrono::seconds(1);
   if (L.h_in_cap < in_bytes || L.h_out_cap < out_bytes || oversized) {
     lane_free_pinned(C, L);
-    if (hipHostMalloc((void**)&L.h_in, in_bytes, hipHostMallocDefault) != hipSuccess) {
+    // mapped: the launch's upload and download kernels address the rows directly (launch_copy_regions)
+    if (hipHostMalloc((void**)&L.h_in, in_bytes, hipHostMallocMapped) != hipSuccess) {
       L.h_in = nullptr;
       return JX_E_NOMEM;
     }
     L.h_in_cap = in_bytes;
-    if (hipHostMalloc((void**)&L.h_out, out_bytes, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc((void**)&L.h_out, out_bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
       L.h_out = nullptr;
       C->pinned += L.h_in_cap;
       lane_free_pinned(C, L);
       return JX_E_NOMEM;
     }
     L.h_out_cap = out_bytes;
+    if (hipHostGetDevicePointer((void**)&L.d_in, L.h_in, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&L.d_out, L.h_out, 0) != hipSuccess) {
+      C->pinned += in_bytes + out_bytes;
+      lane_free_pinned(C, L);
+      return JX_E_HIP;
+    }
     C->pinned += in_bytes + out_bytes;
     L.grown = now;
   }
@@ -310,41 +328,33 @@ static int32_t launch_lane(Coalescer* C, Lane& L, std::string& err) {
     hipError_t s = hipStreamWaitEvent(q->stream, r->batch_ev, 0);
     if (s != hipSuccess) return bad(s, "hipStreamWaitEvent");
   }
-  auto up = [&](void* dst, size_t off, size_t bytes) -> hipError_t {
-    return bytes ? hipMemcpyAsync(dst, L.h_in + off, bytes, hipMemcpyHostToDevice, q->stream) : hipSuccess;
+  // Transfers are kernels on the lane's streams reading / writing the mapped pinned rows (launch_copy_regions): a
+  // copy-engine command of this lane could queue behind another lane's download, which waits for that lane's
+  // K1 (measured 1-2 ms stalls per launch at 64 x 100-report jobs, profiles/r06_jobs_trace_*).
+  const uint8_t* hin = L.d_in;
+  auto add = [](CopyArgs& a, void* dst, uint64_t dstride, const void* src, uint64_t sstride, uint64_t width,
+                uint64_t rows) {
+    if (width && rows) a.r[a.nr++] = CopyRegion{(uint8_t*)dst, (const uint8_t*)src, dstride, sstride, rows, width};
   };
+  auto flat = [&](CopyArgs& a, void* dst, size_t off, uint64_t bytes) { add(a, dst, 0, hin + off, 0, bytes, 1); };
   queued = true;
-  hipError_t s = up(q->d_nonces, L.o_non, m * 16);
-  if (s == hipSuccess && c.ps_bytes) s = up(q->d_ps, L.o_ps, m * c.ps_bytes);
-  if (s == hipSuccess && !leader) s = up(q->d_his, L.o_his, m * c.his_bytes);
+  CopyArgs ua{};
+  flat(ua, q->d_nonces, L.o_non, m * 16);
+  if (c.ps_bytes) flat(ua, q->d_ps, L.o_ps, m * c.ps_bytes);
+  if (!leader) flat(ua, q->d_his, L.o_his, m * c.his_bytes);
   // Helper: the leader prep shares are most of the bytes (SumVec 8x1000/88: 2,864 of 2,960 per report) and only
   // the FLP stage reads them whole; K1 reads each row's last 16 bytes (the leader's joint-rand part). Those go
   // first on the lane stream, the rest of the rows on the lane's upload stream beside K1, and K3 waits for it.
   const bool split_lps = !leader && c.lps_bytes > 16 && c.algo != ALGO_COUNT && c.algo != ALGO_SUMVEC_F64_MULTIPROOF;
-  hipEvent_t before_flp = nullptr;
-  if (s == hipSuccess && !leader && !split_lps) s = up(q->d_lps, L.o_lps, m * c.lps_bytes);
-  if (s == hipSuccess && split_lps) {
-    const size_t P = c.lps_bytes;
-    s = hipMemcpy2DAsync(q->d_lps + P - 16, P, L.h_in + L.o_lps + P - 16, P, 16, m, hipMemcpyHostToDevice, q->stream);
-    if (s == hipSuccess) s = hipEventRecord(L.ev_up0, q->stream);  // after the staging check-out's waits
-    if (s == hipSuccess) s = hipStreamWaitEvent(L.up, L.ev_up0, 0);
-    if (s == hipSuccess)
-      s = hipMemcpy2DAsync(q->d_lps, P, L.h_in + L.o_lps, P, P - 16, m, hipMemcpyHostToDevice, L.up);
-    if (s == hipSuccess) s = hipEventRecord(L.ev_up, L.up);
-    before_flp = L.ev_up;
-  }
-  if (s == hipSuccess && leader) {
-    if (q->lis_stride == c.lis_bytes)
-      s = up(q->d_lis, L.o_lis, m * c.lis_bytes);
-    else
-      s = hipMemcpy2DAsync(q->d_lis, q->lis_stride, L.h_in + L.o_lis, c.lis_bytes, c.lis_bytes, m,
-                           hipMemcpyHostToDevice, q->stream);
-  }
-  if (s == hipSuccess) s = up(q->d_vkeys, L.o_vk, m * vk_row_bytes(c));
-  if (s == hipSuccess && L.has_enc) {
-    s = up(q->d_encrows, L.o_enc, m * sizeof(EncRow));
-    if (s == hipSuccess) s = up(q->d_ct, L.o_ct, L.ct_bytes);
-    if (s == hipSuccess) s = up(q->d_keys, L.o_keys, L.keys.size() * sizeof(HpkeKeyRow));
+  const size_t P = c.lps_bytes;
+  if (!leader && !split_lps) flat(ua, q->d_lps, L.o_lps, m * P);
+  if (split_lps) add(ua, q->d_lps + P - 16, P, hin + L.o_lps + P - 16, P, 16, m);
+  if (leader) add(ua, q->d_lis, q->lis_stride, hin + L.o_lis, c.lis_bytes, c.lis_bytes, m);
+  flat(ua, q->d_vkeys, L.o_vk, m * vk_row_bytes(c));
+  if (L.has_enc) {
+    flat(ua, q->d_encrows, L.o_enc, m * sizeof(EncRow));
+    flat(ua, q->d_ct, L.o_ct, L.ct_bytes);
+    flat(ua, q->d_keys, L.o_keys, L.keys.size() * sizeof(HpkeKeyRow));
   }
   JobSlice* h_jobs = reinterpret_cast<JobSlice*>(L.h_in + L.o_jobs);
   uint64_t max_job = 0;
@@ -352,7 +362,18 @@ static int32_t launch_lane(Coalescer* C, Lane& L, std::string& err) {
     h_jobs[k] = L.reqs[k]->dst;
     if (L.reqs[k]->n > max_job) max_job = L.reqs[k]->n;
   }
-  if (s == hipSuccess) s = up(q->d_jobs, L.o_jobs, L.reqs.size() * sizeof(JobSlice));
+  flat(ua, q->d_jobs, L.o_jobs, L.reqs.size() * sizeof(JobSlice));
+  hipError_t s = launch_copy_regions(ua, q->stream);
+  hipEvent_t before_flp = nullptr;
+  if (s == hipSuccess && split_lps) {
+    CopyArgs ra{};
+    add(ra, q->d_lps, P, hin + L.o_lps, P, P - 16, m);
+    s = hipEventRecord(L.ev_up0, q->stream);  // after the waits above and the previous launch's reads of d_lps
+    if (s == hipSuccess) s = hipStreamWaitEvent(L.up, L.ev_up0, 0);
+    if (s == hipSuccess) s = launch_copy_regions(ra, L.up);
+    if (s == hipSuccess) s = hipEventRecord(L.ev_up, L.up);
+    before_flp = L.ev_up;
+  }
   if (s != hipSuccess) return bad(s, "upload");
   if (L.has_enc) {  // open the encrypted reports into their helper input-share rows
     HpkeRowsArgs ha{m, q->d_encrows, q->d_ct, q->d_pt, q->d_keys, (uint32_t)L.keys.size(), q->d_nonces, q->d_ps,
@@ -376,30 +397,32 @@ static int32_t launch_lane(Coalescer* C, Lane& L, std::string& err) {
   s = launch_scatter_jobs(c, q->d_jobs, (uint32_t)L.reqs.size(), max_job,
                           staging_outs(q), q->d_verdicts, q->d_msgs, q->d_nonces, q->stream);
   if (s != hipSuccess) return bad(s, "scatter");
-  s = hipMemcpyAsync(L.h_out + L.r_ver, q->d_verdicts, m, hipMemcpyDeviceToHost, q->stream);
-  if (s == hipSuccess && c.jr_len)
-    s = hipMemcpyAsync(L.h_out + L.r_msg, q->d_msgs, m * c.seed, hipMemcpyDeviceToHost, q->stream);
-  if (s == hipSuccess && leader)
-    s = hipMemcpyAsync(L.h_out + L.r_lps, q->d_lps_out, m * c.lps_bytes, hipMemcpyDeviceToHost, q->stream);
-  if (s == hipSuccess && L.has_enc)
-    s = hipMemcpyAsync(L.h_out + L.r_st, q->d_status, m, hipMemcpyDeviceToHost, q->stream);
+  CopyArgs da{};
+  add(da, L.d_out + L.r_ver, 0, q->d_verdicts, 0, m, 1);
+  if (c.jr_len) add(da, L.d_out + L.r_msg, 0, q->d_msgs, 0, m * c.seed, 1);
+  if (leader) add(da, L.d_out + L.r_lps, 0, q->d_lps_out, 0, m * c.lps_bytes, 1);
+  if (L.has_enc) add(da, L.d_out + L.r_st, 0, q->d_status, 0, m, 1);
+  s = launch_copy_regions(da, q->stream);
   if (s == hipSuccess) s = hipEventRecord(L.ev_done, q->stream);
+  if (s == hipSuccess) s = launch_host_signal(C->dflag + kFlagStride * (&L - C->lanes), ++L.seq, q->stream);
   if (s != hipSuccess) return bad(s, "download");
   return JX_OK;  // st hands the staging back stream-ordered
 }
 
 static void finish_lane(Coalescer* C, Lane& L, int32_t rc, const std::string& err) {
+  L.unconsumed.store((uint32_t)L.reqs.size());
+  L.state = DONE;
+  if (L.reqs.empty()) {
+    L.state = FREE;
+    C->cv_lane.notify_all();
+  }
   for (CReq* r : L.reqs) {
     r->rc = rc;
     if (rc) r->err = err;
+    // notify under the caller's mutex: once it sees done it may return and destroy r
+    std::lock_guard<std::mutex> g(r->m);
     r->done = true;
     r->cv.notify_one();
-  }
-  L.unconsumed = (uint32_t)L.reqs.size();
-  L.state = DONE;
-  if (L.unconsumed == 0) {
-    L.state = FREE;
-    C->cv_lane.notify_all();
   }
 }
 
@@ -495,25 +518,45 @@ static void dispatcher_main(Coalescer* C, int role) {
   }
 }
 
-// Polls the running launches (of both roles, which complete in any order) and wakes each one's callers.
+// Waits for the running launches (of both roles, which complete in any order) and wakes each one's callers. It
+// spins on the lanes' host flags (launch_host_signal), so it makes no runtime call while launches run: a loop of
+// hipEventQuery measured ~1 ms stalls of the other threads' HIP calls (the dispatcher's uploads, the callers'
+// next batches) behind the runtime's locks. Each running lane's event is still queried every
+// kEventCheckUs, to see a launch that failed (its flag never comes).
+constexpr uint32_t kEventCheckUs = 2000;
 static void completer_main(Coalescer* C) {
   (void)hipSetDevice(C->device);
   std::unique_lock<std::mutex> lk(C->mu);
+  std::vector<clk::time_point> checked(kLanes);
   for (;;) {
     C->cv_comp.wait(lk, [&] { return C->stop || !C->running.empty(); });
     if (C->running.empty() && C->stop) return;
-    const std::vector<int> snap = C->running;
+    std::vector<std::pair<int, uint32_t>> snap;
+    for (int k : C->running) snap.push_back({k, C->lanes[k].seq});
     lk.unlock();
     std::vector<std::pair<int, hipError_t>> done;
-    for (int k : snap) {
-      const hipError_t s = hipEventQuery(C->lanes[k].ev_done);
-      if (s != hipErrorNotReady) done.push_back({k, s});
-    }
-    (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
-    if (done.empty()) {
-      std::this_thread::yield();  // spin: a blocking-sync event's interrupt wake-up measured ms late
-      lk.lock();
-      continue;
+    const auto t_poll = clk::now();
+    for (int spin = 0; done.empty(); spin++) {
+      for (auto& ks : snap)
+        if (__atomic_load_n(C->hflag + kFlagStride * ks.first, __ATOMIC_ACQUIRE) == ks.second)
+          done.push_back({ks.first, hipSuccess});
+      if (!done.empty()) break;
+      const auto now = clk::now();
+      for (auto& ks : snap) {
+        if (now - checked[ks.first] < std::chrono::microseconds(kEventCheckUs)) continue;
+        checked[ks.first] = now;
+        const hipError_t st = hipEventQuery(C->lanes[ks.first].ev_done);
+        if (st != hipSuccess && st != hipErrorNotReady) done.push_back({ks.first, st});
+        (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
+      }
+      if (!done.empty()) break;
+      // a launch queued meanwhile joins the poll
+      if (now - t_poll > std::chrono::microseconds(200)) break;
+      if (spin & 63) {
+        __builtin_ia32_pause();
+      } else {
+        std::this_thread::yield();
+      }
     }
     const auto now = clk::now();
     lk.lock();
@@ -573,6 +616,16 @@ Coalescer* coalescer_for(jx_engine* e) {
   // a launch: up to half the fused path's launch size (its staging comes from the arena per launch)
   C->max_reports = e->auto_chunk / 2 < 4096 ? 4096 : e->auto_chunk / 2;
   C->last_job = clk::now();
+  if (hipHostMalloc((void**)&C->hflag, kLanes * kFlagStride * sizeof(uint32_t),
+                    hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&C->dflag, C->hflag, 0) != hipSuccess) {
+    if (C->hflag) (void)hipHostFree(C->hflag);
+    jx_engine_destroy(base);
+    (void)hipFree(consts);
+    delete C;
+    return nullptr;
+  }
+  memset(C->hflag, 0, kLanes * kFlagStride * sizeof(uint32_t));
   for (uint32_t k = 0; k < kLanes; k++) {
     Lane& L = C->lanes[k];
     L.q = new_child(base);
@@ -591,6 +644,7 @@ Coalescer* coalescer_for(jx_engine* e) {
       }
       jx_engine_destroy(base);
       (void)hipFree(consts);
+      (void)hipHostFree(C->hflag);
       delete C;
       return nullptr;
     }
@@ -635,6 +689,7 @@ void coalescer_release(jx_engine* e) {
   }
   jx_engine_destroy(C->base);
   if (consts) (void)hipFree(consts);
+  if (C->hflag) (void)hipHostFree(C->hflag);
   delete C;
 }
 
@@ -851,8 +906,11 @@ static int32_t coalesced(jx_engine* e, bool leader, uint64_t n, const uint8_t* n
   }
   lk.lock();
   if (--L->copying == 0) C->role[r.role].cv.notify_one();
-  r.cv.wait(lk, [&] { return r.done; });
   lk.unlock();
+  {
+    std::unique_lock<std::mutex> rl(r.m);
+    r.cv.wait(rl, [&] { return r.done; });
+  }
   if (r.rc == JX_OK) {
     memcpy(out_verdicts, L->h_out + L->r_ver + f, n);
     if (out_msgs && c.jr_len) memcpy(out_msgs, L->h_out + L->r_msg + f * c.seed, n * c.seed);
@@ -864,12 +922,12 @@ static int32_t coalesced(jx_engine* e, bool leader, uint64_t n, const uint8_t* n
         memset(out_status, 0, n);
     }
   }
-  lk.lock();
-  if (--L->unconsumed == 0) {
+  if (L->unconsumed.fetch_sub(1) == 1) {
+    lk.lock();
     L->state = FREE;
     C->cv_lane.notify_all();
+    lk.unlock();
   }
-  lk.unlock();
   if (r.rc) {
     fail(e, r.rc, r.err);
     return drop(r.rc);

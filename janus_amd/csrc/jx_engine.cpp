@@ -681,6 +681,12 @@ int32_t jxi::prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const ui
   }
   // the lane pairs with unrolled rounds while each pair-wave has a SIMD to itself (<= 16,384 reports on MI355X)
   if (b.k1_split == 6 && 8 * n <= e->round_reports) b.k1_split = 8;
+  // A lane-pair launch of at most half the CUs' workgroups (<= 8,192 reports on MI355X: the coalescer's launches
+  // of Janus-sized jobs, two in flight) reserves LDS for one workgroup per CU, so a second such launch lands on
+  // other CUs instead of doubling up SIMDs with the first (profiles/r06_jobs_*: K1 3.6 ms alone, 4.5 ms beside
+  // another launch on shared CUs).
+  if ((b.k1_split == 8 || b.k1_split == 6) && e->k1_split == 0 && 16 * n <= e->round_reports)
+    b.k1_pairs_lds = lanes_lds_bytes(1);
   // A lane-split launch past one wave per SIMD puts two of its long chains on some SIMDs and the launch waits
   // for those. Instead the first round_reports / 4 reports (a lane-split wave per SIMD) run lane-split and the
   // rest as lane pairs beside them on the side stream: FixedPointBoundedL2VecSum 16 x 10000, 40,960 reports,
@@ -718,6 +724,7 @@ int32_t jxi::prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const ui
       Bufs head = b, tail = bufs_tail(c, b, split_at);
       head.n = split_at;
       tail.k1_split = 8 * tail.n <= e->round_reports ? 8u : 6u;
+      tail.k1_pairs_lds = 0;
       HIPCHK(e, hipEventRecord(e->ev_fork, e->stream));
       HIPCHK(e, hipStreamWaitEvent(e->side, e->ev_fork, 0));
       HIPCHK(e, launch_xof(c, head, e->stream));
@@ -773,6 +780,53 @@ static int32_t accumulate_one(jx_engine* e, const AccSrc& src, const uint8_t* d_
   HIPCHK(e, stage_end(e, ST_ACC, ev));
   return JX_OK;
 }
+
+// Run the deferred accumulations (jx_accumulate): per aggregation, up to ACC_MULTI_MAX batches per
+// accumulate_multi launch; their slabs go back to the arena stream-ordered after the launches. One launch per
+// aggregation instead of one per job takes the per-job kernel launch off the engine mutex (a coalesced 100-report
+// job's callers return together, and each one's accumulate launch serialised them).
+constexpr uint64_t kAccQReports = 16384;  // a flush once this many reports wait (their batches hold HBM)
+static int32_t flush_acc(jx_engine* e) {
+  if (e->accq.empty()) return JX_OK;
+  std::vector<std::pair<Batch, uint32_t>> q;
+  q.swap(e->accq);
+  e->accq_reports = 0;
+  e->acc_flushes++;
+  std::map<uint32_t, std::vector<size_t>> by;
+  for (size_t k = 0; k < q.size(); k++) by[q[k].second].push_back(k);
+  auto run = [&]() -> int32_t {
+    HIPCHK(e, hipSetDevice(e->device));
+    for (auto& kv : by) {
+      Segment* s = nullptr;
+      int32_t rc = get_segment(e, kv.first, &s);
+      if (rc) return rc;
+      const std::vector<size_t>& ix = kv.second;
+      for (size_t o = 0; o < ix.size(); o += ACC_MULTI_MAX) {
+        AccMultiArgs a{};
+        a.agg = s->agg;
+        a.count = s->count;
+        a.checksum = s->checksum;
+        for (size_t j = o; j < ix.size() && a.nb < ACC_MULTI_MAX; j++) {
+          const Batch& b = q[ix[j]].first;
+          a.d[a.nb++] = AccDesc{b.outs, b.verdicts, b.nonces, b.n};
+        }
+        hipEvent_t ev = nullptr;
+        HIPCHK(e, stage_begin(e, &ev));
+        HIPCHK(e, launch_accumulate_multi(e->cfg, a, e->stream));
+        HIPCHK(e, stage_end(e, ST_ACC, ev));
+      }
+    }
+    return JX_OK;
+  };
+  const int32_t rc = run();
+  for (auto& p : q) arena_put(e->arena, p.first.slab, e->stream);  // after the launches that read them
+  return rc;
+}
+#define FLUSH_ACC(e)                 \
+  do {                               \
+    int32_t _fr = flush_acc(e);      \
+    if (_fr) return _fr;             \
+  } while (0)
 
 // Upload the device pointer table (aggs, counts, checksums) of `targets` into per-call scratch `tbl` (e->d_ptrs
 // points at it while it is held). The pinned host copy is double-buffered and reused only once the upload
@@ -1126,6 +1180,8 @@ void jx_engine_destroy(jx_engine* e) {
   }
   e->segs.clear();
   if (e->arena) {
+    for (auto& p : e->accq) arena_put(e->arena, p.first.slab, e->stream);  // deferred accumulations: unread
+    e->accq.clear();
     for (Slab& sl : e->seg_slabs) arena_put(e->arena, sl, e->stream);
     for (auto& kv : e->batches) arena_put(e->arena, kv.second.slab, e->stream);
   }
@@ -1622,6 +1678,23 @@ int32_t jx_accumulate(jx_engine* e, uint64_t batch_id, uint64_t n, const uint8_t
   int32_t rc = ready_batch(e, batch_id, n, "accumulate", &B);
   if (rc) return rc;
   HIPCHK(e, hipSetDevice(e->device));
+  // one aggregation, every finished report, a job-sized batch: deferred (flush_acc)
+  bool one_seg = true;
+  for (uint64_t i = 1; segment && i < n && one_seg; i++) one_seg = segment[i] == segment[0];
+  if (e->acc_defer && n > 0 && n <= ACC_SMALL && !accept_mask && one_seg) {
+    const uint32_t sid = segment ? segment[0] : 0;
+    Segment* s = nullptr;
+    rc = get_segment(e, sid, &s);  // creates it now (its memset is queued before any later flush)
+    if (rc) return rc;
+    auto it = e->batches.find(batch_id);
+    e->accq.emplace_back(it->second, sid);
+    e->accq_reports += n;
+    e->acc_deferred++;
+    if (e->last_batch == it->first) e->last_batch = 0;
+    e->batches.erase(it);  // a batch is accumulated at most once
+    if (e->accq.size() >= ACC_MULTI_MAX || e->accq_reports >= kAccQReports) return flush_acc(e);
+    return JX_OK;
+  }
   auto run = [&]() -> int32_t {
     if (n == 0) return JX_OK;
     Stage st;
@@ -1927,6 +2000,7 @@ int32_t jx_aggregate_read(jx_engine* e, uint32_t segment, uint8_t* out_agg, uint
   if (!e) return JX_E_INVALID;
   LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
+  FLUSH_ACC(e);  // the deferred accumulations land first
   const Cfg& c = e->cfg;
   const uint32_t fb = c.fb;
   Segment* s = nullptr;
@@ -1948,6 +2022,7 @@ int32_t jx_aggregate_checksum(jx_engine* e, uint32_t segment, uint8_t out_checks
   if (!e || !out_checksum) return JX_E_INVALID;
   LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
+  FLUSH_ACC(e);  // the deferred accumulations land first
   Segment* s = nullptr;
   int32_t rc = get_segment(e, segment, &s);
   if (rc) return rc;
@@ -1960,6 +2035,7 @@ int32_t jx_aggregate_reset(jx_engine* e) {
   if (!e) return JX_E_INVALID;
   LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
+  FLUSH_ACC(e);  // the deferred accumulations land first
   for (auto& kv : e->segs) {
     HIPCHK(e, hipMemsetAsync(kv.second.agg, 0, (size_t)e->cfg.out_len * 16, e->stream));
     HIPCHK(e, hipMemsetAsync(kv.second.checksum, 0, 32, e->stream));
@@ -1973,6 +2049,7 @@ int32_t jx_aggregate_export_device(jx_engine* e, uint32_t segment, void* d_dst) 
   if (!e || !d_dst) return JX_E_INVALID;
   LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
+  FLUSH_ACC(e);  // the deferred accumulations land first
   Segment* s = nullptr;
   int32_t rc = get_segment(e, segment, &s);
   if (rc) return rc;
@@ -2002,6 +2079,7 @@ int32_t jx_shard_record_export_device(jx_engine* e, uint32_t segment, void* d_ds
   if (!e || !d_dst) return JX_E_INVALID;
   LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
+  FLUSH_ACC(e);  // the deferred accumulations land first
   Segment* s = nullptr;
   int32_t rc = get_segment(e, segment, &s);
   if (rc) return rc;
@@ -2029,6 +2107,7 @@ int32_t jx_engine_sync(jx_engine* e) {
   if (!e) return JX_E_INVALID;
   LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
+  FLUSH_ACC(e);  // the deferred accumulations land first
   HIPCHK(e, hipStreamSynchronize(e->stream));
   if (e->d_err) {
     uint32_t bad = 0;
@@ -2053,6 +2132,7 @@ int32_t jx_engine_record_event(jx_engine* e, void* event) {
   if (!e || !event) return JX_E_INVALID;
   LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
+  FLUSH_ACC(e);  // the deferred accumulations land first
   HIPCHK(e, hipEventRecord((hipEvent_t)event, e->stream));
   return JX_OK;
 }
@@ -2071,6 +2151,7 @@ int32_t jx_engine_join_stream(jx_engine* e, void* stream) {
   if (!e) return JX_E_INVALID;
   LOCK(e);
   HIPCHK(e, hipSetDevice(e->device));
+  FLUSH_ACC(e);  // the deferred accumulations land first
   HIPCHK(e, hipEventRecord(e->ev_join, e->stream));
   HIPCHK(e, hipStreamWaitEvent((hipStream_t)stream, e->ev_join, 0));
   return JX_OK;
@@ -2078,6 +2159,8 @@ int32_t jx_engine_join_stream(jx_engine* e, void* stream) {
 
 int32_t jx_engine_stream(jx_engine* e, void** stream) {
   if (!e || !stream) return JX_E_INVALID;
+  LOCK(e);
+  FLUSH_ACC(e);  // work the caller queues on the stream sees the deferred accumulations
   *stream = (void*)e->stream;
   return JX_OK;
 }
@@ -2156,6 +2239,16 @@ int32_t jx_engine_debug(jx_engine* e, int32_t option, int64_t value) {
     if (value < 0 || value > 8) return JX_E_INVALID;
     e->lanes_wg_cap = (uint32_t)value;
     for (jx_engine* q : e->pipes) q->lanes_wg_cap = e->lanes_wg_cap;
+    return JX_OK;
+  }
+  if (option == 8) {  // jx_accumulate of job-sized batches: 1 deferred and flushed together (default), 0 at once
+    if (value != 0 && value != 1) return JX_E_INVALID;
+    if (!value) FLUSH_ACC(e);
+    e->acc_defer = value != 0;
+    return JX_OK;
+  }
+  if (option == 9) {  // tests: run the deferred accumulations now
+    FLUSH_ACC(e);
     return JX_OK;
   }
   if (option == 7) {  // tests: the device coalescer's gathers wait (up to their window) for this many jobs

@@ -245,6 +245,13 @@ struct jx_engine {
   uint64_t h_acc_cap = 0;
   hipEvent_t ev_hacc = nullptr;
   std::vector<uint32_t> h_dense;
+  // deferred small accumulations: jx_accumulate of an unmasked batch of <= ACC_SMALL reports into one
+  // aggregation parks the batch here; a flush runs one accumulate_multi launch per aggregation (a full queue,
+  // or any call that reads, exports, resets or orders work against the aggregations)
+  std::vector<std::pair<jxi::Batch, uint32_t>> accq;  // (batch, aggregation id)
+  uint64_t accq_reports = 0;
+  bool acc_defer = true;      // debug option 8
+  uint64_t acc_flushes = 0, acc_deferred = 0;
   uint32_t* d_err = nullptr;  // combine kernels: non-canonical input seen (reported by jx_engine_sync)
   // timing
   bool timing = false;

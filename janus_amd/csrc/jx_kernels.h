@@ -126,6 +126,8 @@ struct Bufs {
                         // bits <= 32), 8 = lane pairs with unrolled rounds, 7 = a word per lane (xof_words_kernel,
                         // bits <= 32), otherwise the fused kernel
   uint32_t k1_lds;      // dynamic LDS of the lane-split kernel: caps its workgroups per CU (lanes_lds_bytes)
+  uint32_t k1_pairs_lds;  // dynamic LDS of the lane-pair kernel (0: none): one workgroup per CU, so two small
+                          // launches in flight (coalesced jobs) take disjoint CUs instead of sharing SIMDs
 };
 
 struct AccArgs {
@@ -189,6 +191,43 @@ hipError_t launch_accumulate(const Cfg& c, const AccArgs& a, uint4* agg, hipStre
 // Accumulations of at most ACC_SMALL reports: one kernel, no partials or selection scratch (a.partials unused).
 constexpr uint64_t ACC_SMALL = 1024;
 hipError_t launch_accumulate_small(const Cfg& c, const AccArgs& a, uint4* agg, hipStream_t s);
+// Several small batches into ONE aggregation in one kernel (jx_accumulate calls the engine deferred and
+// flushes together): every finished report of every batch is added. The table travels as the kernel argument.
+constexpr uint32_t ACC_MULTI_MAX = 64;
+struct AccDesc {
+  const uint4* outs;
+  const uint8_t* verdicts;
+  const uint8_t* nonces;
+  uint64_t n;
+};
+struct AccMultiArgs {
+  AccDesc d[ACC_MULTI_MAX];
+  uint32_t nb;
+  uint4* agg;
+  unsigned long long* count;
+  uint32_t* checksum;
+};
+hipError_t launch_accumulate_multi(const Cfg& c, const AccMultiArgs& a, hipStream_t s);
+// The host sees a launch complete without a runtime call: one lane stores `seq` into a host-coherent pinned flag
+// once the stream reaches this point (a system-scope release store, so the stream's earlier downloads are
+// visible first). The coalescer's completer polls the flags instead of querying events.
+hipError_t launch_host_signal(uint32_t* flag, uint32_t seq, hipStream_t s);
+// Strided row copies between HBM and mapped pinned host memory by a kernel on the caller's stream (a coalesced
+// launch's uploads and downloads): no copy-engine command, so a lane's transfers never queue behind another
+// lane's download that is waiting for that lane's kernels (measured: ~1-2 ms stalls). Region
+// k copies `rows` rows of `width` bytes; 16-byte vectors when every address, stride and the width allow.
+struct CopyRegion {
+  uint8_t* dst;
+  const uint8_t* src;
+  uint64_t dst_stride, src_stride, rows;
+  uint64_t width;
+};
+constexpr uint32_t COPY_MAX_REGIONS = 12;
+struct CopyArgs {
+  CopyRegion r[COPY_MAX_REGIONS];
+  uint32_t nr;
+};
+hipError_t launch_copy_regions(const CopyArgs& a, hipStream_t s);
 hipError_t launch_combine(const Cfg& c, const uint8_t* parts, uint32_t nparts, uint8_t* out, uint32_t* err,
                           hipStream_t s);
 // ns records of contiguous segment state (agg [ns][out_len], count [ns], checksum [ns][8])

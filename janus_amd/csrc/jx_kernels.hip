@@ -2979,6 +2979,98 @@ __global__ __launch_bounds__(256) void accumulate_small_kernel(Cfg c, AccArgs a,
   }
 }
 
+// K4 for up to ACC_MULTI_MAX small batches into one aggregation (the engine's deferred jx_accumulate calls,
+// flushed together: one launch instead of one per aggregation job). Workgroup i < out_len sums output element
+// i over every batch's finished reports, its wave w taking batches w, w + 4, ... (each 64-report block read
+// as one coalesced 1 KiB row), the four waves' 192-bit sums reduced through LDS and added into the
+// aggregation. Each workgroup past out_len folds one batch into the count and the ReportIdChecksum.
+__global__ __launch_bounds__(256) void accumulate_multi_kernel(Cfg c, AccMultiArgs a) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (blockIdx.x < c.out_len) {
+    const uint32_t i = blockIdx.x;
+    acc192 acc;
+    acc_zero(acc);
+    for (uint32_t k = w; k < a.nb; k += 4) {
+      const AccDesc d = a.d[k];
+      const uint64_t nblk = (d.n + 63) / 64;
+      for (uint64_t bk = 0; bk < nblk; bk++) {
+        const uint64_t r = bk * 64 + lane;
+        if (r < d.n && d.verdicts[r] == 0) acc_add128(acc, u4_to_f(d.outs[il_idx(bk, c.out_len, i, lane)]));
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      uint64_t o0 = ((uint64_t)__shfl_xor((uint32_t)(acc.w0 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w0, off);
+      uint64_t o1 = ((uint64_t)__shfl_xor((uint32_t)(acc.w1 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w1, off);
+      uint64_t o2 = ((uint64_t)__shfl_xor((uint32_t)(acc.w2 >> 32), off) << 32) | __shfl_xor((uint32_t)acc.w2, off);
+      uint32_t cc = 0;
+      acc.w0 = addc64(acc.w0, o0, cc);
+      acc.w1 = addc64(acc.w1, o1, cc);
+      acc.w2 = acc.w2 + o2 + cc;
+    }
+    __shared__ uint64_t red[4][3];
+    if (lane == 0) {
+      red[w][0] = acc.w0;
+      red[w][1] = acc.w1;
+      red[w][2] = acc.w2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int q = 1; q < 4; q++) {
+        uint32_t cc = 0;
+        acc.w0 = addc64(acc.w0, red[q][0], cc);
+        acc.w1 = addc64(acc.w1, red[q][1], cc);
+        acc.w2 = acc.w2 + red[q][2] + cc;
+      }
+      acc_add128(acc, u4_to_f(a.agg[i]));
+      if (c.fb == 8) {
+        const uint64_t v = reduce192_p64(acc.w0, acc.w1, acc.w2);
+        a.agg[i] = make_uint4(lo32(v), hi32(v), 0, 0);
+      } else {
+        a.agg[i] = f_to_u4(acc_reduce(acc));
+      }
+    }
+    return;
+  }
+  const AccDesc d = a.d[blockIdx.x - c.out_len];
+  uint32_t h8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t cnt = 0;
+  for (uint64_t r = threadIdx.x; r < d.n; r += 256) {
+    if (d.verdicts[r] == 0) {
+      uint32_t id[4], h[8];
+      load16(d.nonces + 16 * r, id);
+      sha256_16(id, h);
+#pragma unroll
+      for (int k = 0; k < 8; k++) h8[k] ^= h[k];
+      cnt++;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    uint32_t v = h8[k];
+    for (int off = 32; off > 0; off >>= 1) v ^= __shfl_xor(v, off);
+    h8[k] = v;
+  }
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  __shared__ uint32_t redc[4][9];
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) redc[w][k] = h8[k];
+    redc[w][8] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x < 9) {
+    const uint32_t k = threadIdx.x;
+    uint32_t v = 0;
+    for (uint32_t q = 0; q < 4; q++) v = k < 8 ? (v ^ redc[q][k]) : (v + redc[q][k]);
+    if (v) {
+      if (k < 8)
+        atomicXor(&a.checksum[k], v);
+      else
+        atomicAdd(a.count, (unsigned long long)v);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------- K4 segmented
 // One pass for any number of batch aggregations: a device counting sort of the selected reports by
 // segment (LDS histograms, one global atomic per (workgroup, segment)), work items of <= L sorted
@@ -3365,9 +3457,10 @@ hipError_t launch_xof(const Cfg& c, const Bufs& b, hipStream_t s) {
       hipLaunchKernelGGL(trunc_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, c, b, nout);
     }
   } else if (b.k1_split == 8 && !wide)  // lane pairs, unrolled rounds (<= one pair-wave per SIMD)
-    hipLaunchKernelGGL(xof_pairs_kernel<true>, dim3((4 * nb + K1_WAVES - 1) / K1_WAVES), block, 0, s, c, b);
+    hipLaunchKernelGGL(xof_pairs_kernel<true>, dim3((4 * nb + K1_WAVES - 1) / K1_WAVES), block, b.k1_pairs_lds, s, c, b);
   else if (b.k1_split == 6 && !wide)  // lane pairs: 16 reports per wave
-    hipLaunchKernelGGL(xof_pairs_kernel<false>, dim3((4 * nb + K1_WAVES - 1) / K1_WAVES), block, 0, s, c, b);
+    hipLaunchKernelGGL(xof_pairs_kernel<false>, dim3((4 * nb + K1_WAVES - 1) / K1_WAVES), block, b.k1_pairs_lds, s, c,
+                       b);
   else if (b.k1_split == 3) {  // lane-split: 32 reports per wave
     const dim3 g2((2 * nb + K1_WAVES - 1) / K1_WAVES);
     if (wide)
@@ -3558,6 +3651,58 @@ hipError_t launch_accumulate(const Cfg& c, const AccArgs& a, uint4* agg, hipStre
 
 hipError_t launch_accumulate_small(const Cfg& c, const AccArgs& a, uint4* agg, hipStream_t s) {
   hipLaunchKernelGGL(accumulate_small_kernel, dim3((c.out_len + 3) / 4), dim3(256), 0, s, c, a, agg);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(64) void host_signal_kernel(uint32_t* flag, uint32_t seq) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag + threadIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+hipError_t launch_host_signal(uint32_t* flag, uint32_t seq, hipStream_t s) {
+  hipLaunchKernelGGL(host_signal_kernel, dim3(1), dim3(64), 0, s, flag, seq);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void copy_regions_kernel(CopyArgs a) {
+  const CopyRegion g = a.r[blockIdx.y];
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool vec = ((g.width | g.dst_stride | g.src_stride | (uint64_t)(uintptr_t)g.dst | (uint64_t)(uintptr_t)g.src) & 15) == 0;
+  if (vec) {
+    const uint64_t cpr = g.width / 16, total = cpr * g.rows;
+    for (uint64_t t = t0; t < total; t += step) {
+      const uint64_t row = t / cpr, ch = t - row * cpr;
+      *reinterpret_cast<uint4*>(g.dst + row * g.dst_stride + 16 * ch) =
+          *reinterpret_cast<const uint4*>(g.src + row * g.src_stride + 16 * ch);
+    }
+  } else {
+    const uint64_t total = g.width * g.rows;
+    for (uint64_t t = t0; t < total; t += step) {
+      const uint64_t row = t / g.width, bt = t - row * g.width;
+      g.dst[row * g.dst_stride + bt] = g.src[row * g.src_stride + bt];
+    }
+  }
+}
+hipError_t launch_copy_regions(const CopyArgs& a, hipStream_t s) {
+  if (a.nr == 0) return hipSuccess;
+  if (a.nr > COPY_MAX_REGIONS) return hipErrorInvalidValue;
+  uint64_t most = 0;
+  for (uint32_t k = 0; k < a.nr; k++) {
+    const CopyRegion& g = a.r[k];
+    const bool vec = ((g.width | g.dst_stride | g.src_stride | (uint64_t)(uintptr_t)g.dst | (uint64_t)(uintptr_t)g.src) & 15) == 0;
+    const uint64_t items = vec ? g.width / 16 * g.rows : g.width * g.rows;
+    if (items > most) most = items;
+  }
+  uint64_t gx = (most + 255) / 256;
+  if (gx > 512) gx = 512;
+  if (gx == 0) gx = 1;
+  hipLaunchKernelGGL(copy_regions_kernel, dim3((uint32_t)gx, a.nr), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_accumulate_multi(const Cfg& c, const AccMultiArgs& a, hipStream_t s) {
+  if (a.nb == 0) return hipSuccess;
+  if (a.nb > ACC_MULTI_MAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(accumulate_multi_kernel, dim3(c.out_len + a.nb), dim3(256), 0, s, c, a);
   return hipGetLastError();
 }
 

@@ -39,9 +39,11 @@ if [[ $STEPS == *trace* ]]; then
 fi
 if [[ $STEPS == *noacc* ]]; then
   [ -f /tmp/jp/pool_2_2048.bin ] || timeout -k 10 200 python -u tools/bench_jobs.py --driver cpp --mode coalesce --vdafs sumvec --sizes 10 --threads 1 --seconds 0.2 --keep-pool /tmp/jp > $OUT/prep.log 2>&1 || { echo PREP_FAIL; exit 1; }
-  for T in 64 10; do for A in 1 0; do
-    timeout -k 10 60 tools/bin/jobs_driver /tmp/jp/pool_2_2048.bin /tmp/jp/out.bin 2 8 1000 88 1 000102030405060708090a0b0c0d0e0f 100 $T 2 1 0 1 $A > $OUT/noacc_${T}_$A.json 2> $OUT/noacc_${T}_$A.err || { echo NOACC_FAIL; exit 1; }
-    echo "acc=$A T=$T $(cat $OUT/noacc_${T}_$A.json)"
+  # accumulate per job deferred (default) / at once (JX_JOBS_DEFER=0) / not at all (batches released)
+  for T in 64 10; do for A in 1 0 2; do
+    D=1; ACC=$A; [ $A = 0 ] && D=0 && ACC=1; [ $A = 2 ] && ACC=0
+    JX_JOBS_DEFER=$D timeout -k 10 60 tools/bin/jobs_driver /tmp/jp/pool_2_2048.bin /tmp/jp/out.bin 2 8 1000 88 1 000102030405060708090a0b0c0d0e0f 100 $T 2 1 0 1 $ACC > $OUT/acc_${T}_$A.json 2> $OUT/acc_${T}_$A.err || { echo ACC_FAIL; cat $OUT/acc_${T}_$A.err | tail -3; exit 1; }
+    echo "acc_mode=$A(1 deferred,0 at once,2 none) T=$T $(cat $OUT/acc_${T}_$A.json)"
   done; done
 fi
 echo JOBS_OK

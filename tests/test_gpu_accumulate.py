@@ -538,3 +538,54 @@ def test_small_accumulate_boundary(vdaf):
         sel = (want["verdicts"][:512] == 0) & mask[:512]
         exp = _expected(orc, want, nonces, np.concatenate([sel, np.zeros(n - 512, bool)]))
         assert eng.aggregate_share(0) == exp
+
+
+@pytest.mark.parametrize("vdaf", [Prio3.count(), Prio3.sum_vec(4, 12, 4), Prio3.histogram(40, 5)],
+                         ids=["count-field64", "sumvec-field128", "histogram"])
+def test_deferred_accumulate_of_many_jobs(vdaf):
+    """jx_accumulate of job-sized batches (<= 1,024 reports, no mask, one segment) is deferred and run as one
+    accumulate_multi launch per aggregation (up to 64 batches, auto-flushed when 64 wait): 150 jobs of 1 to 1,024
+    reports into three aggregations, with masked jobs (accumulated at once) interleaved, equal the oracle per
+    aggregation; a reset flushes first (deferred jobs before it are zeroed), and the immediate path (debug
+    option 8 = 0) gives the same aggregates."""
+    vk = bytes(range(40, 56))
+    rng = np.random.default_rng(77)
+    sizes = [int(s) for s in rng.choice([1, 2, 7, 30, 63, 64, 65, 100, 129], size=146)] + [1024, 1024, 5, 1]
+    n = sum(sizes)
+    orc, nonces, ps, his, lps = _batch(vdaf, vk, n, seed=4242)
+    want = orc.helper_prep_batch(vk, nonces, ps, his, lps, nthreads=16, want_out_shares=True)
+    mask = rng.integers(0, 2, size=n).astype(np.uint8)
+    jobs, off = [], 0
+    for k, s in enumerate(sizes):
+        jobs.append((off, off + s, k % 3 + 10, k % 17 == 5))  # (first, end, aggregation id, masked)
+        off += s
+
+    def run(eng):
+        for a, b, seg, masked in jobs:
+            res = eng.helper_initialized_batch(nonces[a:b], ps[a:b], his[a:b], lps[a:b])
+            np.testing.assert_array_equal(res.verdicts, want["verdicts"][a:b])
+            eng.accumulate(b - a, accept_mask=mask[a:b] if masked else None,
+                           segments=np.full(b - a, seg, np.uint32), batch_id=res.batch_id)
+        return {seg: eng.aggregate_share(seg) for seg in (10, 11, 12)}
+
+    exp = {}
+    for seg in (10, 11, 12):
+        sel = np.zeros(n, bool)
+        for a, b, sg, masked in jobs:
+            if sg == seg:
+                sel[a:b] = (want["verdicts"][a:b] == 0) & ((mask[a:b] != 0) if masked else True)
+        exp[seg] = _expected(orc, want, nonces, sel)
+    with HelperEngine(vdaf, vk) as eng:
+        got = run(eng)
+        assert got == exp
+        m = eng.memory()
+        assert m["resident_batches"] == 0
+        # deferred jobs before a reset are applied, then zeroed
+        a, b = jobs[0][0], jobs[0][1]
+        res = eng.helper_initialized_batch(nonces[a:b], ps[a:b], his[a:b], lps[a:b])
+        eng.accumulate(b - a, batch_id=res.batch_id)
+        eng.reset_aggregates()
+        assert eng.aggregate_share(0)[1] == 0
+    with HelperEngine(vdaf, vk) as eng:
+        eng.debug(8, 0)
+        assert run(eng) == exp

@@ -116,6 +116,9 @@ int main(int argc, char** argv) {
   int32_t st = jx_engine_create_ex(&p, vk.data(), (uint32_t)vk.size(), 0, &e);
   if (st) die("create", st, nullptr);
   if (coalesce && (st = jx_engine_coalesce(e, 1, window))) die("coalesce", st, e);
+  // measurement: JX_JOBS_DEFER=0 accumulates every job at once (jx_engine_debug option 8) instead of deferred
+  if (getenv("JX_JOBS_DEFER") && atoi(getenv("JX_JOBS_DEFER")) == 0 && (st = jx_engine_debug(e, 8, 0)))
+    die("debug 8", st, e);
   jx_engine* el = nullptr;
   if (TL > 0) {
     if ((st = jx_engine_create_ex(&p, lvk.data(), (uint32_t)lvk.size(), 0, &el))) die("create leader", st, nullptr);
