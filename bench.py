@@ -56,7 +56,7 @@ OPS_PER_MONT = 56
 OPS_PER_FMUL = 16
 ALG_OPS_PER_PERM = 3720
 ALG_OPS_PER_FMUL = 160
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06_pmc_summary.json")
 K1_KERNEL = "jx::xof_kernel<false, 0>"  # rocprofv3 name of the helper K1 (jx_kernels.hip)
 KERNEL_SOURCES = ["janus_amd/csrc/jx_kernels.hip", "janus_amd/csrc/jx_engine.cpp", "janus_amd/csrc/jx_kernels.h",
                   "janus_amd/csrc/jx_field.h", "janus_amd/csrc/jx_keccak.h", "janus_amd/csrc/jx_sha256.h"]

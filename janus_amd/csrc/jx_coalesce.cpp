@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <thread>
@@ -142,7 +143,7 @@ struct Coalescer {
   uint32_t window_us = 0;   // 0: automatic
   uint32_t min_jobs = 0;    // debug option 7 (tests): a gather waits (up to its window) for this many jobs
   uint64_t max_reports = 0; // reports per launch
-  bool enc_seen = false;    // helper lanes lay out the encrypted-input regions from now on
+  std::atomic<bool> enc_seen{false};  // helper lanes lay out the encrypted-input regions from now on
   clk::time_point last_job;
   size_t pinned = 0;        // bytes of pinned host rows held by the lanes
   uint64_t launches = 0, jobs = 0, reports = 0, enc_jobs = 0;
@@ -173,6 +174,15 @@ static std::string coal_key(const jx_engine* e) {
 constexpr uint32_t kQuietUs = 100;
 constexpr uint32_t kRejoinUs = 1000;
 constexpr uint32_t kMaxRunning = 2;
+// JX_COAL_MAX_RUNNING (measurement): launches of a role in flight before a gather waits for one to complete
+static uint32_t max_running() {
+  static const uint32_t v = [] {
+    const char* s = getenv("JX_COAL_MAX_RUNNING");
+    const int x = s ? atoi(s) : 0;
+    return x >= 1 && x <= (int)kLanes - 1 ? (uint32_t)x : kMaxRunning;
+  }();
+  return v;
+}
 
 // The longest a gathering lane waits for more jobs (automatic: 1.5x the role's recent launch latency,
 // 0.1-20 ms). It matters while another launch runs: the jobs that launch returns join this one instead of
@@ -470,12 +480,12 @@ static void dispatcher_main(Coalescer* C, int role) {
         continue;
       }
       // every caller of the completed launches is back: nobody else is expected, close without a quiet period
-      if (L.all_back && R.nrunning < kMaxRunning) break;
+      if (L.all_back && R.nrunning < max_running()) break;
       const auto quiet_at = L.last_arrival + std::chrono::microseconds(kQuietUs);
       const bool back = R.expect == 0 || now >= R.expect_until;
       // nothing of this role on the device and no caller of a completed launch still to come: waiting buys nothing
       if (R.nrunning == 0 && R.expect == 0) break;
-      if (now >= quiet_at && ((back && R.nrunning < kMaxRunning) || L.reports >= C->max_reports / 4)) break;
+      if (now >= quiet_at && ((back && R.nrunning < max_running()) || L.reports >= C->max_reports / 4)) break;
       auto until = deadline;
       if (now < quiet_at && quiet_at < until) until = quiet_at;
       if (!back && R.expect_until < until) until = R.expect_until;
@@ -708,8 +718,7 @@ void coalescer_set_min_jobs(jx_engine* e, uint32_t jobs) {
 bool coalescer_accepts(const jx_engine* e, bool leader, uint64_t n, bool encrypted, uint64_t ct_bytes) {
   Coalescer* C = e->coal;
   if (!C || n == 0) return false;
-  std::lock_guard<std::mutex> lk(C->mu);
-  const int role = leader ? LEADER : HELPER;
+  const int role = leader ? LEADER : HELPER;  // no lock: the lane limits are fixed, enc_seen only turns on
   return n <= lane_max_reports(C, role, role == HELPER && (C->enc_seen || encrypted)) &&
          (!encrypted || ct_bytes <= kPinnedBudget / 2);
 }
@@ -853,6 +862,7 @@ static int32_t coalesced(jx_engine* e, bool leader, uint64_t n, const uint8_t* n
   r.out_verdicts = out_verdicts;
   r.out_prep_shares = out_prep_shares;
   r.out_status = out_status;
+  Batch* Bp = nullptr;
   {
     std::lock_guard<FairMutex> el(e->mu);
     HIPCHK(e, hipSetDevice(e->device));
@@ -860,6 +870,7 @@ static int32_t coalesced(jx_engine* e, bool leader, uint64_t n, const uint8_t* n
     int32_t rc = batch_new(e, n, leader, &r.id, &B);
     if (rc) return rc;
     B->pending = true;
+    Bp = B;
     r.dst = JobSlice{0, n, B->outs, B->verdicts, B->msgs, B->nonces};
     r.batch_ev = B->slab.ev;
   }
@@ -932,12 +943,11 @@ static int32_t coalesced(jx_engine* e, bool leader, uint64_t n, const uint8_t* n
     fail(e, r.rc, r.err);
     return drop(r.rc);
   }
-  {
-    std::lock_guard<FairMutex> el(e->mu);
-    auto it = e->batches.find(r.id);
-    if (it != e->batches.end()) it->second.pending = false;
-    e->last_batch = r.id;
-  }
+  // the batch is ready: no engine mutex (the callers of a completed launch return together; each lock hand-off
+  // was a wake-up on the way back to the next job). Its map node is stable and no other call touches a pending
+  // batch.
+  __atomic_store_n(&Bp->pending, false, __ATOMIC_RELEASE);
+  e->last_batch.store(r.id);
   if (out_batch_id) *out_batch_id = r.id;
   return JX_OK;
 }

@@ -583,7 +583,7 @@ void jxi::batch_free(jx_engine* e, std::map<uint64_t, Batch>::iterator it) {
 
 static int32_t find_batch(jx_engine* e, uint64_t id, uint64_t n, const char* what, Batch** out) {
   auto it = e->batches.find(id);
-  if (id == 0 || it == e->batches.end() || it->second.pending)
+  if (id == 0 || it == e->batches.end() || __atomic_load_n(&it->second.pending, __ATOMIC_ACQUIRE))
     return fail(e, JX_E_STATE, std::string(what) + ": batch id names no resident prepared batch (released or never made)");
   if (it->second.n != n)
     return fail(e, JX_E_INVALID, std::string(what) + ": report count differs from the batch's");
@@ -1400,7 +1400,7 @@ int32_t jx_engine_batch_id(const jx_engine* e, uint64_t* batch_id) {
   if (!e || !batch_id) return JX_E_INVALID;
   LOCK(const_cast<jx_engine*>(e));
   auto it = e->batches.find(e->last_batch);
-  *batch_id = it != e->batches.end() && !it->second.pending ? e->last_batch : 0;
+  *batch_id = it != e->batches.end() && !__atomic_load_n(&it->second.pending, __ATOMIC_ACQUIRE) ? e->last_batch.load() : 0;
   return JX_OK;
 }
 
@@ -1463,7 +1463,7 @@ int32_t jx_batch_release(jx_engine* e, uint64_t batch_id) {
   if (!e) return JX_E_INVALID;
   LOCK(e);
   auto it = e->batches.find(batch_id);
-  if (batch_id == 0 || it == e->batches.end() || it->second.pending)
+  if (batch_id == 0 || it == e->batches.end() || __atomic_load_n(&it->second.pending, __ATOMIC_ACQUIRE))
     return fail(e, JX_E_STATE, "release: batch id names no resident prepared batch");
   HIPCHK(e, hipSetDevice(e->device));
   batch_free(e, it);

@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
@@ -89,7 +90,9 @@ struct Batch {
   uint64_t n = 0;
   bool leader = false;
   bool finished = false;      // leader: prepare_next has run (once)
-  bool pending = false;       // a coalesced launch is still writing it (not visible to other calls yet)
+  // a coalesced launch is still writing it (not visible to other calls yet); cleared by the job's caller without
+  // the engine mutex (atomic builtins; other calls read it under the mutex)
+  bool pending = false;
   Slab slab;                  // one arena allocation: outs | verdicts | msgs | nonces
   uint4* outs = nullptr;      // interleaved [n/64][out_len][64] (Histogram: the measurement share)
   uint8_t* verdicts = nullptr;
@@ -226,7 +229,8 @@ struct jx_engine {
   uint32_t seg_next = 0;                  // next free state in seg_slabs.back()
   // resident prepared batches by handle; handles are never reused
   std::map<uint64_t, jxi::Batch> batches;
-  uint64_t batch_gen = 0, last_batch = 0;
+  uint64_t batch_gen = 0;
+  std::atomic<uint64_t> last_batch{0};  // a coalesced prepare sets it without the engine mutex
   // segmented accumulation: pointers into the call's arena scratch while it runs (accumulate_many)
   uint32_t* d_segx = nullptr;  // cnt, off, cursor [SEG_MAX each], ioff [SEG_MAX + 1], nitems [2]
   uint32_t* d_perm = nullptr;
