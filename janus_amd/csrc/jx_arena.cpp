@@ -13,7 +13,9 @@
 // frees idle slabs (those whose last user has finished first; the waits and hipFree run outside the arena's
 // lock, so one trim never stalls another engine's check-out), then (for per-call staging, by a caller that
 // holds no slab) waits for another caller's staging to come back; otherwise JX_E_NOMEM.
+#include <cstdio>
 #include <cstdlib>
+#include <ctime>
 
 #include "jx_engine_internal.h"
 
@@ -40,14 +42,38 @@ Arena* arena_for(int device) {
   return A;
 }
 
+// JX_ARENA_TRIM_LOG=<path> (measurement): one line per freed slab, "monotonic <free start> <free end> boottime
+// <free start> <free end> <bytes> <wait ns>": the hipFree's interval in both clocks (to line it up with a kernel
+// trace, tools/stream_gaps.py --trims) and how long the trimming thread first waited for the slab's last user.
+static uint64_t now_ns(clockid_t id) {
+  timespec t;
+  clock_gettime(id, &t);
+  return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+static void log_free(uint64_t m0, uint64_t b0, uint64_t wait_ns, size_t bytes) {
+  static const char* path = getenv("JX_ARENA_TRIM_LOG");
+  if (!path) return;
+  const uint64_t m1 = now_ns(CLOCK_MONOTONIC), b1 = now_ns(CLOCK_BOOTTIME);
+  static std::mutex mu;
+  std::lock_guard<std::mutex> g(mu);
+  if (FILE* f = fopen(path, "a")) {
+    fprintf(f, "monotonic %llu %llu boottime %llu %llu %zu %llu\n", (unsigned long long)m0, (unsigned long long)m1,
+            (unsigned long long)b0, (unsigned long long)b1, bytes, (unsigned long long)wait_ns);
+    fclose(f);
+  }
+}
+
 // Waits for the slab's last user and frees it. Never with A->mu held: the wait can be a 100 ms K1 launch, and
 // every engine's check-outs on the device would stall behind it.
 static void slab_destroy(Slab& s) {
+  const uint64_t w0 = now_ns(CLOCK_MONOTONIC);
   if (s.ev) {
     (void)hipEventSynchronize(s.ev);  // its last user's work
     (void)hipEventDestroy(s.ev);
   }
+  const uint64_t m0 = now_ns(CLOCK_MONOTONIC), b0 = now_ns(CLOCK_BOOTTIME);
   (void)hipFree(s.p);
+  log_free(m0, b0, m0 - w0, s.bytes);
   s = Slab{};
 }
 
@@ -119,8 +145,20 @@ hipError_t arena_get(Arena* A, size_t bytes, hipStream_t s, bool staging, bool m
       }
       if (busy == A->free.end()) busy = it;
     }
-    (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
     const bool room = A->allocated + bytes <= A->budget;
+    // With no room for a new slab, any larger idle slab before freeing one: a trim stalls its caller for the
+    // slab's last user and the hipFree (72 + 49 ms for a 640 MB slab; 7 -> 1 trims in the two-engine trace,
+    // profiles/r06_arena_stream_gaps.json, where the other engine kept launching through the free).
+    if (pick == A->free.end() && !room) {
+      for (auto it = hi; it != A->free.end(); ++it) {
+        if (it->second.last == s || !it->second.last || hipEventQuery(it->second.ev) == hipSuccess) {
+          pick = it;
+          break;
+        }
+        if (busy == A->free.end()) busy = it;
+      }
+    }
+    (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
     if (pick == A->free.end() && busy != A->free.end() && !room) pick = busy;
     if (pick != A->free.end()) {
       out = pick->second;

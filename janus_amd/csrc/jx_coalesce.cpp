@@ -48,6 +48,7 @@ namespace {
 
 using clk = std::chrono::steady_clock;
 constexpr uint32_t kLanes = 4;                   // one gathering lane per role + launches in flight
+constexpr uint32_t kMaxLanes = 8;                // JX_COAL_LANES (measurement) may raise the lanes up to this
 constexpr size_t kPinnedBudget = 512ull << 20;   // the largest lane: pinned input rows
 constexpr uint32_t kIdleFreeMs = 2000;           // pinned rows go back to the OS after this long without jobs
 constexpr uint64_t kMinLaneReports = 1024;
@@ -131,7 +132,8 @@ struct Coalescer {
   jx_engine* base = nullptr;  // owns the constant tables the lanes share
   std::mutex mu;
   std::condition_variable cv_comp, cv_lane;  // the completer (a launch queued); callers waiting for a free lane
-  Lane lanes[kLanes];
+  Lane lanes[kMaxLanes];
+  uint32_t nlanes = kLanes;
   RoleState role[NROLES];
   std::vector<int> running;
   // per lane, a host-coherent pinned flag (one per 64-byte line) the lane's launch sets to its seq when done
@@ -179,7 +181,7 @@ static uint32_t max_running() {
   static const uint32_t v = [] {
     const char* s = getenv("JX_COAL_MAX_RUNNING");
     const int x = s ? atoi(s) : 0;
-    return x >= 1 && x <= (int)kLanes - 1 ? (uint32_t)x : kMaxRunning;
+    return x >= 1 && x <= (int)kMaxLanes - 1 ? (uint32_t)x : kMaxRunning;
   }();
   return v;
 }
@@ -537,7 +539,7 @@ constexpr uint32_t kEventCheckUs = 2000;
 static void completer_main(Coalescer* C) {
   (void)hipSetDevice(C->device);
   std::unique_lock<std::mutex> lk(C->mu);
-  std::vector<clk::time_point> checked(kLanes);
+  std::vector<clk::time_point> checked(kMaxLanes);
   for (;;) {
     C->cv_comp.wait(lk, [&] { return C->stop || !C->running.empty(); });
     if (C->running.empty() && C->stop) return;
@@ -626,7 +628,7 @@ Coalescer* coalescer_for(jx_engine* e) {
   // a launch: up to half the fused path's launch size (its staging comes from the arena per launch)
   C->max_reports = e->auto_chunk / 2 < 4096 ? 4096 : e->auto_chunk / 2;
   C->last_job = clk::now();
-  if (hipHostMalloc((void**)&C->hflag, kLanes * kFlagStride * sizeof(uint32_t),
+  if (hipHostMalloc((void**)&C->hflag, kMaxLanes * kFlagStride * sizeof(uint32_t),
                     hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer((void**)&C->dflag, C->hflag, 0) != hipSuccess) {
     if (C->hflag) (void)hipHostFree(C->hflag);
@@ -635,8 +637,12 @@ Coalescer* coalescer_for(jx_engine* e) {
     delete C;
     return nullptr;
   }
-  memset(C->hflag, 0, kLanes * kFlagStride * sizeof(uint32_t));
-  for (uint32_t k = 0; k < kLanes; k++) {
+  memset(C->hflag, 0, kMaxLanes * kFlagStride * sizeof(uint32_t));
+  if (const char* env = getenv("JX_COAL_LANES")) {
+    const int x = atoi(env);
+    if (x >= 2 && x <= (int)kMaxLanes) C->nlanes = (uint32_t)x;
+  }
+  for (uint32_t k = 0; k < C->nlanes; k++) {
     Lane& L = C->lanes[k];
     L.q = new_child(base);
     // the completer polls this event (a blocking-sync event's interrupt wake-up measured ms late)
@@ -798,7 +804,7 @@ static Lane* reserve(Coalescer* C, std::unique_lock<std::mutex>& lk, CReq* r, in
       L.full = true;  // close it now; wait for the next lane
       R.cv.notify_one();
     } else {
-      for (uint32_t k = 0; k < kLanes; k++) {
+      for (uint32_t k = 0; k < C->nlanes; k++) {
         Lane& L = C->lanes[k];
         if (L.state != FREE) continue;
         int32_t lr = lane_layout(C, L, r->role, r->n, r->ct_bytes);
