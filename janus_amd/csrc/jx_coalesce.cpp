@@ -115,6 +115,7 @@ struct RoleState {
   int open = -1;
   std::condition_variable cv;  // the role's dispatcher: a job joined, copies done, a launch completed
   uint32_t nrunning = 0;       // the role's launches queued on the device and not yet done
+  uint64_t run_reports = 0;    // their reports
   uint32_t expect = 0;         // jobs of completed launches not yet back (closed-loop callers return)
   clk::time_point expect_until;  // ... expected until then
   double ewma_us = 0;          // launch latency
@@ -176,6 +177,15 @@ static std::string coal_key(const jx_engine* e) {
 constexpr uint32_t kQuietUs = 100;
 constexpr uint32_t kRejoinUs = 1000;
 constexpr uint32_t kMaxRunning = 2;
+// JX_COAL_MERGE=1 (measurement): a gather less than half the size of the role's running launches waits for
+// their callers instead of closing as a fragment
+static bool merge_fragments() {
+  static const bool v = [] {
+    const char* s = getenv("JX_COAL_MERGE");
+    return s && atoi(s) == 1;
+  }();
+  return v;
+}
 // JX_COAL_MAX_RUNNING (measurement): launches of a role in flight before a gather waits for one to complete
 static uint32_t max_running() {
   static const uint32_t v = [] {
@@ -335,11 +345,6 @@ static int32_t launch_lane(Coalescer* C, Lane& L, std::string& err) {
     err = thread_error();
     return rc;
   }
-  // every job's batch slab: after its previous user
-  for (CReq* r : L.reqs) {
-    hipError_t s = hipStreamWaitEvent(q->stream, r->batch_ev, 0);
-    if (s != hipSuccess) return bad(s, "hipStreamWaitEvent");
-  }
   // Transfers are kernels on the lane's streams reading / writing the mapped pinned rows (launch_copy_regions): a
   // copy-engine command of this lane could queue behind another lane's download, which waits for that lane's
   // K1 (measured 1-2 ms stalls per launch at 64 x 100-report jobs, profiles/r06_jobs_trace_*).
@@ -376,15 +381,24 @@ static int32_t launch_lane(Coalescer* C, Lane& L, std::string& err) {
   }
   flat(ua, q->d_jobs, L.o_jobs, L.reqs.size() * sizeof(JobSlice));
   hipError_t s = launch_copy_regions(ua, q->stream);
+  // the rest of the leader prep-share rows: on the lane's upload stream once the lane's previous launch has read
+  // d_lps (ev_up0), queued right after K1 so that nothing but the upload and this record precede K1
   hipEvent_t before_flp = nullptr;
+  std::function<int32_t()> side;
   if (s == hipSuccess && split_lps) {
-    CopyArgs ra{};
-    add(ra, q->d_lps, P, hin + L.o_lps, P, P - 16, m);
-    s = hipEventRecord(L.ev_up0, q->stream);  // after the waits above and the previous launch's reads of d_lps
-    if (s == hipSuccess) s = hipStreamWaitEvent(L.up, L.ev_up0, 0);
-    if (s == hipSuccess) s = launch_copy_regions(ra, L.up);
-    if (s == hipSuccess) s = hipEventRecord(L.ev_up, L.up);
+    s = hipEventRecord(L.ev_up0, q->stream);
     before_flp = L.ev_up;
+    side = [&]() -> int32_t {
+      CopyArgs ra{};
+      add(ra, q->d_lps, P, hin + L.o_lps, P, P - 16, m);
+      hipError_t t = hipStreamWaitEvent(L.up, L.ev_up0, 0);
+      if (t == hipSuccess) t = launch_copy_regions(ra, L.up);
+      if (t == hipSuccess) t = hipEventRecord(L.ev_up, L.up);
+      if (t != hipSuccess)  // prep_core returns it; the launch's error path synchronises the lane's streams
+        return fail(q, t == hipErrorOutOfMemory ? JX_E_NOMEM : JX_E_HIP,
+                    std::string("coalesced launch: upload: ") + hipGetErrorString(t));
+      return JX_OK;
+    };
   }
   if (s != hipSuccess) return bad(s, "upload");
   if (L.has_enc) {  // open the encrypted reports into their helper input-share rows
@@ -395,7 +409,7 @@ static int32_t launch_lane(Coalescer* C, Lane& L, std::string& err) {
   }
   rc = prep_core(q, m, q->d_nonces, q->d_ps, q->d_his, q->d_lps, q->d_verdicts, q->d_msgs, staging_outs(q),
                  leader ? q->d_lis : nullptr, leader ? q->d_lps_out : nullptr, leader ? q->lis_stride : 0, q->d_vkeys,
-                 before_flp);
+                 before_flp, side ? &side : nullptr);
   if (rc) {
     err = thread_error();
     (void)hipStreamSynchronize(L.up);
@@ -405,6 +419,11 @@ static int32_t launch_lane(Coalescer* C, Lane& L, std::string& err) {
   if (L.has_enc) {
     s = launch_open_mask(q->d_status, q->d_verdicts, m, q->stream);
     if (s != hipSuccess) return bad(s, "open mask");
+  }
+  // every job's batch slab (only the scatter writes it): after its previous user
+  for (CReq* r : L.reqs) {
+    s = hipStreamWaitEvent(q->stream, r->batch_ev, 0);
+    if (s != hipSuccess) return bad(s, "hipStreamWaitEvent");
   }
   s = launch_scatter_jobs(c, q->d_jobs, (uint32_t)L.reqs.size(), max_job,
                           staging_outs(q), q->d_verdicts, q->d_msgs, q->d_nonces, q->stream);
@@ -481,6 +500,10 @@ static void dispatcher_main(Coalescer* C, int role) {
         R.cv.wait_until(lk, deadline);
         continue;
       }
+      if (merge_fragments() && R.nrunning > 0 && 2 * L.reports < R.run_reports) {
+        R.cv.wait_until(lk, deadline);
+        continue;
+      }
       // every caller of the completed launches is back: nobody else is expected, close without a quiet period
       if (L.all_back && R.nrunning < max_running()) break;
       const auto quiet_at = L.last_arrival + std::chrono::microseconds(kQuietUs);
@@ -524,6 +547,7 @@ static void dispatcher_main(Coalescer* C, int role) {
     } else {
       L.state = RUNNING;
       R.nrunning++;
+      R.run_reports += L.reports;
       C->running.push_back((int)(&L - C->lanes));
       C->cv_comp.notify_one();
     }
@@ -580,6 +604,7 @@ static void completer_main(Coalescer* C) {
       R.ewma_us = R.ewma_us > 0 ? 0.8 * R.ewma_us + 0.2 * us : us;
       C->t_device += us;
       R.nrunning--;
+      R.run_reports -= L.reports;
       R.expect += (uint32_t)L.reqs.size();  // this launch's callers will be back with their next jobs
       R.expect_until = now + std::chrono::microseconds(kRejoinUs);
       R.cv.notify_one();  // a gathering lane may close now
@@ -878,7 +903,7 @@ static int32_t coalesced(jx_engine* e, bool leader, uint64_t n, const uint8_t* n
     B->pending = true;
     Bp = B;
     r.dst = JobSlice{0, n, B->outs, B->verdicts, B->msgs, B->nonces};
-    r.batch_ev = B->slab.ev;
+    r.batch_ev = B->wait_ev ? B->wait_ev : B->slab.ev;
   }
   auto drop = [&](int32_t rc) {
     std::lock_guard<FairMutex> el(e->mu);

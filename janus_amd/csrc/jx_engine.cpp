@@ -561,9 +561,19 @@ int32_t jxi::batch_new(jx_engine* e, uint64_t n, bool leader, uint64_t* id, Batc
   Batch b;
   b.n = n;
   b.leader = leader;
-  hipError_t st = arena_get(e->arena, bytes, e->stream, false, false, b.slab);
-  if (st == hipErrorOutOfMemory) return nomem(e, "new batch", bytes);
-  HIPCHK(e, st);
+  // a slab a deferred-accumulate flush has read (the same job size comes back every time): no arena round trip;
+  // its users wait on that flush (e->stream is in order after it already)
+  auto rit = e->recycle.lower_bound(bytes);
+  if (rit != e->recycle.end() && rit->first <= bytes + bytes / 4) {
+    b.slab = rit->second;
+    b.wait_ev = e->ev_flush;
+    e->recycle_bytes -= rit->first;
+    e->recycle.erase(rit);
+  } else {
+    hipError_t st = arena_get(e->arena, bytes, e->stream, false, false, b.slab);
+    if (st == hipErrorOutOfMemory) return nomem(e, "new batch", bytes);
+    HIPCHK(e, st);
+  }
   uint8_t* m = (uint8_t*)b.slab.p;
   b.outs = (uint4*)(m + o_outs);
   b.verdicts = m + o_ver;
@@ -634,7 +644,8 @@ static bool use_inplace(const jx_engine* e) { return leader_inplace(e->cfg); }
 // seeds to verdicts / msgs.
 int32_t jxi::prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* his,
                        const uint8_t* lps, uint8_t* verdicts, uint8_t* msgs, uint4* outs, const uint8_t* lis,
-                       uint8_t* lps_out, uint64_t lis_rs, const uint8_t* vkeys, hipEvent_t before_flp) {
+                       uint8_t* lps_out, uint64_t lis_rs, const uint8_t* vkeys, hipEvent_t before_flp,
+                       const std::function<int32_t()>* after_k1) {
   const Cfg& c = e->cfg;
   const bool leader = lis != nullptr;
   Bufs b{};
@@ -736,6 +747,10 @@ int32_t jxi::prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const ui
     }
     if (big) HIPCHK(e, arena_big_record(e->arena, e, e->stream));
     HIPCHK(e, stage_end(e, ST_XOF, ev));
+    if (after_k1) {
+      const int32_t rc = (*after_k1)();
+      if (rc) return rc;
+    }
     if (!leader) {  // the leader's shares are explicit: no rejection-sampled streams to redo
       HIPCHK(e, stage_begin(e, &ev));
       HIPCHK(e, launch_xof_slow(c, b, e->stream));
@@ -786,6 +801,7 @@ static int32_t accumulate_one(jx_engine* e, const AccSrc& src, const uint8_t* d_
 // aggregation instead of one per job takes the per-job kernel launch off the engine mutex (a coalesced 100-report
 // job's callers return together, and each one's accumulate launch serialised them).
 constexpr uint64_t kAccQReports = 16384;  // a flush once this many reports wait (their batches hold HBM)
+constexpr size_t kRecycleBytes = 512ull << 20;  // batch slabs an engine keeps from its flushes
 static int32_t flush_acc(jx_engine* e) {
   if (e->accq.empty()) return JX_OK;
   std::vector<std::pair<Batch, uint32_t>> q;
@@ -818,8 +834,21 @@ static int32_t flush_acc(jx_engine* e) {
     }
     return JX_OK;
   };
-  const int32_t rc = run();
-  for (auto& p : q) arena_put(e->arena, p.first.slab, e->stream);  // after the launches that read them
+  int32_t rc = run();
+  // the slabs: kept for the engine's next batches behind one event (up to kRecycleBytes), the rest back to the
+  // arena, after the launches that read them
+  if (rc == JX_OK && !e->ev_flush && hipEventCreateWithFlags(&e->ev_flush, hipEventDisableTiming) != hipSuccess)
+    e->ev_flush = nullptr;
+  const bool keep = rc == JX_OK && e->ev_flush && hipEventRecord(e->ev_flush, e->stream) == hipSuccess;
+  for (auto& p : q) {
+    Slab& sl = p.first.slab;
+    if (keep && e->recycle_bytes + sl.bytes <= kRecycleBytes) {
+      e->recycle_bytes += sl.bytes;
+      e->recycle.emplace(sl.bytes, sl);
+    } else {
+      arena_put(e->arena, sl, e->stream);
+    }
+  }
   return rc;
 }
 #define FLUSH_ACC(e)                 \
@@ -1182,6 +1211,8 @@ void jx_engine_destroy(jx_engine* e) {
   if (e->arena) {
     for (auto& p : e->accq) arena_put(e->arena, p.first.slab, e->stream);  // deferred accumulations: unread
     e->accq.clear();
+    for (auto& kv : e->recycle) arena_put(e->arena, kv.second, e->stream);
+    e->recycle.clear();
     for (Slab& sl : e->seg_slabs) arena_put(e->arena, sl, e->stream);
     for (auto& kv : e->batches) arena_put(e->arena, kv.second.slab, e->stream);
   }
@@ -1196,6 +1227,7 @@ void jx_engine_destroy(jx_engine* e) {
   }
   if (e->h_acc) (void)hipHostFree(e->h_acc);
   if (e->ev_hacc) (void)hipEventDestroy(e->ev_hacc);
+  if (e->ev_flush) (void)hipEventDestroy(e->ev_flush);
   if (e->ev_wait) (void)hipEventDestroy(e->ev_wait);
   if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   if (e->arena) arena_big_forget(e->arena, e);

@@ -9,6 +9,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <string>
@@ -94,6 +95,7 @@ struct Batch {
   // the engine mutex (atomic builtins; other calls read it under the mutex)
   bool pending = false;
   Slab slab;                  // one arena allocation: outs | verdicts | msgs | nonces
+  hipEvent_t wait_ev = nullptr;  // a slab recycled by a deferred-accumulate flush: that flush (else slab.ev)
   uint4* outs = nullptr;      // interleaved [n/64][out_len][64] (Histogram: the measurement share)
   uint8_t* verdicts = nullptr;
   uint8_t* msgs = nullptr;
@@ -255,6 +257,10 @@ struct jx_engine {
   std::vector<std::pair<jxi::Batch, uint32_t>> accq;  // (batch, aggregation id)
   uint64_t accq_reports = 0;
   bool acc_defer = true;      // debug option 8
+  // batch slabs the flushes read, kept for the engine's next batches (no arena round trip, one event per flush)
+  std::multimap<size_t, jxi::Slab> recycle;
+  size_t recycle_bytes = 0;
+  hipEvent_t ev_flush = nullptr;
   uint64_t acc_flushes = 0, acc_deferred = 0;
   uint32_t* d_err = nullptr;  // combine kernels: non-canonical input seen (reported by jx_engine_sync)
   // timing
@@ -311,7 +317,8 @@ size_t stage_bytes(const jx_engine* e, uint64_t cap, uint32_t flags);
 int32_t prep_core(jx_engine* e, uint64_t n, const uint8_t* nonces, const uint8_t* ps, const uint8_t* his,
                   const uint8_t* lps, uint8_t* verdicts, uint8_t* msgs, uint4* outs, const uint8_t* lis = nullptr,
                   uint8_t* lps_out = nullptr, uint64_t lis_rs = 0, const uint8_t* vkeys = nullptr,
-                  hipEvent_t before_flp = nullptr);  // the FLP stage (K3) also waits on this event
+                  hipEvent_t before_flp = nullptr,  // the FLP stage (K3) also waits on this event
+                  const std::function<int32_t()>* after_k1 = nullptr);  // queued right after K1 (before K1', K3)
 uint4* staging_outs(jx_engine* e);
 int32_t batch_new(jx_engine* e, uint64_t n, bool leader, uint64_t* id, Batch** out);
 void batch_free(jx_engine* e, std::map<uint64_t, Batch>::iterator it);
