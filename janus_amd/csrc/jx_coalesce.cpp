@@ -146,6 +146,7 @@ struct Coalescer {
   uint32_t window_us = 0;   // 0: automatic
   uint32_t min_jobs = 0;    // debug option 7 (tests): a gather waits (up to its window) for this many jobs
   uint64_t max_reports = 0; // reports per launch
+  uint64_t flat_reports = 0;  // launches up to this size take the same device time (merge_groups)
   std::atomic<bool> enc_seen{false};  // helper lanes lay out the encrypted-input regions from now on
   clk::time_point last_job;
   size_t pinned = 0;        // bytes of pinned host rows held by the lanes
@@ -177,9 +178,13 @@ static std::string coal_key(const jx_engine* e) {
 constexpr uint32_t kQuietUs = 100;
 constexpr uint32_t kRejoinUs = 1000;
 constexpr uint32_t kMaxRunning = 2;
-// JX_COAL_MERGE=1 (measurement): a gather less than half the size of the role's running launches waits for
-// their callers instead of closing as a fragment
-static bool merge_fragments() {
+// JX_COAL_MERGE=1 (measurement, off by default): a gather that opens while a launch of its role runs, and that
+// together with it stays below flat_reports (where a launch's device time does not depend on its size), waits for
+// that launch's callers instead of closing as a group of its own. Measured (profiles/r06_jobs_merge_ab.jsonl): it
+// would stop a late caller from splitting 10 workers into two alternating groups (5.7-7.4 jobs per launch and
+// 301-317k reports/s in the runs that split, 330k in those that do not), but at 64 x 100 the groups then take
+// turns on the device: 0.89M against 1.15M. Off.
+static bool merge_groups() {
   static const bool v = [] {
     const char* s = getenv("JX_COAL_MERGE");
     return s && atoi(s) == 1;
@@ -500,7 +505,7 @@ static void dispatcher_main(Coalescer* C, int role) {
         R.cv.wait_until(lk, deadline);
         continue;
       }
-      if (merge_fragments() && R.nrunning > 0 && 2 * L.reports < R.run_reports) {
+      if (merge_groups() && R.nrunning > 0 && L.reports + R.run_reports <= C->flat_reports) {
         R.cv.wait_until(lk, deadline);
         continue;
       }
@@ -652,6 +657,7 @@ Coalescer* coalescer_for(jx_engine* e) {
   C->base = base;
   // a launch: up to half the fused path's launch size (its staging comes from the arena per launch)
   C->max_reports = e->auto_chunk / 2 < 4096 ? 4096 : e->auto_chunk / 2;
+  C->flat_reports = e->round_reports / 16;  // one lane-pair workgroup per CU (prep_core), 8,192 SumVec reports
   C->last_job = clk::now();
   if (hipHostMalloc((void**)&C->hflag, kMaxLanes * kFlagStride * sizeof(uint32_t),
                     hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
