@@ -95,6 +95,21 @@ void ht_fe(int op, const uint8_t a[32], const uint8_t b[32], uint8_t out[32]) {
   fe_to_bytes(ow, r);
   memcpy(out, ow, 32);
 }
+// op 0 mul, 1 sq, 4 mul_small(121665) on raw limbs (loosely reduced inputs up to 2^28 - 1, as fe_sub / fe_add
+// produce them inside the ladder); the output limbs as the reduction leaves them (bounds checked by the test)
+void ht_fe_limbs(int op, const uint32_t a[10], const uint32_t b[10], uint32_t out[10]) {
+  fe x, y, r;
+  for (int i = 0; i < 10; i++) {
+    x.v[i] = a[i];
+    y.v[i] = b[i];
+  }
+  switch (op) {
+    case 0: fe_mul(r, x, y); break;
+    case 1: fe_sq(r, x); break;
+    default: fe_mul_small(r, x, 121665); break;
+  }
+  for (int i = 0; i < 10; i++) out[i] = r.v[i];
+}
 static uint8_t HT_SBOX[256];
 static void ht_sbox_init() {
   // FIPS 197 S-box generated from GF(2^8) inverses (independent of the kernel's table)

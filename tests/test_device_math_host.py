@@ -230,6 +230,30 @@ def test_fe25519_ops(ht):
             assert int.from_bytes(out.raw, "little") == pow(a, P25519 - 2, P25519)
 
 
+def test_fe25519_reduction_bounds(ht):
+    """The product reduction on the loosest inputs the ladder makes (every limb up to 2^28 - 1): the value is the
+    product mod p, and the output limbs stay within what fe_sub's 2p needs (limb 0 < 2^26 + 19, limbs 1..8 <=
+    2^26, limb 9 <= 2^21)."""
+    rnd = random.Random(25519)
+    L = ctypes.c_uint32 * 10
+    ht.ht_fe_limbs.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    top = (1 << 28) - 1
+    cases = [[top] * 10, [0] * 10, [1] + [0] * 9] + [[rnd.randrange(1 << 28) for _ in range(10)] for _ in range(300)]
+    cases += [[rnd.choice([0, top, 1 << 26, (1 << 26) - 1, 1 << 27]) for _ in range(10)] for _ in range(100)]
+
+    def val(v):
+        return sum(x << (26 * i) for i, x in enumerate(v))
+
+    for i, a in enumerate(cases):
+        b = cases[(7 * i + 3) % len(cases)]
+        for op in (0, 1, 4):
+            out = L()
+            ht.ht_fe_limbs(op, L(*a), L(*b), out)
+            want = val(a) * (val(b) if op == 0 else val(a) if op == 1 else 121665) % P25519
+            assert val(out) % P25519 == want, (op, a, b)
+            assert out[0] < (1 << 26) + 19 and all(x <= 1 << 26 for x in out[1:9]) and out[9] <= 1 << 21, list(out)
+
+
 def test_x25519_vs_oracle(ht):
     from oracle import hpke_oracle as H
     rnd = random.Random(11)
