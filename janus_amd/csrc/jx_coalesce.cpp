@@ -178,16 +178,20 @@ static std::string coal_key(const jx_engine* e) {
 constexpr uint32_t kQuietUs = 100;
 constexpr uint32_t kRejoinUs = 1000;
 constexpr uint32_t kMaxRunning = 2;
-// JX_COAL_MERGE=1 (measurement, off by default): a gather that opens while a launch of its role runs, and that
-// together with it stays below flat_reports (where a launch's device time does not depend on its size), waits for
-// that launch's callers instead of closing as a group of its own. Measured (profiles/r06_jobs_merge_ab.jsonl): it
-// would stop a late caller from splitting 10 workers into two alternating groups (5.7-7.4 jobs per launch and
-// 301-317k reports/s in the runs that split, 330k in those that do not), but at 64 x 100 the groups then take
-// turns on the device: 0.89M against 1.15M. Off.
+// Below flat_reports (the word-per-lane K1's range, 1,024 SumVec reports) a launch takes the same time whatever its
+// size. A gather that opens while a launch of its role runs, and that fits that range together with it, waits for
+// that launch's callers instead of closing as a group of its own: a late caller would otherwise split a few
+// workers into two groups that alternate for good, each launch sharing the CUs with the other's (10 x 100-report
+// jobs: 5.3-7.4 jobs per launch and 292-317k reports/s in the runs that split, 10 and ~330k otherwise). A
+// completion also clears the gathering lane's all-back mark, which was stale and closed such a gather before the
+// callers it now expects were back. Measured (profiles/r06_jobs_merge_ab.jsonl, runs r06mgc/d): every 10-worker
+// run at 10 jobs per launch, 64 x 100 unchanged (1.15-1.21M), sealed 64 x 100 0.90-0.91M against 0.84-0.87M. An
+// 8,192-report range instead (the lane-pair kernel's) made 64 x 100 take turns on the device: 0.89M.
+// JX_COAL_MERGE=0 turns it off (A/B).
 static bool merge_groups() {
   static const bool v = [] {
     const char* s = getenv("JX_COAL_MERGE");
-    return s && atoi(s) == 1;
+    return !(s && atoi(s) == 0);
   }();
   return v;
 }
@@ -612,6 +616,7 @@ static void completer_main(Coalescer* C) {
       R.run_reports -= L.reports;
       R.expect += (uint32_t)L.reqs.size();  // this launch's callers will be back with their next jobs
       R.expect_until = now + std::chrono::microseconds(kRejoinUs);
+      if (R.open >= 0) C->lanes[R.open].all_back = false;  // the gathering lane now expects these callers too
       R.cv.notify_one();  // a gathering lane may close now
       finish_lane(C, L, d.second == hipSuccess ? JX_OK : JX_E_HIP,
                   d.second == hipSuccess ? std::string() : std::string("coalesced launch: ") + hipGetErrorString(d.second));
@@ -657,7 +662,9 @@ Coalescer* coalescer_for(jx_engine* e) {
   C->base = base;
   // a launch: up to half the fused path's launch size (its staging comes from the arena per launch)
   C->max_reports = e->auto_chunk / 2 < 4096 ? 4096 : e->auto_chunk / 2;
-  C->flat_reports = e->round_reports / 16;  // one lane-pair workgroup per CU (prep_core), 8,192 SumVec reports
+  // the word-per-lane K1's range (one report-wave per SIMD, 1,024 SumVec reports): a launch of all of them takes
+  // the time of a launch of a few (prep_core)
+  C->flat_reports = e->round_reports / 128;
   C->last_job = clk::now();
   if (hipHostMalloc((void**)&C->hflag, kMaxLanes * kFlagStride * sizeof(uint32_t),
                     hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||

@@ -1,4 +1,4 @@
-# Round 6: group merging A/B (JX_COAL_MERGE=0 off, 1 on: the default) at 64 and 10 threads, plain and HPKE-sealed 100-report SumVec jobs
+# Round 6: group merging A/B (JX_COAL_MERGE=0 off, 1 on = the default) at 64 and 10 threads, plain and HPKE-sealed 100-report SumVec jobs
 # (tools/bench_jobs.py: every job and the aggregate verified), 2 s per case.
 # usage: bash scripts/gpu_r06_merge_ab.sh <name>
 set -o pipefail
