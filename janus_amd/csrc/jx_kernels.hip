@@ -16,6 +16,7 @@
 //
 // Prio3Count (Field64, 3 permutations) runs as one lane-per-report kernel.
 // Algorithm: draft-irtf-cfrg-vdaf-08 as implemented by prio 0.16.1; see DESIGN.md.
+#include <cstdlib>
 #include <stdlib.h>
 
 #include <type_traits>
@@ -3692,8 +3693,15 @@ hipError_t launch_copy_regions(const CopyArgs& a, hipStream_t s) {
     const uint64_t items = vec ? g.width / 16 * g.rows : g.width * g.rows;
     if (items > most) most = items;
   }
+  // PCIe-bound: a few hundred waves keep enough reads in flight, and a big launch's K1 keeps the rest of the
+  // SIMDs (JX_COPY_WGS overrides the cap for measurement)
+  static const uint64_t cap = [] {
+    const char* e = getenv("JX_COPY_WGS");
+    const long v = e ? atol(e) : 0;
+    return v >= 1 && v <= 4096 ? (uint64_t)v : (uint64_t)64;
+  }();
   uint64_t gx = (most + 255) / 256;
-  if (gx > 512) gx = 512;
+  if (gx > cap) gx = cap;
   if (gx == 0) gx = 1;
   hipLaunchKernelGGL(copy_regions_kernel, dim3((uint32_t)gx, a.nr), dim3(256), 0, s, a);
   return hipGetLastError();
