@@ -38,15 +38,19 @@ JX_HD void fe_from_bytes(fe& h, const uint32_t w[8]) {  // 32 bytes LE (8 LE wor
   }
 }
 
-// reduce 20 64-bit columns (sum c[k] 2^(26k)) to a loosely reduced element
+// Reduce the 64-bit columns of a product (sum c[k] 2^(26k), k < 19; the inputs' limbs < 2^28, so every column
+// < 10 * 2^56 < 2^59.4) to a loosely reduced element. One open is ~2,800 of these in a chain, and the wave issues
+// them alone on its SIMD, so the count of instructions is the time: the high columns fold down first, split at
+// bit 26 (2^260 == 608: the low part to k - 10, the high part to k - 9; no column can overflow), then ONE carry
+// chain over the ten limbs and the carry out of bit 255 back x19 (instead of a 19-limb chain before the fold and a
+// second chain after it). Out: limb 0 < 2^26, limb 1 < 2^26 + 2^17, limbs 2..8 < 2^26, limb 9 < 2^21 (fe_sub's 2p
+// needs <= 2^27 - 38, 2^27 - 2, 2^22 - 2).
 JX_HD void fe_reduce_cols(fe& h, uint64_t c[20]) {
 #pragma unroll
-  for (int k = 0; k < 19; k++) {
-    c[k + 1] += c[k] >> 26;
-    c[k] &= M26;
+  for (int k = 10; k < 19; k++) {
+    c[k - 10] += 608ull * (c[k] & M26);
+    c[k - 9] += 608ull * (c[k] >> 26);
   }
-#pragma unroll
-  for (int k = 10; k < 20; k++) c[k - 10] += 608ull * c[k];  // 2^260 == 2^5 * 19
 #pragma unroll
   for (int k = 0; k < 9; k++) {
     c[k + 1] += c[k] >> 26;

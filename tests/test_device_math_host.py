@@ -232,8 +232,8 @@ def test_fe25519_ops(ht):
 
 def test_fe25519_reduction_bounds(ht):
     """The product reduction on the loosest inputs the ladder makes (every limb up to 2^28 - 1): the value is the
-    product mod p, and the output limbs stay within what fe_sub's 2p needs (limb 0 < 2^26 + 19, limbs 1..8 <=
-    2^26, limb 9 <= 2^21)."""
+    product mod p, and the output limbs stay within what fe_sub's 2p needs (limb 0 <= 2^27 - 38, limbs 1..8 <=
+    2^27 - 2, limb 9 <= 2^22 - 2) and small enough that a sum or difference of two stays under 2^28."""
     rnd = random.Random(25519)
     L = ctypes.c_uint32 * 10
     ht.ht_fe_limbs.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
@@ -251,7 +251,8 @@ def test_fe25519_reduction_bounds(ht):
             ht.ht_fe_limbs(op, L(*a), L(*b), out)
             want = val(a) * (val(b) if op == 0 else val(a) if op == 1 else 121665) % P25519
             assert val(out) % P25519 == want, (op, a, b)
-            assert out[0] < (1 << 26) + 19 and all(x <= 1 << 26 for x in out[1:9]) and out[9] <= 1 << 21, list(out)
+            assert out[0] <= (1 << 27) - 38 and all(x <= (1 << 27) - 2 for x in out[1:9]) and out[9] <= (1 << 22) - 2
+            assert max(out) < (1 << 26) + (1 << 17), list(out)
 
 
 def test_x25519_vs_oracle(ht):
