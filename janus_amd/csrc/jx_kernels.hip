@@ -3675,6 +3675,13 @@ __global__ __launch_bounds__(256) void copy_regions_kernel(CopyArgs a) {
       *reinterpret_cast<uint4*>(g.dst + row * g.dst_stride + 16 * ch) =
           *reinterpret_cast<const uint4*>(g.src + row * g.src_stride + 16 * ch);
     }
+  } else if (g.rows == 1 && (((uint64_t)(uintptr_t)g.dst | (uint64_t)(uintptr_t)g.src) & 15) == 0) {
+    // one flat run of a length that is not a multiple of 16 (a launch's verdicts, open statuses): 16-byte vectors
+    // and a byte tail, not one PCIe write per byte
+    const uint64_t nv = g.width / 16;
+    for (uint64_t t = t0; t < nv; t += step)
+      reinterpret_cast<uint4*>(g.dst)[t] = reinterpret_cast<const uint4*>(g.src)[t];
+    if (t0 < g.width - 16 * nv) g.dst[16 * nv + t0] = g.src[16 * nv + t0];
   } else {
     const uint64_t total = g.width * g.rows;
     for (uint64_t t = t0; t < total; t += step) {
@@ -3690,7 +3697,8 @@ hipError_t launch_copy_regions(const CopyArgs& a, hipStream_t s) {
   for (uint32_t k = 0; k < a.nr; k++) {
     const CopyRegion& g = a.r[k];
     const bool vec = ((g.width | g.dst_stride | g.src_stride | (uint64_t)(uintptr_t)g.dst | (uint64_t)(uintptr_t)g.src) & 15) == 0;
-    const uint64_t items = vec ? g.width / 16 * g.rows : g.width * g.rows;
+    const bool flat16 = g.rows == 1 && (((uint64_t)(uintptr_t)g.dst | (uint64_t)(uintptr_t)g.src) & 15) == 0;
+    const uint64_t items = vec ? g.width / 16 * g.rows : flat16 ? g.width / 16 + 16 : g.width * g.rows;
     if (items > most) most = items;
   }
   // PCIe-bound: a few hundred waves keep enough reads in flight, and a big launch's K1 keeps the rest of the
