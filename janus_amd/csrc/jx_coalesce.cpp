@@ -177,6 +177,20 @@ static std::string coal_key(const jx_engine* e) {
 // rejoin window re-measured on the final kernels and host path: 1 ms, against 1.5 / 2 / 3 ms).
 constexpr uint32_t kQuietUs = 100;
 constexpr uint32_t kRejoinUs = 1000;
+// The rejoin window grows to 30 % of the role's launch latency when that is longer than kRejoinUs: callers come
+// back later when the host is busy, e.g. beside a leader role's multi-MB input copies. 32 helper + 32 leader
+// threads of 100-report SumVec jobs on one Prio3 instance (profiles/r06_rejoin_ab.jsonl): helper 183-198k ->
+// 291-320k reports/s, leader 98-99k -> 110-124k, leader jobs per launch 16-20 -> 31 (as many as alone); one role
+// alone unchanged. JX_COAL_REJOIN_FRAC (percent, 0 = the fixed 1 ms) overrides it for A/B.
+static uint32_t rejoin_us(const RoleState& R) {
+  static const uint32_t pct = [] {
+    const char* s = getenv("JX_COAL_REJOIN_FRAC");
+    const int x = s ? atoi(s) : 30;
+    return x >= 0 && x <= 100 ? (uint32_t)x : 30u;
+  }();
+  const double w = R.ewma_us * pct / 100.0;
+  return w > kRejoinUs ? (uint32_t)w : kRejoinUs;
+}
 constexpr uint32_t kMaxRunning = 2;
 // Below flat_reports (the word-per-lane K1's range, 1,024 SumVec reports) a launch takes the same time whatever its
 // size. A gather that opens while a launch of its role runs, and that fits that range together with it, waits for
@@ -615,7 +629,7 @@ static void completer_main(Coalescer* C) {
       R.nrunning--;
       R.run_reports -= L.reports;
       R.expect += (uint32_t)L.reqs.size();  // this launch's callers will be back with their next jobs
-      R.expect_until = now + std::chrono::microseconds(kRejoinUs);
+      R.expect_until = now + std::chrono::microseconds(rejoin_us(R));
       if (R.open >= 0) C->lanes[R.open].all_back = false;  // the gathering lane now expects these callers too
       R.cv.notify_one();  // a gathering lane may close now
       finish_lane(C, L, d.second == hipSuccess ? JX_OK : JX_E_HIP,
